@@ -1,0 +1,98 @@
+import hashlib
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(ROOT, "qwen2-audio-whisper-ggml_amd")
+sys.path.insert(0, PKG)
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+GOLDEN_DIR = os.path.join(ROOT, "tests", "golden")
+TOOL = os.path.join(PKG, "bin", "q2a_tool")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C-ABI library)")
+    config.addinivalue_line("markers", "slow: full-size (L=32, D=1280) model cases")
+
+
+def _sha(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 22), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+@pytest.fixture(scope="session")
+def host_build():
+    subprocess.check_call(["make", "-C", PKG, "host", "-j8"], stdout=subprocess.DEVNULL)
+    subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle"), "oracle"], stdout=subprocess.DEVNULL)
+    return True
+
+
+@pytest.fixture(scope="session")
+def golden():
+    with open(os.path.join(GOLDEN_DIR, "golden.json")) as f:
+        meta = json.load(f)
+    arrays = dict(np.load(os.path.join(GOLDEN_DIR, "golden.npz"), allow_pickle=False))
+    return meta, arrays
+
+
+@pytest.fixture(scope="session")
+def workdir(tmp_path_factory):
+    return str(tmp_path_factory.mktemp("q2a"))
+
+
+@pytest.fixture(scope="session")
+def make_model(host_build, workdir, golden):
+    """make_model(cfg, wt) -> path of a deterministic model file, verified against the golden SHA-256."""
+    meta, _ = golden
+    cache = {}
+
+    def make(cfg, wt):
+        key = (cfg, wt)
+        if key in cache:
+            return cache[key]
+        base = os.path.join(workdir, f"{cfg}-f16.bin")
+        if not os.path.exists(base):
+            subprocess.check_call([TOOL, "gen-model", base, cfg, "f16", "0x51A2", str(min(16, os.cpu_count() or 8))])
+        path = base
+        if wt != "f16":
+            path = os.path.join(workdir, f"{cfg}-{wt}.bin")
+            if not os.path.exists(path):
+                subprocess.check_call([TOOL, "quantize", base, path, wt, str(min(16, os.cpu_count() or 8))])
+        want = meta["models"].get(f"{cfg}-{wt}", {}).get("sha256")
+        if want is not None:
+            assert _sha(path) == want, f"generator/quantizer drift for {cfg}-{wt}"
+        cache[key] = path
+        return path
+
+    return make
+
+
+@pytest.fixture(scope="session")
+def make_clip(host_build, workdir, golden):
+    meta, _ = golden
+
+    def make(c, n=None):
+        info = meta["clips"].get(str(c))
+        n = n if n is not None else info["n_samples"]
+        path = os.path.join(workdir, f"clip{c}_{n}.f32")
+        if not os.path.exists(path):
+            subprocess.check_call([TOOL, "synth-clip", path, str(n), str(c)])
+        if info is not None and info["n_samples"] == n:
+            assert _sha(path) == info["sha256"], f"clip generator drift for clip {c}"
+        return np.fromfile(path, dtype=np.float32)
+
+    return make
+
+
+def rel_errors(out, ref):
+    d = out.astype(np.float64) - ref.astype(np.float64)
+    return float(np.abs(d).max() / np.abs(ref).max()), float(np.linalg.norm(d) / np.linalg.norm(ref))
