@@ -1,0 +1,102 @@
+/*
+ * q2a_encoder.h — C ABI of the MI355X-native Qwen2-Audio encoder hot path (libq2a.so, gfx950).
+ *
+ * This is the drop-in boundary for the reference's hot path: PCM -> log-mel -> Conv1d x2 + GELU -> 32 pre-LN
+ * encoder blocks -> AvgPool1d(2) -> LayerNorm, i.e. what `whisper_full()` computes in the reference
+ * (src/qwen2-whisper.cpp:2341-2383: whisper_encoder_output_with_state -> whisper_pcm_to_mel_with_state +
+ * whisper_encode_qwen2_internal). Plain pointers and sizes only; no torch types.
+ *
+ * The reference-named API (whisper_init_from_file_with_params / whisper_full / whisper_pcm_to_mel /
+ * whisper_print_emb_enc / whisper_free, include/qwen2-whisper.h:141,446,211,527,203) is layered on top of this
+ * in include/q2a_whisper.h and exported from the same library.
+ *
+ * Threading: one q2a_engine per device per host thread (like one whisper_state, include/qwen2-whisper.h:44-45).
+ * Errors: functions return 0 / a non-NULL handle on success; negative q2a_status codes otherwise, with a message
+ * retrievable through q2a_last_error(). No call aborts the process.
+ */
+#ifndef Q2A_ENCODER_H
+#define Q2A_ENCODER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct q2a_engine q2a_engine;
+
+typedef enum {
+    Q2A_OK = 0,
+    Q2A_ERR_IO = -1,           /* model file missing / unreadable */
+    Q2A_ERR_FORMAT = -2,       /* bad magic, bad tensor shapes, unsupported ftype */
+    Q2A_ERR_HIP = -3,          /* HIP runtime error (no device, launch failure, ...) */
+    Q2A_ERR_ARG = -4,          /* invalid argument (sizes, NULL pointers, batch too large) */
+    Q2A_ERR_OOM = -5,          /* device allocation failed */
+    Q2A_ERR_UNSUPPORTED = -6   /* model variant not implemented on this path */
+} q2a_status;
+
+/* per-clip result status written by the encode calls */
+#define Q2A_CLIP_ENCODED 0
+#define Q2A_CLIP_SKIPPED 1   /* < 1 s of audio after the offset: the reference returns 0 without encoding
+                                (qwen2-whisper.cpp:2359-2365); the clip's output rows are left untouched */
+
+typedef struct {
+    int32_t n_audio_ctx, n_audio_state, n_audio_head, n_audio_layer, n_mels;
+    int32_t wtype;          /* ggml type of the linear weights: 1 F16, 12 Q4_K, 8 Q8_0, 2 Q4_0 */
+    int32_t n_out;          /* output vectors per clip (n_audio_ctx / 2 = 750) */
+    int32_t device;
+    int64_t weight_bytes;   /* device bytes of the packed weight blob */
+    int64_t workspace_bytes;
+} q2a_info;
+
+const char * q2a_last_error(void);
+
+/* Load a reference-format ggml model file (models/convert-pt-to-ggml.py layout) onto HIP device `device`. */
+q2a_engine * q2a_open(const char * model_path, int device);
+
+/* Multi-GPU: pack the model into its device layout on the host (rank 0), move the bytes to every rank's device
+ * (e.g. one RCCL broadcast over xGMI), then open an engine on the device copy. The blob is self-describing. */
+int64_t q2a_pack_model(const char * model_path, void ** host_blob);   /* returns size in bytes, < 0 on error */
+void q2a_free_host_blob(void * host_blob);
+q2a_engine * q2a_open_device_blob(const void * device_blob, int64_t size, int device);  /* blob not owned */
+
+void q2a_close(q2a_engine * e);
+int q2a_get_info(const q2a_engine * e, q2a_info * info);
+
+/* Reserve device workspace for up to max_clips clips of up to max_samples samples (optional; grown on demand). */
+int q2a_reserve(q2a_engine * e, int max_clips, int64_t max_samples);
+
+/* Encode n_clips independent clips whose PCM (16 kHz mono f32) is already in device memory:
+ *   pcm_dev    [n_clips][pcm_stride] floats, clip c has n_samples[c] valid samples (host array)
+ *   offset_ms  whisper_full_params.offset_ms (window start = offset_ms / 10 mel frames)
+ *   out_dev    [n_clips][n_out][n_audio_state] f32 (embd_enc of each clip)
+ *   status     host array [n_clips] (Q2A_CLIP_*), may be NULL
+ *   stream     hipStream_t to run on (NULL = the engine's own stream); the call is asynchronous w.r.t. the
+ *              host except for the small per-batch metadata upload, synchronise the stream before reading out_dev.
+ * Audio longer than 30 s is truncated to one 30 s window, as in the reference (qwen2-whisper.cpp:2366-2372). */
+int q2a_encode_device(q2a_engine * e, const float * pcm_dev, int64_t pcm_stride, const int32_t * n_samples,
+                      int n_clips, int offset_ms, float * out_dev, int32_t * status, void * stream);
+
+/* Same with host buffers in and out (PCIe transfers included; synchronous). out_host [n_clips][n_out][D]. */
+int q2a_encode_host(q2a_engine * e, const float * const * pcm, const int32_t * n_samples, int n_clips,
+                    int offset_ms, float * out_host, int32_t * status);
+
+/* log-mel of one clip (whisper_pcm_to_mel semantics): writes [n_mels][n_len] into mel_out (capacity
+ * mel_cap floats) and *n_len. Runs the same kernels as the encoder on the engine's device. */
+int q2a_pcm_to_mel(q2a_engine * e, const float * pcm, int n_samples, float * mel_out, int64_t mel_cap, int * n_len);
+
+/* ---- kernel-level entry points (device pointers), used by the parity tests ------------------------------ */
+/* Y[M][N] = X[M][K] . W[N][K]^T for one linear weight of the loaded model (layer `layer`, which = 0 qkv
+ * (raw, no bias/scale), 1 out_proj, 2 fc1, 3 fc2), with ggml's activation conversion of X (fp16 / Q8_K / Q8_0). */
+int q2a_test_linear(q2a_engine * e, int layer, int which, const float * x_dev, int M, float * y_dev, void * stream);
+/* One encoder block in place on X [n_clips*T][D] (f32, device). */
+int q2a_test_block(q2a_engine * e, int layer, float * x_dev, int n_clips, void * stream);
+/* Attention only: q,k,v [n_clips*T][D] f32 (q already scaled), out [n_clips*T][D] f32. */
+int q2a_test_attention(q2a_engine * e, const float * q_dev, const float * k_dev, const float * v_dev, int n_clips,
+                       float * out_dev, void * stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* Q2A_ENCODER_H */

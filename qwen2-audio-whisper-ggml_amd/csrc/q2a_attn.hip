@@ -1,0 +1,188 @@
+// q2a_attn.hip — fused multi-head self-attention for gfx950 (flash-style, no T x T score tensor in HBM).
+//
+// Replaces, per layer (qwen2-whisper.cpp:2052-2107): KQ = mul_mat(K, Q) (F32, ggml.c:12439), SOFT_MAX
+// (ggml.c:13854-13950, scale 1, no mask), KQV = mul_mat(cont(V^T), KQ_soft_max), the permutes and the merge.
+// The reference materialises 20 x 1500 x 1500 F32 scores per layer (180 MB per clip).
+//
+// Numerics: the reference computes QK^T in F32. Here Q and K arrive as fp16 hi/lo pairs (x = hi + lo, 22
+// significant bits) and S = Kh.Qh + Kl.Qh + Kh.Ql on fp16 MFMA with fp32 accumulation (the lo.lo term is below
+// 2^-22 relative), i.e. F32-class scores. P (in [0,1]) and V are fp16 for the P.V product. Online softmax keeps
+// a running max/sum per query; the 1/sum normalisation is applied once at the end.
+//
+// Structure: one 256-thread workgroup = 4 waves x 32 queries of one (clip, head); K/V tiles of 64 keys are
+// register-staged into double-buffered LDS images (rows padded to 144 B / 136 B: conflict-free ds_read_b128 /
+// ds_read_b64 for 32 distinct rows). S^T = K.Q^T is computed with v_mfma_f32_32x32x16_f16 so each lane owns one
+// query column (softmax is lane-local plus one lane^32 exchange) and the S accumulator feeds the P.V MFMA as
+// its B operand with no data movement (cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand").
+#include "q2a_internal.h"
+
+namespace {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef float f16v __attribute__((ext_vector_type(16)));
+
+constexpr int KT = 64;            // keys per LDS tile
+constexpr int KROW = 144;         // bytes per K image row (64 halves + 16 B pad)
+constexpr int VROW = 136;         // bytes per V^T image row (64 halves + 8 B pad)
+constexpr int KIMG = KT * KROW;   // 9216
+constexpr int VIMG = 64 * VROW;   // 8704
+constexpr int STAGE = 2 * KIMG + VIMG;
+
+__global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
+    __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int h = blockIdx.y, clip = blockIdx.z;
+    const int T = p.T, D = p.D;
+    const int q0 = blockIdx.x * 128 + wave * 32;
+    const int64_t rowbase = (int64_t) clip * T;
+    const int hi = lane >> 5, col = lane & 31;
+
+    // Q fragments (B operand of S^T = K.Q^T): lane holds Q[q0+col][16s + 8hi .. +7]
+    half8 qh[4], ql[4];
+    {
+        const int q = min(q0 + col, T - 1);
+        const q2a_half * sh = p.qh + (rowbase + q) * D + h * 64 + 8 * hi;
+        const q2a_half * sl = p.ql + (rowbase + q) * D + h * 64 + 8 * hi;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            qh[s] = *(const half8 *) (sh + 16 * s);
+            ql[s] = *(const half8 *) (sl + 16 * s);
+        }
+    }
+
+    // staging: each thread moves 2 x 16 B of Kh, of Kl and of V^T per tile
+    const q2a_half * vt_base = p.vt + ((int64_t) clip * p.H + h) * 64 * p.TP;
+    uint4 rk_h[2], rk_l[2], rv[2];
+    auto load_tile = [&](int t) {
+        const int kb0 = t * KT;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int c = tid + u * 256, r = c >> 3, ch = c & 7;
+            const int key = min(kb0 + r, T - 1);
+            rk_h[u] = *(const uint4 *) (p.kh + (rowbase + key) * D + h * 64 + ch * 8);
+            rk_l[u] = *(const uint4 *) (p.kl + (rowbase + key) * D + h * 64 + ch * 8);
+            rv[u] = *(const uint4 *) (vt_base + (int64_t) r * p.TP + kb0 + ch * 8);
+        }
+    };
+    auto store_tile = [&](int buf) {
+        char * st = lds + buf * STAGE;
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+            const int c = tid + u * 256, r = c >> 3, ch = c & 7;
+            *(uint4 *) (st + r * KROW + ch * 16) = rk_h[u];
+            *(uint4 *) (st + KIMG + r * KROW + ch * 16) = rk_l[u];
+            uint2 * v = (uint2 *) (st + 2 * KIMG + r * VROW + ch * 16);
+            v[0] = make_uint2(rv[u].x, rv[u].y);
+            v[1] = make_uint2(rv[u].z, rv[u].w);
+        }
+    };
+
+    f16v o[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+    float m_run = -1e30f, l_run = 0.f;
+
+    const int ntiles = (T + KT - 1) / KT;
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+
+    for (int t = 0; t < ntiles; ++t) {
+        const int cur = t & 1;
+        if (t + 1 < ntiles) load_tile(t + 1);
+        const char * kh_img = lds + cur * STAGE;
+        const char * kl_img = kh_img + KIMG;
+        const char * vt_img = kh_img + 2 * KIMG;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+            f16v s;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) s[r] = 0.f;
+            const int krow = kb * 32 + col;
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                const int off = krow * KROW + (2 * st + hi) * 16;
+                const half8 ah = *(const half8 *) (kh_img + off);
+                const half8 al = *(const half8 *) (kl_img + off);
+                s = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, qh[st], s, 0, 0, 0);
+                s = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, qh[st], s, 0, 0, 0);
+                s = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ql[st], s, 0, 0, 0);
+            }
+            // mask keys >= T (row of reg r = (r&3) + 8(r>>2) + 4hi)
+            const int key0 = t * KT + kb * 32;
+            float mx = -1e30f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
+                if (key >= T) s[r] = -1e30f;
+                mx = fmaxf(mx, s[r]);
+            }
+            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            const float m_new = fmaxf(m_run, mx);
+            const float alpha = __expf(m_run - m_new);
+            float ls = 0.f;
+            half8 pf[2];
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float pv = __expf(s[r] - m_new);
+                ls += pv;
+                pf[r >> 3][r & 7] = (_Float16) pv;
+            }
+            l_run = l_run * alpha + ls;
+            m_run = m_new;
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+            // O^T[d][q] += V^T[d][keys] . P^T[keys][q]
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt) {
+                const char * vrow = vt_img + (dt * 32 + col) * VROW;
+#pragma unroll
+                for (int sp = 0; sp < 2; ++sp) {
+                    const int kbyte = 2 * (kb * 32 + 16 * sp + 4 * hi);
+                    const half4 v0 = *(const half4 *) (vrow + kbyte);
+                    const half4 v1 = *(const half4 *) (vrow + kbyte + 16);
+                    const half8 va = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, pf[sp], o[dt], 0, 0, 0);
+                }
+            }
+        }
+        // buffer cur^1 was last read in iteration t-1, before the barrier that ended it
+        if (t + 1 < ntiles) store_tile(cur ^ 1);
+        __syncthreads();
+    }
+
+    const float l_tot = l_run + __shfl_xor(l_run, 32);
+    const float inv = 1.0f / l_tot;
+    const int q = q0 + col;
+    if (q < T) {
+        const int64_t orow = (rowbase + q) * D + h * 64;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d = dt * 32 + 8 * g + 4 * hi;
+                const float v0 = o[dt][4 * g + 0] * inv, v1 = o[dt][4 * g + 1] * inv;
+                const float v2 = o[dt][4 * g + 2] * inv, v3 = o[dt][4 * g + 3] * inv;
+                if (p.outH) {
+                    const half4 hv = {(_Float16) v0, (_Float16) v1, (_Float16) v2, (_Float16) v3};
+                    *(half4 *) (p.outH + orow + d) = hv;
+                } else {
+                    *(float4 *) (p.outF + orow + d) = make_float4(v0, v1, v2, v3);
+                }
+            }
+    }
+}
+
+}  // namespace
+
+hipError_t q2a_launch_attention(const q2a_attn_args & a, hipStream_t s) {
+    if (a.D != a.H * 64 || a.TP < ((a.T + KT - 1) / KT) * KT) return hipErrorInvalidValue;
+    dim3 grid((a.T + 127) / 128, a.H, a.n_clips);
+    hipLaunchKernelGGL(k_attn, grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}

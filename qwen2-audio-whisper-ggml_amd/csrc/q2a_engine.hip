@@ -1,0 +1,866 @@
+// q2a_engine.hip — host orchestration of the MI355X encoder path behind the C ABI (include/q2a_encoder.h).
+//
+// Replaces whisper_full -> whisper_encoder_output_with_state (src/qwen2-whisper.cpp:2341-2383):
+// log_mel_spectrogram (:2575) + whisper_encode_qwen2_internal (:2241) with its conv graph (:1892) and encoder
+// graph (:1954), for a BATCH of independent clips in one pass. No ggml graph build / sched split / allocator at
+// run time: the model is packed once into a device blob and every intermediate lives in a workspace reserved
+// for the batch size, so a batch is ~11 launches per layer on one stream (capturable into a hipGraph).
+#include "q2a_encoder.h"
+#include "q2a_format.h"
+#include "q2a_internal.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cerrno>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+void set_err(const char * fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+}
+
+#define HIP_TRY(x)                                                                        \
+    do {                                                                                  \
+        hipError_t e_ = (x);                                                              \
+        if (e_ != hipSuccess) {                                                           \
+            set_err("%s failed: %s (%s:%d)", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+            return Q2A_ERR_HIP;                                                           \
+        }                                                                                 \
+    } while (0)
+
+// ------------------------------------------------------------------------------------------------
+// packed device blob: 16 KiB self-describing header + 256-B aligned sections
+// ------------------------------------------------------------------------------------------------
+constexpr uint32_t BLOB_MAGIC = 0x42413251u;   // "Q2AB"
+constexpr uint32_t BLOB_VERSION = 1;
+constexpr int MAX_LAYERS = 64;
+constexpr size_t HEADER_BYTES = 16384;
+
+enum { G_CONV1_W, G_CONV1_B, G_CONV2_W, G_CONV2_B, G_PE, G_LNP_W, G_LNP_B, G_FILT, G_TAB, G_GELU, G_COUNT };
+// per-matrix arrays: W (fp16 [N][K]), DX (f32 [N][nblk]), DMIN (f32 [N][nblk]), WEXT (fp16 [N][nblk][16])
+enum { A_W, A_DX, A_DMIN, A_WEXT, A_COUNT };
+enum { L_BQKV, L_BO, L_B1, L_B2, L_LN1W, L_LN1B, L_LN2W, L_LN2B, L_MAT0, L_COUNT = L_MAT0 + 4 * A_COUNT };
+
+struct blob_header {
+    uint32_t magic, version;
+    q2a_hparams hp;
+    int32_t wtype, blk, n_bins, reserved;
+    uint64_t total;
+    uint64_t goff[G_COUNT];
+    uint64_t loff[MAX_LAYERS][L_COUNT];
+};
+static_assert(sizeof(blob_header) <= HEADER_BYTES, "header too large");
+
+struct dims {
+    int T, D, H, L, M, F, TM, TO;
+};
+dims dims_of(const q2a_hparams & hp) {
+    dims d;
+    d.T = hp.n_audio_ctx; d.D = hp.n_audio_state; d.H = hp.n_audio_head; d.L = hp.n_audio_layer; d.M = hp.n_mels;
+    d.F = 4 * d.D; d.TM = 2 * d.T; d.TO = d.T / 2;
+    return d;
+}
+void mat_dims(const dims & d, int which, int & N, int & K) {
+    switch (which) {
+        case 0: N = 3 * d.D; K = d.D; break;
+        case 1: N = d.D; K = d.D; break;
+        case 2: N = d.F; K = d.D; break;
+        default: N = d.D; K = d.F; break;
+    }
+}
+int blk_of(int wtype) { return wtype == Q2A_TYPE_Q4_K ? 256 : (wtype == Q2A_TYPE_Q8_0 || wtype == Q2A_TYPE_Q4_0) ? 32 : 0; }
+
+bool plan(blob_header & h, const q2a_hparams & hp, int wtype) {
+    memset(&h, 0, sizeof(h));
+    h.magic = BLOB_MAGIC; h.version = BLOB_VERSION; h.hp = hp; h.wtype = wtype; h.blk = blk_of(wtype); h.n_bins = 201;
+    const dims d = dims_of(hp);
+    if (d.L > MAX_LAYERS) return false;
+    uint64_t off = HEADER_BYTES;
+    auto take = [&](uint64_t bytes) { const uint64_t o = off; off += (bytes + 255) & ~uint64_t(255); return o; };
+    h.goff[G_CONV1_W] = take((uint64_t) d.D * 6 * d.M * 2);
+    h.goff[G_CONV1_B] = take((uint64_t) d.D * 4);
+    h.goff[G_CONV2_W] = take((uint64_t) d.D * 3 * d.D * 2);
+    h.goff[G_CONV2_B] = take((uint64_t) d.D * 4);
+    h.goff[G_PE] = take((uint64_t) d.T * d.D * 4);
+    h.goff[G_LNP_W] = take((uint64_t) d.D * 4);
+    h.goff[G_LNP_B] = take((uint64_t) d.D * 4);
+    h.goff[G_FILT] = take((uint64_t) d.M * 201 * 4);
+    h.goff[G_TAB] = take(1200 * 4);
+    h.goff[G_GELU] = take(65536 * 2);
+    for (int l = 0; l < d.L; ++l) {
+        uint64_t * lo = h.loff[l];
+        lo[L_BQKV] = take((uint64_t) 3 * d.D * 4);
+        lo[L_BO] = take((uint64_t) d.D * 4);
+        lo[L_B1] = take((uint64_t) d.F * 4);
+        lo[L_B2] = take((uint64_t) d.D * 4);
+        lo[L_LN1W] = take((uint64_t) d.D * 4);
+        lo[L_LN1B] = take((uint64_t) d.D * 4);
+        lo[L_LN2W] = take((uint64_t) d.D * 4);
+        lo[L_LN2B] = take((uint64_t) d.D * 4);
+        for (int w = 0; w < 4; ++w) {
+            int N, K;
+            mat_dims(d, w, N, K);
+            uint64_t * a = lo + L_MAT0 + w * A_COUNT;
+            a[A_W] = take((uint64_t) N * K * 2);
+            if (h.blk) a[A_DX] = take((uint64_t) N * (K / h.blk) * 4);
+            if (h.blk == 256) {
+                a[A_DMIN] = take((uint64_t) N * (K / 256) * 4);
+                a[A_WEXT] = take((uint64_t) N * (K / 256) * 16 * 2);
+            }
+        }
+    }
+    h.total = off;
+    return true;
+}
+
+inline void scale_min_k4(int j, const uint8_t * q, uint8_t * dd, uint8_t * mm) {   // ggml-quants.c:1898
+    if (j < 4) { *dd = q[j] & 63; *mm = q[j + 4] & 63; }
+    else {
+        *dd = (uint8_t) ((q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4));
+        *mm = (uint8_t) ((q[j + 4] >> 4) | ((q[j - 0] >> 6) << 4));
+    }
+}
+
+// Expand rows [r0, r1) of a ggml weight matrix into the blob arrays (rows offset by dst_row0).
+// F16: copied. Q4_K: W' = sc_j * q (exact small integers), DX = d, DMIN = dmin, WEXT = (64 m_j, m_j).
+// Q8_0: W' = q, DX = d. Q4_0: W' = q - 8, DX = d.
+void expand_rows(const uint8_t * src, int wtype, int K, int r0, int r1, uint8_t * blob, const uint64_t * a, int dst_row0) {
+    uint16_t * W = (uint16_t *) (blob + a[A_W]);
+    const size_t rs = q2a_row_size(wtype, K);
+    for (int r = r0; r < r1; ++r) {
+        const uint8_t * row = src + (size_t) r * rs;
+        const int n = dst_row0 + r;
+        uint16_t * wr = W + (size_t) n * K;
+        if (wtype == Q2A_TYPE_F16) {
+            memcpy(wr, row, (size_t) K * 2);
+        } else if (wtype == Q2A_TYPE_Q4_K) {
+            const int nb = K / 256;
+            float * dx = (float *) (blob + a[A_DX]) + (size_t) n * nb;
+            float * dm = (float *) (blob + a[A_DMIN]) + (size_t) n * nb;
+            uint16_t * we = (uint16_t *) (blob + a[A_WEXT]) + (size_t) n * nb * 16;
+            for (int b = 0; b < nb; ++b) {
+                const q2a_block_q4_K * x = (const q2a_block_q4_K *) row + b;
+                dx[b] = q2a_fp16_to_fp32(x->d);
+                dm[b] = q2a_fp16_to_fp32(x->dmin);
+                for (int j = 0; j < 8; ++j) {
+                    uint8_t sc, m;
+                    scale_min_k4(j, x->scales, &sc, &m);
+                    we[b * 16 + 2 * j + 0] = q2a_fp32_to_fp16(64.0f * m);
+                    we[b * 16 + 2 * j + 1] = q2a_fp32_to_fp16((float) m);
+                    const uint8_t * q = x->qs + 32 * (j / 2);
+                    for (int l = 0; l < 32; ++l) {
+                        const int v = (j & 1) ? (q[l] >> 4) : (q[l] & 0xF);
+                        wr[b * 256 + 32 * j + l] = q2a_fp32_to_fp16((float) (sc * v));
+                    }
+                }
+            }
+        } else if (wtype == Q2A_TYPE_Q8_0) {
+            const int nb = K / 32;
+            float * dx = (float *) (blob + a[A_DX]) + (size_t) n * nb;
+            for (int b = 0; b < nb; ++b) {
+                const q2a_block_q8_0 * x = (const q2a_block_q8_0 *) row + b;
+                dx[b] = q2a_fp16_to_fp32(x->d);
+                for (int l = 0; l < 32; ++l) wr[b * 32 + l] = q2a_fp32_to_fp16((float) x->qs[l]);
+            }
+        } else if (wtype == Q2A_TYPE_Q4_0) {
+            const int nb = K / 32;
+            float * dx = (float *) (blob + a[A_DX]) + (size_t) n * nb;
+            for (int b = 0; b < nb; ++b) {
+                const q2a_block_q4_0 * x = (const q2a_block_q4_0 *) row + b;
+                dx[b] = q2a_fp16_to_fp32(x->d);
+                for (int l = 0; l < 16; ++l) {
+                    wr[b * 32 + l] = q2a_fp32_to_fp16((float) ((x->qs[l] & 0xF) - 8));
+                    wr[b * 32 + 16 + l] = q2a_fp32_to_fp16((float) ((x->qs[l] >> 4) - 8));
+                }
+            }
+        }
+    }
+}
+
+int pack(const char * path, std::vector<uint8_t> & out) {
+    char err[256];
+    q2a_model_file * mf = q2a_model_file_read(path, err, sizeof(err));
+    if (!mf) { set_err("%s", err); return errno == ENOENT ? Q2A_ERR_IO : Q2A_ERR_FORMAT; }
+    struct guard { q2a_model_file * m; ~guard() { q2a_model_file_free(m); } } gd{mf};
+    const q2a_hparams & hp = mf->hp;
+    const int wtype = mf->wtype;
+    if (wtype == Q2A_TYPE_F32) { set_err("all-F32 model files (ftype 0) are not supported on this path yet"); return Q2A_ERR_UNSUPPORTED; }
+    const dims d = dims_of(hp);
+    if (d.D % 128 || d.D != d.H * 64 || d.T % 2 || d.M % 4 || (blk_of(wtype) == 256 && d.D % 256)) {
+        set_err("unsupported shapes: D=%d H=%d T=%d M=%d", d.D, d.H, d.T, d.M);
+        return Q2A_ERR_UNSUPPORTED;
+    }
+    if (mf->n_mel_filt != d.M || mf->n_fft_filt != 201) { set_err("bad mel filter shape"); return Q2A_ERR_FORMAT; }
+    blob_header h;
+    if (!plan(h, hp, wtype)) { set_err("too many layers"); return Q2A_ERR_UNSUPPORTED; }
+    out.assign(h.total, 0);
+    uint8_t * blob = out.data();
+    memcpy(blob, &h, sizeof(h));
+
+    auto T = [&](const std::string & name, int type, std::initializer_list<int64_t> ne) -> const uint8_t * {
+        const q2a_tensor_desc * t = q2a_model_file_find(mf, name.c_str());
+        if (!t) { set_err("tensor '%s' missing from model file", name.c_str()); return nullptr; }
+        if (type >= 0 && t->type != type) { set_err("tensor '%s' has type %d, expected %d", name.c_str(), t->type, type); return nullptr; }
+        int i = 0;
+        for (int64_t v : ne) {
+            if (t->ne[i] != v) { set_err("tensor '%s' has wrong shape", name.c_str()); return nullptr; }
+            ++i;
+        }
+        return mf->data + t->offset;
+    };
+    auto cpy = [&](uint64_t off, const uint8_t * src, size_t n) { memcpy(blob + off, src, n); };
+
+    // conv1: [oc][ic][k] F16 -> [oc][k*2M + (0|M) + ic] (k-major, duplicated for the hi|lo operand halves)
+    const uint8_t * c1 = T("conv1.weight", Q2A_TYPE_F16, {3, d.M, d.D});
+    const uint8_t * c1b = T("conv1.bias", Q2A_TYPE_F32, {1, d.D});
+    const uint8_t * c2 = T("conv2.weight", Q2A_TYPE_F16, {3, d.D, d.D});
+    const uint8_t * c2b = T("conv2.bias", Q2A_TYPE_F32, {1, d.D});
+    const uint8_t * pe = T("embed_positions.weight", Q2A_TYPE_F32, {d.D, d.T});
+    const uint8_t * lnw = T("layer_norm.weight", Q2A_TYPE_F32, {d.D});
+    const uint8_t * lnb = T("layer_norm.bias", Q2A_TYPE_F32, {d.D});
+    if (!c1 || !c1b || !c2 || !c2b || !pe || !lnw || !lnb) return Q2A_ERR_FORMAT;
+    {
+        const uint16_t * s = (const uint16_t *) c1;
+        uint16_t * w = (uint16_t *) (blob + h.goff[G_CONV1_W]);
+        for (int oc = 0; oc < d.D; ++oc)
+            for (int ic = 0; ic < d.M; ++ic)
+                for (int k = 0; k < 3; ++k) {
+                    const uint16_t v = s[((size_t) oc * d.M + ic) * 3 + k];
+                    w[(size_t) oc * 6 * d.M + k * 2 * d.M + ic] = v;
+                    w[(size_t) oc * 6 * d.M + k * 2 * d.M + d.M + ic] = v;
+                }
+        const uint16_t * s2 = (const uint16_t *) c2;
+        uint16_t * w2 = (uint16_t *) (blob + h.goff[G_CONV2_W]);
+        for (int oc = 0; oc < d.D; ++oc)
+            for (int ic = 0; ic < d.D; ++ic)
+                for (int k = 0; k < 3; ++k) w2[(size_t) oc * 3 * d.D + k * d.D + ic] = s2[((size_t) oc * d.D + ic) * 3 + k];
+    }
+    cpy(h.goff[G_CONV1_B], c1b, (size_t) d.D * 4);
+    cpy(h.goff[G_CONV2_B], c2b, (size_t) d.D * 4);
+    cpy(h.goff[G_PE], pe, (size_t) d.T * d.D * 4);
+    cpy(h.goff[G_LNP_W], lnw, (size_t) d.D * 4);
+    cpy(h.goff[G_LNP_B], lnb, (size_t) d.D * 4);
+    cpy(h.goff[G_FILT], (const uint8_t *) mf->filters, (size_t) d.M * 201 * 4);
+    q2a_make_mel_tables((float *) (blob + h.goff[G_TAB]));
+    q2a_make_gelu_table((uint16_t *) (blob + h.goff[G_GELU]));
+
+    struct job { const uint8_t * src; int K, r0, r1; const uint64_t * a; int dst0; };
+    std::vector<job> jobs;
+    for (int l = 0; l < d.L; ++l) {
+        const std::string p = "layers." + std::to_string(l) + ".";
+        const uint64_t * lo = h.loff[l];
+        const uint8_t * wq = T(p + "self_attn.q_proj.weight", wtype, {d.D, d.D});
+        const uint8_t * bq = T(p + "self_attn.q_proj.bias", Q2A_TYPE_F32, {d.D});
+        const uint8_t * wk = T(p + "self_attn.k_proj.weight", wtype, {d.D, d.D});
+        const uint8_t * wv = T(p + "self_attn.v_proj.weight", wtype, {d.D, d.D});
+        const uint8_t * bv = T(p + "self_attn.v_proj.bias", Q2A_TYPE_F32, {d.D});
+        const uint8_t * wo = T(p + "self_attn.out_proj.weight", wtype, {d.D, d.D});
+        const uint8_t * bo = T(p + "self_attn.out_proj.bias", Q2A_TYPE_F32, {d.D});
+        const uint8_t * l1w = T(p + "self_attn_layer_norm.weight", Q2A_TYPE_F32, {d.D});
+        const uint8_t * l1b = T(p + "self_attn_layer_norm.bias", Q2A_TYPE_F32, {d.D});
+        const uint8_t * w1 = T(p + "fc1.weight", wtype, {d.D, d.F});
+        const uint8_t * b1 = T(p + "fc1.bias", Q2A_TYPE_F32, {d.F});
+        const uint8_t * w2 = T(p + "fc2.weight", wtype, {d.F, d.D});
+        const uint8_t * b2 = T(p + "fc2.bias", Q2A_TYPE_F32, {d.D});
+        const uint8_t * l2w = T(p + "final_layer_norm.weight", Q2A_TYPE_F32, {d.D});
+        const uint8_t * l2b = T(p + "final_layer_norm.bias", Q2A_TYPE_F32, {d.D});
+        if (!wq || !bq || !wk || !wv || !bv || !wo || !bo || !l1w || !l1b || !w1 || !b1 || !w2 || !b2 || !l2w || !l2b)
+            return Q2A_ERR_FORMAT;
+        float * bqkv = (float *) (blob + lo[L_BQKV]);
+        memcpy(bqkv, bq, (size_t) d.D * 4);                 // q bias; k has no bias (qwen2-whisper.cpp:2037)
+        memcpy(bqkv + 2 * d.D, bv, (size_t) d.D * 4);
+        cpy(lo[L_BO], bo, (size_t) d.D * 4);
+        cpy(lo[L_B1], b1, (size_t) d.F * 4);
+        cpy(lo[L_B2], b2, (size_t) d.D * 4);
+        cpy(lo[L_LN1W], l1w, (size_t) d.D * 4);
+        cpy(lo[L_LN1B], l1b, (size_t) d.D * 4);
+        cpy(lo[L_LN2W], l2w, (size_t) d.D * 4);
+        cpy(lo[L_LN2B], l2b, (size_t) d.D * 4);
+        const uint64_t * a0 = lo + L_MAT0;
+        jobs.push_back({wq, d.D, 0, d.D, a0, 0});
+        jobs.push_back({wk, d.D, 0, d.D, a0, d.D});
+        jobs.push_back({wv, d.D, 0, d.D, a0, 2 * d.D});
+        jobs.push_back({wo, d.D, 0, d.D, lo + L_MAT0 + A_COUNT, 0});
+        jobs.push_back({w1, d.D, 0, d.F, lo + L_MAT0 + 2 * A_COUNT, 0});
+        jobs.push_back({w2, d.F, 0, d.D, lo + L_MAT0 + 3 * A_COUNT, 0});
+    }
+    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t]() {
+            for (const job & j : jobs) {
+                const int n = j.r1 - j.r0;
+                expand_rows(j.src, wtype, j.K, j.r0 + n * t / nt, j.r0 + n * (t + 1) / nt, blob, j.a, j.dst0);
+            }
+        });
+    for (auto & x : th) x.join();
+    return Q2A_OK;
+}
+
+__global__ void k_split_hilo(const float * x, q2a_half * hi, q2a_half * lo, int64_t n) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float v = x[i];
+    const _Float16 h = (_Float16) v;
+    hi[i] = h;
+    lo[i] = (_Float16) (v - (float) h);
+}
+
+__global__ void k_to_vt(const float * v, q2a_half * vt, int clips, int T, int H, int TP) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t D = (int64_t) H * 64;
+    if (i >= (int64_t) clips * T * D) return;
+    const int64_t m = i / D;
+    const int c = (int) (i % D);
+    const int clip = (int) (m / T), t = (int) (m % T);
+    vt[(((int64_t) clip * H + c / 64) * 64 + (c % 64)) * TP + t] = (_Float16) v[i];
+}
+
+__global__ void k_to_half(const float * x, q2a_half * y, int64_t n) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = (_Float16) x[i];
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// engine
+// ------------------------------------------------------------------------------------------------
+struct q2a_engine {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    blob_header h;
+    dims d;
+    int wtype = 0, blk = 0;
+    uint8_t * blob = nullptr;
+    bool own_blob = false;
+    int64_t blob_size = 0;
+
+    // workspace (capacity)
+    int cap_clips = 0;
+    int64_t cap_samples = 0;
+    void * ws = nullptr;
+    size_t ws_bytes = 0;
+    float * pcm_stage = nullptr;     // host-API staging [cap][cap_samples]
+    float * out_stage = nullptr;     // unused (outputs are written straight to the user buffer)
+    int32_t * meta = nullptr;        // device: nsamp | seek | clip_ok | clip_max
+    int32_t * meta_host = nullptr;   // pinned
+    float * mel = nullptr;
+    q2a_half * xc1 = nullptr;
+    q2a_half * y1 = nullptr;
+    float * X = nullptr;
+    q2a_half * actD = nullptr;
+    q2a_half * actF = nullptr;
+    float * dyD = nullptr;
+    float * dyF = nullptr;
+    q2a_half * aextD = nullptr;
+    q2a_half * aextF = nullptr;
+    q2a_half *qh = nullptr, *ql = nullptr, *kh = nullptr, *kl = nullptr, *vt = nullptr;
+    float * attF = nullptr;
+    float * hF = nullptr;
+    int TP = 0;
+
+    template <class P> P g(int i) const { return (P) (blob + h.goff[i]); }
+    template <class P> P lv(int l, int i) const { return (P) (blob + h.loff[l][i]); }
+    const uint64_t * mat(int l, int w) const { return h.loff[l] + L_MAT0 + w * A_COUNT; }
+};
+
+namespace {
+
+int engine_init(q2a_engine * e, int device) {
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) { set_err("device %d not available (%d devices)", device, n); return Q2A_ERR_HIP; }
+    e->device = device;
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    return Q2A_OK;
+}
+
+int engine_adopt_header(q2a_engine * e) {
+    if (e->h.magic != BLOB_MAGIC || e->h.version != BLOB_VERSION) { set_err("not a q2a weight blob"); return Q2A_ERR_FORMAT; }
+    e->d = dims_of(e->h.hp);
+    e->wtype = e->h.wtype;
+    e->blk = e->h.blk;
+    e->TP = ((e->d.T + 63) / 64) * 64;
+    return Q2A_OK;
+}
+
+void free_ws(q2a_engine * e) {
+    if (e->ws) (void) hipFree(e->ws);
+    if (e->meta_host) (void) hipHostFree(e->meta_host);
+    if (e->pcm_stage) (void) hipFree(e->pcm_stage);
+    e->ws = nullptr; e->meta_host = nullptr; e->pcm_stage = nullptr;
+    e->cap_clips = 0; e->ws_bytes = 0;
+}
+
+int reserve(q2a_engine * e, int B) {
+    if (B <= e->cap_clips) return Q2A_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    if (e->ws) { (void) hipFree(e->ws); e->ws = nullptr; }
+    if (e->meta_host) { (void) hipHostFree(e->meta_host); e->meta_host = nullptr; }
+    const dims & d = e->d;
+    const int64_t BT = (int64_t) B * d.T;
+    const bool quant = e->blk != 0;
+    size_t off = 0;
+    auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
+    const size_t o_meta = take((size_t) B * 4 * 4);
+    const size_t o_mel = take((size_t) B * d.M * d.TM * 4);
+    const size_t o_xc1 = take((size_t) B * (d.TM + 2) * 2 * d.M * 2);
+    const size_t o_y1 = take((size_t) B * (d.TM + 1) * d.D * 2);
+    const size_t o_X = take((size_t) BT * d.D * 4);
+    const size_t o_actD = take((size_t) BT * d.D * 2);
+    const size_t o_actF = take((size_t) BT * d.F * 2);
+    const size_t o_qh = take((size_t) BT * d.D * 2);
+    const size_t o_ql = take((size_t) BT * d.D * 2);
+    const size_t o_kh = take((size_t) BT * d.D * 2);
+    const size_t o_kl = take((size_t) BT * d.D * 2);
+    const size_t o_vt = take((size_t) B * d.H * 64 * e->TP * 2);
+    size_t o_dyD = 0, o_dyF = 0, o_aD = 0, o_aF = 0, o_att = 0, o_hF = 0;
+    if (quant) {
+        o_dyD = take((size_t) BT * (d.D / 32) * 4);
+        o_dyF = take((size_t) BT * (d.F / 32) * 4);
+        o_aD = take((size_t) BT * (d.D / 256 + 1) * 16 * 2);
+        o_aF = take((size_t) BT * (d.F / 256 + 1) * 16 * 2);
+        o_att = take((size_t) BT * d.D * 4);
+        o_hF = take((size_t) BT * d.F * 4);
+    }
+    void * ws = nullptr;
+    if (hipMalloc(&ws, off) != hipSuccess) {
+        (void) hipGetLastError();
+        set_err("workspace allocation of %.2f GB for %d clips failed", off / 1e9, B);
+        return Q2A_ERR_OOM;
+    }
+    HIP_TRY(hipMemsetAsync(ws, 0, off, e->stream));   // zero pad rows (xc1 rows 0/last, y1 row 0, V^T tail)
+    HIP_TRY(hipHostMalloc((void **) &e->meta_host, (size_t) B * 4 * 4, hipHostMallocDefault));
+    uint8_t * b = (uint8_t *) ws;
+    e->ws = ws; e->ws_bytes = off; e->cap_clips = B;
+    e->meta = (int32_t *) (b + o_meta);
+    e->mel = (float *) (b + o_mel);
+    e->xc1 = (q2a_half *) (b + o_xc1);
+    e->y1 = (q2a_half *) (b + o_y1);
+    e->X = (float *) (b + o_X);
+    e->actD = (q2a_half *) (b + o_actD);
+    e->actF = (q2a_half *) (b + o_actF);
+    e->qh = (q2a_half *) (b + o_qh); e->ql = (q2a_half *) (b + o_ql);
+    e->kh = (q2a_half *) (b + o_kh); e->kl = (q2a_half *) (b + o_kl);
+    e->vt = (q2a_half *) (b + o_vt);
+    if (quant) {
+        e->dyD = (float *) (b + o_dyD); e->dyF = (float *) (b + o_dyF);
+        e->aextD = (q2a_half *) (b + o_aD); e->aextF = (q2a_half *) (b + o_aF);
+        e->attF = (float *) (b + o_att); e->hF = (float *) (b + o_hF);
+    }
+    HIP_TRY(hipStreamSynchronize(e->stream));
+    return Q2A_OK;
+}
+
+q2a_gemm_args gemm_base(const q2a_engine * e, int l, int which, const q2a_half * A, int M) {
+    q2a_gemm_args a;
+    memset(&a, 0, sizeof(a));
+    int N, K;
+    mat_dims(e->d, which, N, K);
+    const uint64_t * m = e->mat(l, which);
+    a.A = A; a.lda = K; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
+    a.W = (const q2a_half *) (e->blob + m[A_W]); a.ldw = K;
+    a.M = M; a.N = N; a.K = K;
+    a.gelu_tab = e->g<const uint16_t *>(G_GELU);
+    a.T = e->d.T; a.D = e->d.D; a.H = e->d.H; a.TP = e->TP;
+    if (e->blk) {
+        a.nblk = K / e->blk;
+        a.dx = (const float *) (e->blob + m[A_DX]);
+        a.dy = K == e->d.D ? e->dyD : e->dyF;
+        if (e->blk == 256) {
+            a.dmin = (const float *) (e->blob + m[A_DMIN]);
+            a.wext = (const q2a_half *) (e->blob + m[A_WEXT]);
+            a.aext = K == e->d.D ? e->aextD : e->aextF;
+        }
+    }
+    return a;
+}
+
+int ln_mode(const q2a_engine * e) { return e->blk == 0 ? 0 : e->blk == 256 ? 1 : 2; }
+
+#define LAUNCH(x)                                                                     \
+    do {                                                                              \
+        hipError_t e_ = (x);                                                          \
+        if (e_ != hipSuccess) {                                                       \
+            set_err("%s: %s", #x, hipGetErrorString(e_));                           \
+            return Q2A_ERR_HIP;                                                       \
+        }                                                                             \
+    } while (0)
+
+// one pre-LN encoder block on X [B*T][D] (qwen2-whisper.cpp:2014-2155)
+int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
+    const dims & d = e->d;
+    const int M = B * d.T;
+    const int mode = ln_mode(e);
+    q2a_ln_args ln{e->X, M, d.D, e->lv<const float *>(l, L_LN1W), e->lv<const float *>(l, L_LN1B), mode, e->actD, e->dyD, e->aextD};
+    LAUNCH(q2a_launch_layernorm(ln, s));
+    {
+        q2a_gemm_args a = gemm_base(e, l, 0, e->actD, M);
+        a.bias = e->lv<const float *>(l, L_BQKV);
+        a.qh = e->qh; a.ql = e->ql; a.kh = e->kh; a.kl = e->kl; a.vt = e->vt;
+        a.qscale = 1.0f / sqrtf((float) (d.D / d.H));
+        LAUNCH(q2a_launch_gemm(a, Q2A_EPI_QKV, e->blk, s));
+    }
+    {
+        q2a_attn_args at{e->qh, e->ql, e->kh, e->kl, e->vt, B, d.T, d.D, d.H, e->TP, nullptr, nullptr};
+        if (mode == 0) at.outH = e->actD; else at.outF = e->attF;
+        LAUNCH(q2a_launch_attention(at, s));
+        if (mode) {
+            q2a_quant_args qa{e->attF, M, d.D, mode, e->actD, e->dyD, e->aextD};
+            LAUNCH(q2a_launch_quant_act(qa, s));
+        }
+    }
+    {
+        q2a_gemm_args a = gemm_base(e, l, 1, e->actD, M);
+        a.bias = e->lv<const float *>(l, L_BO);
+        a.outF = e->X; a.ldo = d.D;
+        LAUNCH(q2a_launch_gemm(a, Q2A_EPI_RESID, e->blk, s));
+    }
+    q2a_ln_args ln2{e->X, M, d.D, e->lv<const float *>(l, L_LN2W), e->lv<const float *>(l, L_LN2B), mode, e->actD, e->dyD, e->aextD};
+    LAUNCH(q2a_launch_layernorm(ln2, s));
+    {
+        q2a_gemm_args a = gemm_base(e, l, 2, e->actD, M);
+        a.bias = e->lv<const float *>(l, L_B1);
+        if (mode == 0) {
+            a.outH = e->actF; a.ldo = d.F; a.o_rpg = M; a.o_gstride = 0; a.o_off = 0;
+            LAUNCH(q2a_launch_gemm(a, Q2A_EPI_GELU_H, 0, s));
+        } else {
+            a.outF = e->hF; a.ldo = d.F;
+            LAUNCH(q2a_launch_gemm(a, Q2A_EPI_GELU_F, e->blk, s));
+            q2a_quant_args qa{e->hF, M, d.F, mode, e->actF, e->dyF, e->aextF};
+            LAUNCH(q2a_launch_quant_act(qa, s));
+        }
+    }
+    {
+        q2a_gemm_args a = gemm_base(e, l, 3, e->actF, M);
+        a.bias = e->lv<const float *>(l, L_B2);
+        a.outF = e->X; a.ldo = d.D;
+        LAUNCH(q2a_launch_gemm(a, Q2A_EPI_RESID, e->blk, s));
+    }
+    return Q2A_OK;
+}
+
+// mel + conv frontend: PCM -> X [B*T][D] (conv graph qwen2-whisper.cpp:1892-1952 + pe add :2005)
+int run_frontend(q2a_engine * e, const float * pcm, int64_t stride, int B, int max_frames, hipStream_t s) {
+    const dims & d = e->d;
+    int32_t * nsamp = e->meta;
+    int32_t * seek = e->meta + B;
+    int32_t * cmax = e->meta + 3 * B;
+    LAUNCH(hipMemsetAsync(cmax, 0x80, (size_t) B * 4, s));
+    q2a_mel_args ma;
+    ma.pcm = pcm; ma.pcm_stride = stride; ma.n_samples = nsamp; ma.seek = seek; ma.n_clips = B;
+    ma.n_mel = d.M; ma.n_bins = 201; ma.n_frames_win = d.TM; ma.max_frames = max_frames;
+    ma.filters = e->g<const float *>(G_FILT); ma.tab = e->g<const float *>(G_TAB);
+    ma.mel = e->mel; ma.clip_max = cmax; ma.xc1 = e->xc1;
+    LAUNCH(q2a_launch_mel(ma, s));
+    {   // conv1: implicit GEMM, A row t = xc1 rows t..t+2 of its clip (768 halves), K = 6M
+        q2a_gemm_args a;
+        memset(&a, 0, sizeof(a));
+        a.A = e->xc1; a.lda = 2 * d.M; a.a_rpg = d.TM; a.a_gstride = d.TM + 2; a.a_step = 1;
+        a.W = e->g<const q2a_half *>(G_CONV1_W); a.ldw = 6 * d.M;
+        a.M = B * d.TM; a.N = d.D; a.K = 6 * d.M;
+        a.bias = e->g<const float *>(G_CONV1_B);
+        a.outH = e->y1; a.ldo = d.D; a.o_rpg = d.TM; a.o_gstride = d.TM + 1; a.o_off = 1;
+        a.gelu_tab = e->g<const uint16_t *>(G_GELU);
+        LAUNCH(q2a_launch_gemm(a, Q2A_EPI_GELU_H, 0, s));
+    }
+    {   // conv2 (stride 2): A row t = y1 rows 2t..2t+2 (inputs 2t-1..2t+1), K = 3D; + pe
+        q2a_gemm_args a;
+        memset(&a, 0, sizeof(a));
+        a.A = e->y1; a.lda = d.D; a.a_rpg = d.T; a.a_gstride = d.TM + 1; a.a_step = 2;
+        a.W = e->g<const q2a_half *>(G_CONV2_W); a.ldw = 3 * d.D;
+        a.M = B * d.T; a.N = d.D; a.K = 3 * d.D;
+        a.bias = e->g<const float *>(G_CONV2_B);
+        a.outF = e->X; a.ldo = d.D; a.pe = e->g<const float *>(G_PE); a.T = d.T;
+        a.gelu_tab = e->g<const uint16_t *>(G_GELU);
+        LAUNCH(q2a_launch_gemm(a, Q2A_EPI_CONV2, 0, s));
+    }
+    return Q2A_OK;
+}
+
+// per-clip metadata (host): whisper_encoder_output_with_state's seek / too-short logic (:2356-2365)
+int prepare_meta(q2a_engine * e, const int32_t * n_samples, int B, int offset_ms, int32_t * status, int & max_frames,
+                 int64_t max_valid, hipStream_t s) {
+    int32_t * mh = e->meta_host;
+    max_frames = 0;
+    const int seek = offset_ms / 10;
+    for (int c = 0; c < B; ++c) {
+        const int n = n_samples[c];
+        if (n < 0 || (max_valid >= 0 && n > max_valid)) { set_err("clip %d: bad n_samples %d", c, n); return Q2A_ERR_ARG; }
+        const int n_len_org = 1 + (n + 200 - 400) / 160;   // mel.n_len_org (:2613), C truncation
+        const bool ok = n > 200 && !(n_len_org < seek + 100);
+        mh[c] = ok ? n : 0;
+        mh[B + c] = seek;
+        mh[2 * B + c] = ok ? 1 : 0;
+        if (status) status[c] = ok ? Q2A_CLIP_ENCODED : Q2A_CLIP_SKIPPED;
+        max_frames = std::max(max_frames, (int) (((int64_t) mh[c] + 480000) / 160));
+    }
+    HIP_TRY(hipMemcpyAsync(e->meta, mh, (size_t) B * 3 * 4, hipMemcpyHostToDevice, s));
+    return Q2A_OK;
+}
+
+int encode_impl(q2a_engine * e, const float * pcm, int64_t stride, const int32_t * n_samples, int B, int offset_ms,
+                float * out, int32_t * status, hipStream_t s) {
+    if (B <= 0 || !pcm || !n_samples || !out) { set_err("invalid arguments"); return Q2A_ERR_ARG; }
+    if (offset_ms < 0) { set_err("offset_ms must be >= 0"); return Q2A_ERR_ARG; }
+    HIP_TRY(hipSetDevice(e->device));
+    int rc = reserve(e, B);
+    if (rc) return rc;
+    int max_frames = 0;
+    rc = prepare_meta(e, n_samples, B, offset_ms, status, max_frames, stride, s);
+    if (rc) return rc;
+    rc = run_frontend(e, pcm, stride, B, max_frames, s);
+    if (rc) return rc;
+    for (int l = 0; l < e->d.L; ++l) {
+        rc = run_block(e, l, B, s);
+        if (rc) return rc;
+    }
+    q2a_pool_args pa{e->X, B, e->d.T, e->d.D, e->g<const float *>(G_LNP_W), e->g<const float *>(G_LNP_B), out, e->meta + 2 * B};
+    LAUNCH(q2a_launch_pool_ln(pa, s));
+    return Q2A_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------------
+extern "C" {
+
+const char * q2a_last_error(void) { return g_err.c_str(); }
+
+int64_t q2a_pack_model(const char * path, void ** host_blob) {
+    std::vector<uint8_t> v;
+    const int rc = pack(path, v);
+    if (rc) return rc;
+    void * p = malloc(v.size());
+    if (!p) { set_err("host allocation failed"); return Q2A_ERR_OOM; }
+    memcpy(p, v.data(), v.size());
+    *host_blob = p;
+    return (int64_t) v.size();
+}
+
+void q2a_free_host_blob(void * p) { free(p); }
+
+q2a_engine * q2a_open(const char * model_path, int device) {
+    q2a_engine * e = new q2a_engine();
+    std::vector<uint8_t> v;
+    if (engine_init(e, device) || pack(model_path, v)) { q2a_close(e); return nullptr; }
+    memcpy(&e->h, v.data(), sizeof(blob_header));
+    if (engine_adopt_header(e)) { q2a_close(e); return nullptr; }
+    if (hipMalloc((void **) &e->blob, v.size()) != hipSuccess) {
+        (void) hipGetLastError();
+        set_err("weight allocation of %.2f GB failed", v.size() / 1e9);
+        q2a_close(e);
+        return nullptr;
+    }
+    e->own_blob = true;
+    e->blob_size = (int64_t) v.size();
+    if (hipMemcpy(e->blob, v.data(), v.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        set_err("weight upload failed");
+        q2a_close(e);
+        return nullptr;
+    }
+    return e;
+}
+
+q2a_engine * q2a_open_device_blob(const void * dev_blob, int64_t size, int device) {
+    if (!dev_blob || size < (int64_t) HEADER_BYTES) { set_err("invalid blob"); return nullptr; }
+    q2a_engine * e = new q2a_engine();
+    if (engine_init(e, device)) { q2a_close(e); return nullptr; }
+    if (hipMemcpy(&e->h, dev_blob, sizeof(blob_header), hipMemcpyDeviceToHost) != hipSuccess) {
+        set_err("cannot read blob header from device");
+        q2a_close(e);
+        return nullptr;
+    }
+    if (engine_adopt_header(e) || (int64_t) e->h.total != size) {
+        if (g_err.empty()) set_err("blob size mismatch");
+        q2a_close(e);
+        return nullptr;
+    }
+    e->blob = (uint8_t *) dev_blob;
+    e->own_blob = false;
+    e->blob_size = size;
+    return e;
+}
+
+void q2a_close(q2a_engine * e) {
+    if (!e) return;
+    (void) hipSetDevice(e->device);
+    if (e->stream) (void) hipStreamSynchronize(e->stream);
+    free_ws(e);
+    if (e->own_blob && e->blob) (void) hipFree(e->blob);
+    if (e->stream) (void) hipStreamDestroy(e->stream);
+    delete e;
+}
+
+int q2a_get_info(const q2a_engine * e, q2a_info * info) {
+    if (!e || !info) return Q2A_ERR_ARG;
+    info->n_audio_ctx = e->d.T; info->n_audio_state = e->d.D; info->n_audio_head = e->d.H;
+    info->n_audio_layer = e->d.L; info->n_mels = e->d.M; info->wtype = e->wtype; info->n_out = e->d.TO;
+    info->device = e->device; info->weight_bytes = e->blob_size; info->workspace_bytes = (int64_t) e->ws_bytes;
+    return Q2A_OK;
+}
+
+int q2a_reserve(q2a_engine * e, int max_clips, int64_t max_samples) {
+    if (!e || max_clips <= 0) return Q2A_ERR_ARG;
+    (void) max_samples;
+    return reserve(e, max_clips);
+}
+
+int q2a_encode_device(q2a_engine * e, const float * pcm_dev, int64_t pcm_stride, const int32_t * n_samples,
+                      int n_clips, int offset_ms, float * out_dev, int32_t * status, void * stream) {
+    if (!e) return Q2A_ERR_ARG;
+    hipStream_t s = stream ? (hipStream_t) stream : e->stream;
+    return encode_impl(e, pcm_dev, pcm_stride, n_samples, n_clips, offset_ms, out_dev, status, s);
+}
+
+int q2a_encode_host(q2a_engine * e, const float * const * pcm, const int32_t * n_samples, int n_clips, int offset_ms,
+                    float * out_host, int32_t * status) {
+    if (!e || !pcm || !n_samples || !out_host || n_clips <= 0) { set_err("invalid arguments"); return Q2A_ERR_ARG; }
+    HIP_TRY(hipSetDevice(e->device));
+    int64_t maxn = 1;
+    for (int c = 0; c < n_clips; ++c) maxn = std::max<int64_t>(maxn, n_samples[c]);
+    maxn = (maxn + 63) & ~int64_t(63);
+    float * dpcm = nullptr;
+    float * dout = nullptr;
+    const size_t out_bytes = (size_t) n_clips * e->d.TO * e->d.D * 4;
+    HIP_TRY(hipMalloc((void **) &dpcm, (size_t) n_clips * maxn * 4));
+    if (hipMalloc((void **) &dout, out_bytes) != hipSuccess) { (void) hipFree(dpcm); set_err("alloc failed"); return Q2A_ERR_OOM; }
+    int rc = Q2A_OK;
+    for (int c = 0; c < n_clips && rc == Q2A_OK; ++c)
+        if (hipMemcpyAsync(dpcm + c * maxn, pcm[c], (size_t) n_samples[c] * 4, hipMemcpyHostToDevice, e->stream) != hipSuccess)
+            rc = Q2A_ERR_HIP;
+    // outputs of skipped clips are left untouched: seed the device buffer with the caller's current contents
+    if (rc == Q2A_OK && hipMemcpyAsync(dout, out_host, out_bytes, hipMemcpyHostToDevice, e->stream) != hipSuccess) rc = Q2A_ERR_HIP;
+    if (rc == Q2A_OK) rc = encode_impl(e, dpcm, maxn, n_samples, n_clips, offset_ms, dout, status, e->stream);
+    if (rc == Q2A_OK && hipMemcpyAsync(out_host, dout, out_bytes, hipMemcpyDeviceToHost, e->stream) != hipSuccess) rc = Q2A_ERR_HIP;
+    if (hipStreamSynchronize(e->stream) != hipSuccess && rc == Q2A_OK) { set_err("stream error"); rc = Q2A_ERR_HIP; }
+    (void) hipFree(dpcm);
+    (void) hipFree(dout);
+    return rc;
+}
+
+int q2a_pcm_to_mel(q2a_engine * e, const float * pcm, int n_samples, float * mel_out, int64_t mel_cap, int * n_len_out) {
+    if (!e || !pcm || !mel_out || !n_len_out || n_samples <= 200) { set_err("invalid arguments"); return Q2A_ERR_ARG; }
+    HIP_TRY(hipSetDevice(e->device));
+    const dims & d = e->d;
+    const int n_len = (int) (((int64_t) n_samples + 480000) / 160);
+    if (mel_cap < (int64_t) d.M * n_len) { set_err("mel buffer too small (%d frames)", n_len); return Q2A_ERR_ARG; }
+    int rc = reserve(e, 1);
+    if (rc) return rc;
+    // run the mel kernel with a window covering every frame, in chunks of TM frames
+    float * dpcm = nullptr;
+    HIP_TRY(hipMalloc((void **) &dpcm, (size_t) n_samples * 4));
+    std::vector<float> chunk((size_t) d.M * d.TM);
+    hipStream_t s = e->stream;
+    rc = Q2A_OK;
+    if (hipMemcpy(dpcm, pcm, (size_t) n_samples * 4, hipMemcpyHostToDevice) != hipSuccess) rc = Q2A_ERR_HIP;
+    int32_t cmax = 0;
+    for (int f0 = 0; f0 < n_len && rc == Q2A_OK; f0 += d.TM) {
+        int32_t * mh = e->meta_host;
+        mh[0] = n_samples; mh[1] = f0; mh[2] = 1;
+        if (hipMemcpyAsync(e->meta, mh, 12, hipMemcpyHostToDevice, s) != hipSuccess) { rc = Q2A_ERR_HIP; break; }
+        if (hipMemsetAsync(e->meta + 3, 0x80, 4, s) != hipSuccess) { rc = Q2A_ERR_HIP; break; }
+        q2a_mel_args ma;
+        ma.pcm = dpcm; ma.pcm_stride = n_samples; ma.n_samples = e->meta; ma.seek = e->meta + 1; ma.n_clips = 1;
+        ma.n_mel = d.M; ma.n_bins = 201; ma.n_frames_win = d.TM; ma.max_frames = n_len;
+        ma.filters = e->g<const float *>(G_FILT); ma.tab = e->g<const float *>(G_TAB);
+        ma.mel = e->mel; ma.clip_max = e->meta + 3; ma.xc1 = e->xc1;
+        if (q2a_launch_mel(ma, s) != hipSuccess) { rc = Q2A_ERR_HIP; break; }
+        if (hipMemcpyAsync(chunk.data(), e->mel, chunk.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(&cmax, e->meta + 3, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) { rc = Q2A_ERR_HIP; break; }
+        const int nf = std::min(d.TM, n_len - f0);
+        for (int j = 0; j < d.M; ++j) memcpy(mel_out + (size_t) j * n_len + f0, chunk.data() + (size_t) j * d.TM, (size_t) nf * 4);
+    }
+    (void) hipFree(dpcm);
+    if (rc) { set_err("mel computation failed"); return rc; }
+    // clamp + normalise exactly as the reference (:2633-2649) on the host (the device path fuses this into conv1)
+    const float mx_f = [&] { int32_t i = cmax; i = i >= 0 ? i : i ^ 0x7fffffff; float f; memcpy(&f, &i, 4); return f; }();
+    const double mmax = (double) mx_f - 8.0;
+    for (int64_t i = 0; i < (int64_t) d.M * n_len; ++i) {
+        float v = mel_out[i];
+        if (v < mmax) v = (float) mmax;
+        mel_out[i] = (float) ((v + 4.0) / 4.0);
+    }
+    *n_len_out = n_len;
+    return Q2A_OK;
+}
+
+int q2a_test_linear(q2a_engine * e, int layer, int which, const float * x, int M, float * y, void * stream) {
+    if (!e || layer < 0 || layer >= e->d.L || which < 0 || which > 3 || M <= 0) return Q2A_ERR_ARG;
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = stream ? (hipStream_t) stream : e->stream;
+    const dims & d = e->d;
+    int rc = reserve(e, (M + d.T - 1) / d.T);
+    if (rc) return rc;
+    int N, K;
+    mat_dims(d, which, N, K);
+    q2a_half * A = K == d.D ? e->actD : e->actF;
+    const int mode = ln_mode(e);
+    if (mode == 0) {
+        const int64_t n = (int64_t) M * K;
+        hipLaunchKernelGGL(k_to_half, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, A, n);
+        LAUNCH(hipGetLastError());
+    } else {
+        q2a_quant_args qa{x, M, K, mode, A, K == d.D ? e->dyD : e->dyF, K == d.D ? e->aextD : e->aextF};
+        LAUNCH(q2a_launch_quant_act(qa, s));
+    }
+    q2a_gemm_args a = gemm_base(e, layer, which, A, M);
+    a.outF = y; a.ldo = N;
+    LAUNCH(q2a_launch_gemm(a, Q2A_EPI_STORE_F, e->blk, s));
+    return Q2A_OK;
+}
+
+int q2a_test_block(q2a_engine * e, int layer, float * x, int n_clips, void * stream) {
+    if (!e || layer < 0 || layer >= e->d.L || n_clips <= 0) return Q2A_ERR_ARG;
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = stream ? (hipStream_t) stream : e->stream;
+    int rc = reserve(e, n_clips);
+    if (rc) return rc;
+    const size_t bytes = (size_t) n_clips * e->d.T * e->d.D * 4;
+    HIP_TRY(hipMemcpyAsync(e->X, x, bytes, hipMemcpyDeviceToDevice, s));
+    rc = run_block(e, layer, n_clips, s);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(x, e->X, bytes, hipMemcpyDeviceToDevice, s));
+    return Q2A_OK;
+}
+
+int q2a_test_attention(q2a_engine * e, const float * q, const float * k, const float * v, int n_clips, float * out,
+                       void * stream) {
+    if (!e || n_clips <= 0) return Q2A_ERR_ARG;
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = stream ? (hipStream_t) stream : e->stream;
+    int rc = reserve(e, n_clips);
+    if (rc) return rc;
+    const dims & d = e->d;
+    const int64_t n = (int64_t) n_clips * d.T * d.D;
+    const dim3 g((unsigned) ((n + 255) / 256)), b(256);
+    hipLaunchKernelGGL(k_split_hilo, g, b, 0, s, q, e->qh, e->ql, n);
+    hipLaunchKernelGGL(k_split_hilo, g, b, 0, s, k, e->kh, e->kl, n);
+    hipLaunchKernelGGL(k_to_vt, g, b, 0, s, v, e->vt, n_clips, d.T, d.H, e->TP);
+    LAUNCH(hipGetLastError());
+    q2a_attn_args at{e->qh, e->ql, e->kh, e->kl, e->vt, n_clips, d.T, d.D, d.H, e->TP, nullptr, out};
+    LAUNCH(q2a_launch_attention(at, s));
+    return Q2A_OK;
+}
+
+}  // extern "C"

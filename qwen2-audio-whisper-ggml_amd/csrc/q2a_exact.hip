@@ -1,0 +1,384 @@
+// q2a_exact.hip — kernels whose float operation order follows the reference op-for-op (compiled with
+// -ffp-contract=off): log-mel frontend, LayerNorm (+ activation quantizers), AvgPool + final LayerNorm.
+// All are HBM/latency-bound; they are fused so that each tensor is read once and written once.
+#include "q2a_internal.h"
+
+#include <math.h>
+
+namespace {
+
+constexpr int NFFT = 400;
+
+// ------------------------------------------------------------------------------------------------
+// log-mel (log_mel_spectrogram + worker, qwen2-whisper.cpp:2443-2665)
+// One wave per frame. The radix-2 recursion of `fft` (:2465-2507) is unrolled by depth: 16 leaf 25-point
+// DFTs (`dft`, :2443-2459) on the decimated inputs x[id + 16n], then 4 combine levels; every butterfly uses
+// the reference's expression order, so the power spectrum is bit-identical to the CPU path.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int32_t f2ord(float f) {
+    int32_t i = __float_as_int(f);
+    return i >= 0 ? i : i ^ 0x7fffffff;
+}
+__device__ __forceinline__ float ord2f(int32_t i) { return __int_as_float(i >= 0 ? i : i ^ 0x7fffffff); }
+
+__global__ __launch_bounds__(256) void k_mel_frames(const q2a_mel_args p) {
+    __shared__ float s_in[4][NFFT];
+    __shared__ float s_a[4][2 * NFFT];
+    __shared__ float s_b[4][2 * NFFT];
+    __shared__ float s_pow[4][208];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int c = blockIdx.y;
+    const int i = blockIdx.x * 4 + w;
+    const int n = p.n_samples[c];
+    const int n_len = (int) (((int64_t) n + 480000) / 160);         // (n + 30 s + 2*200 - 400) / 160 (:2611)
+    const int n_s = n + 200;                                         // worker's n_samples (:2621)
+    const int n_fft_frames = min(n_s / 160 + 1, n_len);               // (:2522)
+    const bool active = i < n_len;
+    const bool do_fft = active && i < n_fft_frames;
+    const int win = i - p.seek[c];
+    const bool in_win = active && win >= 0 && win < p.n_frames_win;
+    float * mel_out = p.mel + (int64_t) c * p.n_mel * p.n_frames_win;
+    const float * hann = p.tab;
+    const float * cosv = p.tab + NFFT;
+    const float * sinv = p.tab + 2 * NFFT;
+
+    if (active && !do_fft) {                                         // constant frames (:2565-2571)
+        const float v = (float) log10(1e-10);
+        if (in_win)
+            for (int j = lane; j < p.n_mel; j += 64) mel_out[(int64_t) j * p.n_frames_win + win] = v;
+        if (lane == 0) atomicMax(p.clip_max + c, f2ord(v));
+    }
+    // every wave reaches every barrier below; inactive waves just skip the work
+    // windowed input: samples_padded = [reflect(200) | pcm | zeros], read up to n_s (:2526-2533)
+    const float * pcm = p.pcm + (int64_t) c * p.pcm_stride;
+    const int off = i * 160;
+    if (do_fft) {
+        for (int j = lane; j < NFFT; j += 64) {
+            const int x = off + j;
+            float v = 0.f;
+            if (x < n_s) v = x < 200 ? (200 - x < n ? pcm[200 - x] : 0.f) : pcm[x - 200];
+            s_in[w][j] = x < n_s ? hann[j] * v : 0.f;
+        }
+    }
+    __syncthreads();
+    // leaves: node id (0..15) takes x[id + 16 n], n = 0..24; DFT step 400/25 = 16
+    float * cur = s_a[w];
+    if (do_fft) {
+        for (int o = lane; o < NFFT; o += 64) {
+            const int id = o / 25, k = o % 25;
+            float re = 0, im = 0;
+            for (int t = 0; t < 25; ++t) {
+                const int idx = (k * t * 16) % NFFT;
+                const float x = s_in[w][id + 16 * t];
+                re += x * cosv[idx];
+                im -= x * sinv[idx];
+            }
+            cur[2 * o + 0] = re;
+            cur[2 * o + 1] = im;
+        }
+    }
+    __syncthreads();
+    // combine levels: depth d has 2^d nodes of length 400/2^d; children of node id: id (even), id + 2^d (odd)
+    float * nxt = s_b[w];
+    for (int d = 3; d >= 0; --d) {
+        const int nn = 1 << d, nc = NFFT >> (d + 1), step = NFFT / (2 * nc);
+        if (do_fft) {
+            for (int b = lane; b < nn * nc; b += 64) {
+                const int id = b / nc, k = b % nc;
+                const float * E = cur + 2 * (id * nc);
+                const float * O = cur + 2 * ((id + nn) * nc);
+                float * out = nxt + 2 * (id * 2 * nc);
+                const int idx = k * step;
+                const float re = cosv[idx], im = -sinv[idx];
+                const float ro = O[2 * k + 0], io = O[2 * k + 1];
+                out[2 * k + 0] = E[2 * k + 0] + re * ro - im * io;
+                out[2 * k + 1] = E[2 * k + 1] + re * io + im * ro;
+                out[2 * (k + nc) + 0] = E[2 * k + 0] - re * ro + im * io;
+                out[2 * (k + nc) + 1] = E[2 * k + 1] - re * io - im * ro;
+            }
+        }
+        __syncthreads();
+        float * t = cur; cur = nxt; nxt = t;
+    }
+    // |X|^2 for bins 0..200 (:2540-2542)
+    if (do_fft)
+        for (int j = lane; j < p.n_bins; j += 64) s_pow[w][j] = cur[2 * j] * cur[2 * j] + cur[2 * j + 1] * cur[2 * j + 1];
+    __syncthreads();
+    if (!do_fft) return;
+    // mel filterbank in double with the reference's 4-way unrolled float partial sums (:2545-2561)
+    float lmax = -INFINITY;
+    const float * P = s_pow[w];
+    for (int j = lane; j < p.n_mel; j += 64) {
+        const float * f = p.filters + (int64_t) j * p.n_bins;
+        double sum = 0.0;
+        int k = 0;
+        for (k = 0; k < p.n_bins - 3; k += 4) sum += P[k] * f[k] + P[k + 1] * f[k + 1] + P[k + 2] * f[k + 2] + P[k + 3] * f[k + 3];
+        for (; k < p.n_bins; k++) sum += P[k] * f[k];
+        const float v = (float) log10(fmax(sum, 1e-10));
+        if (in_win) mel_out[(int64_t) j * p.n_frames_win + win] = v;
+        lmax = fmaxf(lmax, v);
+    }
+    for (int o = 32; o > 0; o >>= 1) lmax = fmaxf(lmax, __shfl_xor(lmax, o));
+    if (lane == 0) atomicMax(p.clip_max + c, f2ord(lmax));
+}
+
+// clamp to (max - 8), (x + 4) / 4 (:2633-2649), then write the conv1 operand rows [hi(128) | lo(128)] as fp16
+// (x = hi + lo to 22 bits, so the fp16 MFMA conv reproduces the F32 im2col x F32-upcast-kernel product).
+__global__ __launch_bounds__(256) void k_mel_norm(const q2a_mel_args p) {
+    __shared__ float tile[128][65];
+    const int c = blockIdx.y, t0 = blockIdx.x * 64;
+    const double mmax = (double) ord2f(p.clip_max[c]) - 8.0;
+    const float * mel = p.mel + (int64_t) c * p.n_mel * p.n_frames_win;
+    for (int e = threadIdx.x; e < p.n_mel * 64; e += 256) {
+        const int j = e / 64, tt = e % 64;
+        float v = 0.f;
+        if (t0 + tt < p.n_frames_win) {
+            v = mel[(int64_t) j * p.n_frames_win + t0 + tt];
+            if (v < mmax) v = (float) mmax;
+            v = (float) ((v + 4.0) / 4.0);
+        }
+        tile[j][tt] = v;
+    }
+    __syncthreads();
+    const int nm = p.n_mel;
+    q2a_half * xc = p.xc1 + (int64_t) c * (p.n_frames_win + 2) * 2 * nm;
+    for (int e = threadIdx.x; e < nm * 64; e += 256) {
+        const int tt = e / nm, j = e % nm;
+        if (t0 + tt >= p.n_frames_win) continue;
+        const float v = tile[j][tt];
+        const _Float16 h = (_Float16) v;
+        const _Float16 l = (_Float16) (v - (float) h);
+        q2a_half * row = xc + (int64_t) (t0 + tt + 1) * 2 * nm;
+        row[j] = h;
+        row[nm + j] = l;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// LayerNorm (ggml_compute_forward_norm_f32 ggml.c:11941-11990: double sums, eps 1e-5) + affine (MUL, ADD),
+// fused with the conversion ggml applies to the next MUL_MAT's src1 (ggml.c:12462-12475):
+//   mode 0 fp16 RNE;  mode 1 Q8_K (quantize_row_q8_K_ref ggml-quants.c:3785-3822);
+//   mode 2 Q8_0 (x86 quantize_row_q8_0 ggml-quants.c:943-1000: d = amax/127, id = 127/amax, round-half-even).
+// One wave per row; lane l owns float4 chunks l, l+64, ... so a 256-block is one float4 per lane.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ double wave_sum_d(double v) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// quantize one 256-block (one float4 per lane) to Q8_K codes; writes codes, d and the bsum hi/lo operand
+__device__ __forceinline__ void quant_q8k_block(float4 y, int lane, q2a_half * codes, float * dy_out, q2a_half * aext) {
+    // max |x| and the signed value of its FIRST occurrence (strict '>' scan, :3793-3798)
+    float av[4] = {fabsf(y.x), fabsf(y.y), fabsf(y.z), fabsf(y.w)};
+    float vv[4] = {y.x, y.y, y.z, y.w};
+    float amax = av[0], mx = vv[0];
+    int idx = lane * 4;
+    for (int e = 1; e < 4; ++e)
+        if (av[e] > amax) { amax = av[e]; mx = vv[e]; idx = lane * 4 + e; }
+    for (int o = 32; o > 0; o >>= 1) {
+        const float a2 = __shfl_xor(amax, o), m2 = __shfl_xor(mx, o);
+        const int i2 = __shfl_xor(idx, o);
+        if (a2 > amax || (a2 == amax && i2 < idx)) { amax = a2; mx = m2; idx = i2; }
+    }
+    int q[4] = {0, 0, 0, 0};
+    float d = 0.f;
+    if (amax != 0.f) {
+        const float iscale = -127.f / mx;
+        for (int e = 0; e < 4; ++e) q[e] = min(127, (int) rintf(iscale * vv[e]));
+        d = 1 / iscale;
+    }
+    for (int e = 0; e < 4; ++e) codes[e] = (_Float16) (float) q[e];
+    if (lane == 0) *dy_out = d;
+    // bsums over 16 = 4 lanes, then bsum32_j = lanes 8j..8j+7
+    int s = q[0] + q[1] + q[2] + q[3];
+    s += __shfl_xor(s, 1);
+    s += __shfl_xor(s, 2);
+    s += __shfl_xor(s, 4);
+    if ((lane & 7) == 0) {
+        const int j = lane >> 3;
+        const int hi = (s >= 0) ? (s >> 6) : -((-s + 63) >> 6);   // floor(s / 64)
+        const int lo = s - 64 * hi;
+        aext[2 * j + 0] = (_Float16) (float) hi;
+        aext[2 * j + 1] = (_Float16) (float) lo;
+    }
+}
+
+// quantize one 32-block (8 lanes x float4) to Q8_0 codes with the x86 AVX2 semantics
+__device__ __forceinline__ void quant_q80_block(float4 y, int lane, q2a_half * codes, float * dy_out) {
+    float amax = fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w)));
+    amax = fmaxf(amax, __shfl_xor(amax, 1));
+    amax = fmaxf(amax, __shfl_xor(amax, 2));
+    amax = fmaxf(amax, __shfl_xor(amax, 4));
+    const float d = amax / 127.f;
+    const float id = (amax != 0.0f) ? 127.f / amax : 0.0f;
+    codes[0] = (_Float16) rintf(y.x * id);
+    codes[1] = (_Float16) rintf(y.y * id);
+    codes[2] = (_Float16) rintf(y.z * id);
+    codes[3] = (_Float16) rintf(y.w * id);
+    if ((lane & 7) == 0) *dy_out = (float) (_Float16) d;    // block d is stored as fp16 (GGML_FP32_TO_FP16)
+}
+
+template <int MODE, bool LN>
+__global__ __launch_bounds__(256) void k_rownorm(const float * __restrict__ X, int M, int D, const float * __restrict__ g,
+                                                 const float * __restrict__ b, q2a_half * outH, float * dy, q2a_half * aext) {
+    const int lane = threadIdx.x & 63;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (row >= M) return;
+    const float4 * x4 = (const float4 *) (X + (int64_t) row * D);
+    const int nch = D / 4;
+    constexpr int MAXC = 8;   // D <= 2048
+    float4 v[MAXC];
+    float mean = 0.f, scale = 1.f;
+    if (LN) {
+        double s = 0.0;
+#pragma unroll
+        for (int u = 0; u < MAXC; ++u) {
+            const int c = lane + 64 * u;
+            if (c < nch) {
+                v[u] = x4[c];
+                s += (double) v[u].x + (double) v[u].y + (double) v[u].z + (double) v[u].w;
+            }
+        }
+        s = wave_sum_d(s);
+        mean = (float) (s / D);
+        double s2 = 0.0;
+#pragma unroll
+        for (int u = 0; u < MAXC; ++u) {
+            const int c = lane + 64 * u;
+            if (c < nch) {
+                v[u].x = v[u].x - mean; v[u].y = v[u].y - mean; v[u].z = v[u].z - mean; v[u].w = v[u].w - mean;
+                s2 += (double) (v[u].x * v[u].x) + (double) (v[u].y * v[u].y) + (double) (v[u].z * v[u].z) +
+                      (double) (v[u].w * v[u].w);
+            }
+        }
+        s2 = wave_sum_d(s2);
+        const float variance = (float) (s2 / D);
+        scale = 1.0f / sqrtf(variance + 1e-5f);
+    } else {
+#pragma unroll
+        for (int u = 0; u < MAXC; ++u) {
+            const int c = lane + 64 * u;
+            if (c < nch) v[u] = x4[c];
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < MAXC; ++u) {
+        const int c = lane + 64 * u;
+        if (c >= nch) continue;
+        float4 y = v[u];
+        if (LN) {
+            const float4 gg = ((const float4 *) g)[c], bb = ((const float4 *) b)[c];
+            y.x = (y.x * scale) * gg.x + bb.x;
+            y.y = (y.y * scale) * gg.y + bb.y;
+            y.z = (y.z * scale) * gg.z + bb.z;
+            y.w = (y.w * scale) * gg.w + bb.w;
+        }
+        q2a_half * o = outH + (int64_t) row * D + 4 * c;
+        if (MODE == 0) {
+            o[0] = (_Float16) y.x; o[1] = (_Float16) y.y; o[2] = (_Float16) y.z; o[3] = (_Float16) y.w;
+        } else if (MODE == 1) {
+            const int nb = D / 256;
+            quant_q8k_block(y, lane, o, dy + (int64_t) row * nb + u, aext + ((int64_t) row * nb + u) * 16);
+        } else {
+            const int nb = D / 32;
+            quant_q80_block(y, lane, o, dy + (int64_t) row * nb + (4 * c) / 32);
+        }
+    }
+}
+
+// AvgPool1d(k=2,s=2) over time (ggml.c:15077-15125: drow = 0; += a; += b; /= 2) + final LayerNorm -> f32
+__global__ __launch_bounds__(256) void k_pool_ln(const q2a_pool_args p) {
+    const int lane = threadIdx.x & 63;
+    const int TO = p.T / 2;
+    const int orow = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (orow >= p.n_clips * TO) return;
+    const int c = orow / TO, t = orow % TO;
+    if (!p.clip_ok[c]) return;
+    const float4 * a4 = (const float4 *) (p.X + ((int64_t) c * p.T + 2 * t) * p.D);
+    const float4 * b4 = (const float4 *) (p.X + ((int64_t) c * p.T + 2 * t + 1) * p.D);
+    const int nch = p.D / 4;
+    constexpr int MAXC = 8;
+    float4 v[MAXC];
+    double s = 0.0;
+#pragma unroll
+    for (int u = 0; u < MAXC; ++u) {
+        const int ch = lane + 64 * u;
+        if (ch < nch) {
+            const float4 a = a4[ch], b = b4[ch];
+            v[u].x = ((0.f + a.x) + b.x) / 2; v[u].y = ((0.f + a.y) + b.y) / 2;
+            v[u].z = ((0.f + a.z) + b.z) / 2; v[u].w = ((0.f + a.w) + b.w) / 2;
+            s += (double) v[u].x + (double) v[u].y + (double) v[u].z + (double) v[u].w;
+        }
+    }
+    s = wave_sum_d(s);
+    const float mean = (float) (s / p.D);
+    double s2 = 0.0;
+#pragma unroll
+    for (int u = 0; u < MAXC; ++u) {
+        const int ch = lane + 64 * u;
+        if (ch < nch) {
+            v[u].x -= mean; v[u].y -= mean; v[u].z -= mean; v[u].w -= mean;
+            s2 += (double) (v[u].x * v[u].x) + (double) (v[u].y * v[u].y) + (double) (v[u].z * v[u].z) +
+                  (double) (v[u].w * v[u].w);
+        }
+    }
+    s2 = wave_sum_d(s2);
+    const float scale = 1.0f / sqrtf((float) (s2 / p.D) + 1e-5f);
+    float4 * o4 = (float4 *) (p.out + ((int64_t) c * TO + t) * p.D);
+#pragma unroll
+    for (int u = 0; u < MAXC; ++u) {
+        const int ch = lane + 64 * u;
+        if (ch < nch) {
+            const float4 gg = ((const float4 *) p.g)[ch], bb = ((const float4 *) p.b)[ch];
+            float4 y;
+            y.x = (v[u].x * scale) * gg.x + bb.x;
+            y.y = (v[u].y * scale) * gg.y + bb.y;
+            y.z = (v[u].z * scale) * gg.z + bb.z;
+            y.w = (v[u].w * scale) * gg.w + bb.w;
+            o4[ch] = y;
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t q2a_launch_mel(const q2a_mel_args & a, hipStream_t s) {
+    if (a.n_bins > 208 || a.n_mel > 128 * 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_mel_frames, dim3((a.max_frames + 3) / 4, a.n_clips), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_mel_norm, dim3((a.n_frames_win + 63) / 64, a.n_clips), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t q2a_launch_layernorm(const q2a_ln_args & a, hipStream_t s) {
+    if (a.D % 4 != 0 || a.D > 2048) return hipErrorInvalidValue;
+    if (a.mode == 1 && a.D % 256) return hipErrorInvalidValue;
+    if (a.mode == 2 && a.D % 32) return hipErrorInvalidValue;
+    const dim3 grid((a.M + 3) / 4), blk(256);
+    if (a.mode == 0) hipLaunchKernelGGL((k_rownorm<0, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext);
+    else if (a.mode == 1) hipLaunchKernelGGL((k_rownorm<1, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext);
+    else hipLaunchKernelGGL((k_rownorm<2, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext);
+    return hipGetLastError();
+}
+
+hipError_t q2a_launch_quant_act(const q2a_quant_args & a, hipStream_t s) {
+    if (a.K % 256 != 0 || a.K > 8192) return hipErrorInvalidValue;
+    // rows longer than 2048 (fc2 input, K = 4D) are processed as K/1024 independent 1024-wide segments
+    const int seg = a.K > 2048 ? 1024 : a.K;
+    const int nseg = a.K / seg;
+    const dim3 grid((a.M * nseg + 3) / 4), blk(256);
+    // view X as [M*nseg][seg]: contiguous, and the block structure (256 / 32) never straddles a segment
+    if (a.mode == 1) {
+        hipLaunchKernelGGL((k_rownorm<1, false>), grid, blk, 0, s, a.X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext);
+    } else if (a.mode == 2) {
+        hipLaunchKernelGGL((k_rownorm<2, false>), grid, blk, 0, s, a.X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t q2a_launch_pool_ln(const q2a_pool_args & a, hipStream_t s) {
+    if (a.D % 4 != 0 || a.D > 2048) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_pool_ln, dim3((a.n_clips * (a.T / 2) + 3) / 4), dim3(256), 0, s, a);
+    return hipGetLastError();
+}

@@ -305,6 +305,29 @@ extern "C" void q2a_quantize_row_q4_0(const float * x, void * vy, int64_t k) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// reference numerics tables
+// ------------------------------------------------------------------------------------------------
+extern "C" void q2a_make_gelu_table(uint16_t * tab) {
+    const float GELU_COEF_A = 0.044715f;
+    const float SQRT_2_OVER_PI = 0.79788456080286535587989211986876f;
+    for (int i = 0; i < 65536; ++i) {
+        const float x = q2a_fp16_to_fp32((uint16_t) i);
+        const float g = 0.5f * x * (1.0f + tanhf(SQRT_2_OVER_PI * x * (1.0f + GELU_COEF_A * x * x)));
+        tab[i] = q2a_fp32_to_fp16(g);
+    }
+}
+
+extern "C" void q2a_make_mel_tables(float * t) {
+    const int N = 400;
+    for (int i = 0; i < N; i++) {
+        const double theta = (2 * M_PI * i) / N;
+        t[N + i] = cosf((float) theta);
+        t[2 * N + i] = sinf((float) theta);
+    }
+    for (int i = 0; i < N; i++) t[i] = (float) (0.5 * (1.0 - cosf((float) ((2.0 * M_PI * i) / N))));
+}
+
+// ------------------------------------------------------------------------------------------------
 // writer
 // ------------------------------------------------------------------------------------------------
 namespace {

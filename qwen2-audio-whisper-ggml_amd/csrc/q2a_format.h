@@ -78,6 +78,12 @@ void q2a_quantize_row_q4_K(const float * x, void * y, int64_t k);   // quantize_
 void q2a_quantize_row_q8_0(const float * x, void * y, int64_t k);   // quantize_row_q8_0_ref ggml-quants.c:848
 void q2a_quantize_row_q4_0(const float * x, void * y, int64_t k);   // quantize_row_q4_0_ref ggml-quants.c:761
 
+// Reference numerics tables (built on the host, compiled without FMA contraction, like the reference):
+//   GELU fp16 table (ggml.c:3797-3806): tab[h] = fp16(gelu_f32(fp32(h)))
+//   mel tables (whisper_global_cache, qwen2-whisper.cpp:2404-2437): hann[400] | cos[400] | sin[400]
+void q2a_make_gelu_table(uint16_t * tab65536);
+void q2a_make_mel_tables(float * hann_cos_sin1200);
+
 // ---- model-file reader -----------------------------------------------------------------------------
 typedef struct {
     char name[96];

@@ -1,0 +1,115 @@
+// q2a_internal.h — device-side argument structs and launch wrappers shared by the kernel files and the
+// engine. Not part of the public C ABI (include/q2a_encoder.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef _Float16 q2a_half;
+
+// Epilogue kinds of the fused weight GEMM (one template instantiation each)
+enum q2a_epi {
+    Q2A_EPI_QKV = 0,        // +bias, Q*(1/sqrt(dh)) -> Qh/Ql, K -> Kh/Kl (fp16 hi/lo), V -> Vt (fp16, [clip][head][d][TP])
+    Q2A_EPI_RESID = 1,      // outF[m][n] = (acc + bias[n]) + outF[m][n]           (O-proj, fc2)
+    Q2A_EPI_GELU_H = 2,     // outH[orow(m)][n] = fp16(gelu_lut(acc + bias[n]))   (fc1, conv1)
+    Q2A_EPI_CONV2 = 3,      // outF[m][n] = gelu_lut(acc + bias[n]) + pe[m % T][n] (conv2 + positional add)
+    Q2A_EPI_GELU_F = 4,     // outF[m][n] = gelu_lut(acc + bias[n])               (fc1 on the quantized paths)
+    Q2A_EPI_STORE_F = 5,    // outF[m][n] = acc                                   (unit tests)
+};
+
+struct q2a_gemm_args {
+    // A: fp16 [rows][lda]; logical row m lives at row  (m / a_rpg) * a_gstride + (m % a_rpg) * a_step
+    const q2a_half * A;
+    int64_t lda;
+    int a_rpg, a_gstride, a_step;
+    // W: fp16 [N][ldw] (row n = output feature, K contiguous)
+    const q2a_half * W;
+    int64_t ldw;
+    int M, N, K;
+    // epilogue
+    const float * bias;
+    float * outF;
+    int64_t ldo;
+    q2a_half * outH;
+    int o_rpg, o_gstride, o_off;      // output row remap for outH: (m / o_rpg) * o_gstride + (m % o_rpg) + o_off
+    const float * pe;
+    int T;                            // positions per clip
+    q2a_half *qh, *ql, *kh, *kl, *vt;
+    int D, H, TP;
+    float qscale;
+    const uint16_t * gelu_tab;        // 65536-entry fp16 table: fp16(gelu_f32(fp16 x)) (ggml.c:3797-3806)
+    // blocked (k-quant) accumulation: acc += dy[m][b]*dx[n][b]*S1 - dy[m][b]*dmin[n][b]*S2 per K-block b
+    const float * dy;                 // [M][nblk]
+    const float * dx;                 // [N][nblk]
+    const float * dmin;               // [N][nblk] (Q4_K only)
+    const q2a_half * aext;            // [M][nblk][16] bsum hi/lo pairs (Q4_K only)
+    const q2a_half * wext;            // [N][nblk][16] (64*m_j, m_j) pairs (Q4_K only)
+    int nblk;
+};
+
+// blk: 0 (plain fp16 GEMM), 256 (Q4_K x Q8_K), 32 (Q8_0/Q4_0 x Q8_0)
+hipError_t q2a_launch_gemm(const q2a_gemm_args & a, int epi, int blk, hipStream_t s);
+
+struct q2a_attn_args {
+    const q2a_half *qh, *ql, *kh, *kl, *vt;
+    int n_clips, T, D, H, TP;
+    q2a_half * outH;     // [clips*T][D] fp16 (F16 path) or
+    float * outF;        // [clips*T][D] f32  (quantized paths)
+};
+hipError_t q2a_launch_attention(const q2a_attn_args & a, hipStream_t s);
+
+// ---- exact-order kernels (q2a_exact.hip, compiled with -ffp-contract=off)
+struct q2a_mel_args {
+    const float * pcm;          // [clips][pcm_stride]
+    int64_t pcm_stride;
+    const int32_t * n_samples;  // [clips] (device)
+    const int32_t * seek;       // [clips] first frame of the window (device)
+    int n_clips;
+    int n_mel, n_bins;          // 128, 201
+    int n_frames_win;           // 2*n_ctx = 3000
+    int max_frames;             // max n_len over the batch (grid extent)
+    const float * filters;      // [n_mel][n_bins]
+    const float * tab;          // hann[400] | cos[400] | sin[400]
+    float * mel;                // [clips][n_mel][n_frames_win] raw log10 values
+    int32_t * clip_max;         // [clips] ordered-int encoding of the max over ALL frames
+    q2a_half * xc1;             // [clips][n_frames_win+2][2*n_mel] conv1 operand (hi|lo per row), rows 0/last = 0
+};
+hipError_t q2a_launch_mel(const q2a_mel_args & a, hipStream_t s);
+
+// LayerNorm over rows of X [M][D] (ggml_norm + mul + add, eps 1e-5), output by mode:
+//   0: fp16 [M][D]                     (F16 weights)
+//   1: Q8_K as fp16 codes + dy[M][D/256] + aext (Q4_K weights)
+//   2: Q8_0 as fp16 codes + dy[M][D/32]  (Q8_0 / Q4_0 weights)
+struct q2a_ln_args {
+    const float * X;
+    int M, D;
+    const float * g;
+    const float * b;
+    int mode;
+    q2a_half * outH;
+    float * dy;
+    q2a_half * aext;
+};
+hipError_t q2a_launch_layernorm(const q2a_ln_args & a, hipStream_t s);
+
+// activation quantizer for F32 rows (attention output / gelu output on the quantized paths): modes 1, 2
+struct q2a_quant_args {
+    const float * X;
+    int M, K;
+    int mode;
+    q2a_half * outH;
+    float * dy;
+    q2a_half * aext;
+};
+hipError_t q2a_launch_quant_act(const q2a_quant_args & a, hipStream_t s);
+
+// AvgPool1d(2,2) over time + final LayerNorm -> out [clips][T/2][D] f32
+struct q2a_pool_args {
+    const float * X;     // [clips*T][D]
+    int n_clips, T, D;
+    const float * g;
+    const float * b;
+    float * out;
+    const int32_t * clip_ok;   // [clips] 1 = write output, 0 = leave untouched (reference early return)
+};
+hipError_t q2a_launch_pool_ln(const q2a_pool_args & a, hipStream_t s);

@@ -1,0 +1,163 @@
+"""Python host mirror of the MI355X encoder path (ctypes over the C ABI in include/q2a_encoder.h).
+
+The product is lib/libq2a.so (HIP kernels for gfx950). This module only marshals arguments; there is no
+CPU fallback: if the library or a GPU is missing every call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libq2a.so")
+HOST_LIB_PATH = os.path.join(PKG_DIR, "lib", "libq2a_host.so")
+TOOL_PATH = os.path.join(PKG_DIR, "bin", "q2a_tool")
+
+EXPORTS = (
+    "q2a_last_error", "q2a_open", "q2a_pack_model", "q2a_free_host_blob", "q2a_open_device_blob", "q2a_close",
+    "q2a_get_info", "q2a_reserve", "q2a_encode_device", "q2a_encode_host", "q2a_pcm_to_mel",
+    "q2a_test_linear", "q2a_test_block", "q2a_test_attention",
+)
+
+CLIP_ENCODED, CLIP_SKIPPED = 0, 1
+
+
+class Q2AError(RuntimeError):
+    pass
+
+
+class Info(C.Structure):
+    _fields_ = [("n_audio_ctx", C.c_int32), ("n_audio_state", C.c_int32), ("n_audio_head", C.c_int32),
+                ("n_audio_layer", C.c_int32), ("n_mels", C.c_int32), ("wtype", C.c_int32), ("n_out", C.c_int32),
+                ("device", C.c_int32), ("weight_bytes", C.c_int64), ("workspace_bytes", C.c_int64)]
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libq2a.so (raises if it was not built: there is no fallback path)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise Q2AError(f"{LIB_PATH} not built; run `make -C {PKG_DIR}` (hipcc --offload-arch=gfx950)")
+        L = C.CDLL(LIB_PATH)
+        vp, i32p, f32p = C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_float)
+        L.q2a_last_error.restype = C.c_char_p
+        L.q2a_open.restype = vp
+        L.q2a_open.argtypes = [C.c_char_p, C.c_int]
+        L.q2a_pack_model.restype = C.c_int64
+        L.q2a_pack_model.argtypes = [C.c_char_p, C.POINTER(vp)]
+        L.q2a_free_host_blob.argtypes = [vp]
+        L.q2a_open_device_blob.restype = vp
+        L.q2a_open_device_blob.argtypes = [vp, C.c_int64, C.c_int]
+        L.q2a_close.argtypes = [vp]
+        L.q2a_get_info.argtypes = [vp, C.POINTER(Info)]
+        L.q2a_reserve.argtypes = [vp, C.c_int, C.c_int64]
+        L.q2a_encode_device.argtypes = [vp, vp, C.c_int64, i32p, C.c_int, C.c_int, vp, i32p, vp]
+        L.q2a_encode_host.argtypes = [vp, C.POINTER(vp), i32p, C.c_int, C.c_int, vp, i32p]
+        L.q2a_pcm_to_mel.argtypes = [vp, vp, C.c_int, vp, C.c_int64, i32p]
+        L.q2a_test_linear.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int, vp, vp]
+        L.q2a_test_block.argtypes = [vp, C.c_int, vp, C.c_int, vp]
+        L.q2a_test_attention.argtypes = [vp, vp, vp, vp, C.c_int, vp, vp]
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise Q2AError(f"q2a error {rc}: {lib().q2a_last_error().decode()}")
+
+
+class Engine:
+    """One encoder engine on one HIP device (the analogue of a whisper_context + whisper_state)."""
+
+    def __init__(self, model_path: str | None = None, device: int = 0, device_blob: int | None = None,
+                 blob_size: int | None = None):
+        L = lib()
+        if device_blob is not None:
+            h = L.q2a_open_device_blob(C.c_void_p(device_blob), C.c_int64(blob_size), device)
+        else:
+            h = L.q2a_open(model_path.encode(), device)
+        if not h:
+            raise Q2AError(L.q2a_last_error().decode())
+        self.h = h
+        self.info = Info()
+        _check(L.q2a_get_info(self.h, C.byref(self.info)))
+
+    def close(self):
+        if self.h:
+            lib().q2a_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def out_shape(self):
+        return (self.info.n_out, self.info.n_audio_state)
+
+    def reserve(self, n_clips: int, max_samples: int = 0):
+        _check(lib().q2a_reserve(self.h, n_clips, max_samples))
+        _check(lib().q2a_get_info(self.h, C.byref(self.info)))
+
+    def encode_device(self, pcm_ptr: int, pcm_stride: int, n_samples, out_ptr: int, offset_ms: int = 0,
+                      stream: int | None = None):
+        ns = np.ascontiguousarray(n_samples, dtype=np.int32)
+        st = np.zeros(len(ns), dtype=np.int32)
+        _check(lib().q2a_encode_device(self.h, C.c_void_p(pcm_ptr), C.c_int64(pcm_stride),
+                                       ns.ctypes.data_as(C.POINTER(C.c_int32)), len(ns), offset_ms,
+                                       C.c_void_p(out_ptr), st.ctypes.data_as(C.POINTER(C.c_int32)),
+                                       C.c_void_p(stream) if stream else None))
+        return st
+
+    def encode_host(self, clips, offset_ms: int = 0, out: np.ndarray | None = None):
+        clips = [np.ascontiguousarray(c, dtype=np.float32) for c in clips]
+        n = len(clips)
+        if out is None:
+            out = np.zeros((n,) + self.out_shape, dtype=np.float32)
+        ptrs = (C.c_void_p * n)(*[c.ctypes.data for c in clips])
+        ns = np.array([len(c) for c in clips], dtype=np.int32)
+        st = np.zeros(n, dtype=np.int32)
+        _check(lib().q2a_encode_host(self.h, ptrs, ns.ctypes.data_as(C.POINTER(C.c_int32)), n, offset_ms,
+                                     C.c_void_p(out.ctypes.data), st.ctypes.data_as(C.POINTER(C.c_int32))))
+        return out, st
+
+    def pcm_to_mel(self, pcm: np.ndarray) -> np.ndarray:
+        pcm = np.ascontiguousarray(pcm, dtype=np.float32)
+        n_len = (len(pcm) + 480000) // 160
+        out = np.empty((self.info.n_mels, n_len), dtype=np.float32)
+        got = C.c_int32(0)
+        _check(lib().q2a_pcm_to_mel(self.h, C.c_void_p(pcm.ctypes.data), len(pcm), C.c_void_p(out.ctypes.data),
+                                    C.c_int64(out.size), C.byref(got)))
+        assert got.value == n_len
+        return out
+
+    # kernel-level entry points on device pointers (parity tests)
+    def test_linear(self, layer, which, x_ptr, M, y_ptr, stream=None):
+        _check(lib().q2a_test_linear(self.h, layer, which, C.c_void_p(x_ptr), M, C.c_void_p(y_ptr),
+                                     C.c_void_p(stream) if stream else None))
+
+    def test_block(self, layer, x_ptr, n_clips, stream=None):
+        _check(lib().q2a_test_block(self.h, layer, C.c_void_p(x_ptr), n_clips, C.c_void_p(stream) if stream else None))
+
+    def test_attention(self, q_ptr, k_ptr, v_ptr, n_clips, out_ptr, stream=None):
+        _check(lib().q2a_test_attention(self.h, C.c_void_p(q_ptr), C.c_void_p(k_ptr), C.c_void_p(v_ptr), n_clips,
+                                        C.c_void_p(out_ptr), C.c_void_p(stream) if stream else None))
+
+
+def pack_model(path: str) -> bytes:
+    """Pack a model file into the device-layout blob (host bytes), e.g. for an RCCL broadcast."""
+    p = C.c_void_p()
+    n = lib().q2a_pack_model(path.encode(), C.byref(p))
+    if n < 0:
+        raise Q2AError(lib().q2a_last_error().decode())
+    try:
+        return C.string_at(p, n)
+    finally:
+        lib().q2a_free_host_blob(p)

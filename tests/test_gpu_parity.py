@@ -1,0 +1,196 @@
+"""Parity of the HIP path (lib/libq2a.so through its C ABI) against the CPU oracle and the reference's golden
+vectors. All tests here need an MI355X."""
+import numpy as np
+import pytest
+
+from conftest import rel_errors
+import oracle_py
+from q2a import ggmlfile
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def engines(make_model):
+    import q2a
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    cache = {}
+
+    def get(cfg, wt):
+        if (cfg, wt) not in cache:
+            cache[(cfg, wt)] = q2a.Engine(make_model(cfg, wt), device=0)
+        return cache[(cfg, wt)]
+
+    yield get
+    for e in cache.values():
+        e.close()
+
+
+def _tensor_raw(mf, name):
+    return np.ascontiguousarray(mf.t(name).data)
+
+
+# ---------------------------------------------------------------- mel frontend
+@pytest.mark.parametrize("clip", [0, 2, 3])
+def test_mel_matches_oracle(engines, make_model, make_clip, golden, clip):
+    meta, g = golden
+    e = engines("tiny", "f16")
+    pcm = make_clip(clip)
+    mel = e.pcm_to_mel(pcm)
+    orc = oracle_py.Oracle(ggmlfile.read(make_model("tiny", "f16"))).log_mel(pcm)
+    assert mel.shape == orc.shape
+    diff = np.abs(mel - orc)
+    # same FFT recursion / op order as the reference; only double log10 ulps could differ
+    assert diff.max() <= 1e-6, diff.max()
+    assert (diff == 0).mean() > 0.999
+    assert np.array_equal(mel.reshape(-1)[g[f"mel{clip}_idx"]] == g[f"mel{clip}_val"],
+                          np.ones(len(g[f"mel{clip}_idx"]), bool)) or np.abs(
+        mel.reshape(-1)[g[f"mel{clip}_idx"]] - g[f"mel{clip}_val"]).max() <= 1e-6
+
+
+# ---------------------------------------------------------------- weight GEMMs (ggml activation conversion)
+@pytest.mark.parametrize("wt", ["f16", "q4_k", "q8_0", "q4_0"])
+@pytest.mark.parametrize("which", [0, 1, 2, 3])
+def test_linear_matches_oracle(engines, make_model, wt, which):
+    e = engines("tiny", wt)
+    mf = ggmlfile.read(make_model("tiny", wt))
+    D, F = 256, 1024
+    K = F if which == 3 else D
+    names = {0: ["self_attn.q_proj.weight", "self_attn.k_proj.weight", "self_attn.v_proj.weight"],
+             1: ["self_attn.out_proj.weight"], 2: ["fc1.weight"], 3: ["fc2.weight"]}[which]
+    w = np.concatenate([_tensor_raw(mf, f"layers.1.{n}") for n in names])
+    N = {0: 3 * D, 1: D, 2: F, 3: D}[which]
+    M = 1500 + 37   # ragged row tail
+    rng = np.random.default_rng(which)
+    x = (rng.standard_normal((M, K)) * (1.0 if which != 3 else 0.3)).astype(np.float32)
+    xd = torch.from_numpy(x).cuda()
+    yd = torch.empty((M, N), dtype=torch.float32, device="cuda")
+    e.test_linear(1, which, xd.data_ptr(), M, yd.data_ptr())
+    torch.cuda.synchronize()
+    y = yd.cpu().numpy()
+    ref = oracle_py.gemm(mf.wtype, w, x, N)
+    mx, l2 = rel_errors(y, ref)
+    # identical integer / fp16-exact products; only fp32 summation order differs
+    assert mx < 1e-5 and l2 < 1e-6, (mx, l2)
+
+
+# ---------------------------------------------------------------- attention vs a plain PyTorch fp32 reference
+def test_attention_matches_fp32_reference(engines):
+    e = engines("tiny", "f16")
+    T, D, H = 1500, 256, 4
+    B = 2
+    g = torch.Generator(device="cpu").manual_seed(0)
+    q = (torch.randn(B * T, D, generator=g) * 0.5).cuda()
+    k = (torch.randn(B * T, D, generator=g) * 1.5).cuda()
+    v = torch.randn(B * T, D, generator=g).cuda()
+    out = torch.empty_like(q)
+    e.test_attention(q.data_ptr(), k.data_ptr(), v.data_ptr(), B, out.data_ptr())
+    torch.cuda.synchronize()
+    qh = q.view(B, T, H, 64).permute(0, 2, 1, 3).double()
+    kh = k.view(B, T, H, 64).permute(0, 2, 1, 3).double()
+    vh = v.view(B, T, H, 64).permute(0, 2, 1, 3).double()
+    p = torch.softmax(qh @ kh.transpose(-1, -2), dim=-1)
+    ref = (p @ vh).permute(0, 2, 1, 3).reshape(B * T, D).float()
+    mx, l2 = rel_errors(out.cpu().numpy(), ref.cpu().numpy())
+    # split-precision QK^T is F32-class; P and V enter the PV MFMA as fp16 (rel. 2^-11 each)
+    assert mx < 2e-3 and l2 < 5e-4, (mx, l2)
+
+
+# ---------------------------------------------------------------- end to end, tiny model
+def _encode(e, clips):
+    out, st = e.encode_host(clips)
+    return out, st
+
+
+def test_encoder_tiny_f16_vs_reference(engines, make_clip, golden):
+    _, g = golden
+    e = engines("tiny", "f16")
+    out, st = _encode(e, [make_clip(0)])
+    assert st[0] == 0
+    mx, l2 = rel_errors(out[0], g["tiny_f16_c0"])
+    assert mx < 1e-3 and l2 < 1e-4, (mx, l2)
+
+
+@pytest.mark.parametrize("wt", ["q4_k", "q8_0", "q4_0"])
+def test_encoder_tiny_quantized_vs_reference(engines, make_clip, golden, wt):
+    meta, g = golden
+    e = engines("tiny", wt)
+    out, st = _encode(e, [make_clip(0)])
+    mx, l2 = rel_errors(out[0][g["rows_stride5"]], g[f"tiny_{wt}_c0_rows"])
+    # activation re-quantization makes single int8 flips unavoidable (see test_oracle_golden)
+    assert l2 < 1e-3 and mx < 5e-3, (mx, l2)
+
+
+def test_batch_equals_single_and_edge_clips(engines, make_clip, golden):
+    """Ragged batch: two 30 s clips, a 7.3 s clip and a 41 s clip in one batch must equal the clips encoded
+    alone, bit for bit (no cross-clip state), and match the reference outputs for each length."""
+    _, g = golden
+    e = engines("tiny", "f16")
+    clips = [make_clip(c) for c in (0, 1, 2, 3)]
+    outb, st = _encode(e, clips)
+    assert list(st) == [0, 0, 0, 0]
+    for i, c in enumerate((0, 1, 2, 3)):
+        single, _ = _encode(e, [clips[i]])
+        assert np.array_equal(single[0], outb[i]), f"clip {c} differs between batch and single"
+        ref = g["tiny_f16_c0"][g["rows_stride5"]] if c == 0 else g[f"tiny_f16_c{c}_rows"]
+        mx, l2 = rel_errors(outb[i][g["rows_stride5"]], ref)
+        assert mx < 1e-3 and l2 < 1e-4, (c, mx, l2)
+
+
+def test_short_audio_is_skipped_like_reference(engines, make_clip):
+    """< 1 s after the offset: the reference returns 0 without encoding (qwen2-whisper.cpp:2359-2365)."""
+    e = engines("tiny", "f16")
+    sentinel = np.full((2,) + e.out_shape, 7.0, dtype=np.float32)
+    out, st = e.encode_host([make_clip(5, 12000), make_clip(0)], out=sentinel.copy())
+    assert st[0] == 1 and st[1] == 0
+    assert np.all(out[0] == 7.0)
+    assert not np.all(out[1] == 7.0)
+
+
+def test_device_blob_path_matches_file_path(engines, make_model, make_clip):
+    """The multi-GPU path (pack on host -> device copy (RCCL broadcast) -> open on the device blob) must give
+    bit-identical outputs to opening the file."""
+    import q2a
+    path = make_model("tiny", "q4_k")
+    blob = q2a.pack_model(path)
+    dev = torch.frombuffer(bytearray(blob), dtype=torch.uint8).cuda()
+    e2 = q2a.Engine(device=0, device_blob=dev.data_ptr(), blob_size=len(blob))
+    clip = make_clip(0)
+    a, _ = engines("tiny", "q4_k").encode_host([clip])
+    b, _ = e2.encode_host([clip])
+    e2.close()
+    assert np.array_equal(a, b)
+
+
+def test_encoder_tiny_matches_oracle_intermediate_free(engines, make_model, make_clip):
+    """Oracle (CPU restatement) on a second clip, full output compared."""
+    e = engines("tiny", "f16")
+    mf = ggmlfile.read(make_model("tiny", "f16"))
+    o = oracle_py.Oracle(mf)
+    pcm = make_clip(1)
+    ref = o.encode(o.mel_window(o.log_mel(pcm)))
+    out, _ = _encode(e, [pcm])
+    mx, l2 = rel_errors(out[0], ref)
+    assert mx < 1e-3 and l2 < 1e-4, (mx, l2)
+
+
+# ---------------------------------------------------------------- full size (L=32, D=1280, H=20)
+@pytest.mark.parametrize("wt", ["f16", "q4_k"])
+def test_encoder_full_size_vs_reference_samples(engines, make_clip, golden, wt):
+    meta, g = golden
+    e = engines("full", wt)
+    out, st = _encode(e, [make_clip(0)])
+    o = out[0].reshape(-1)
+    val = g[f"full_{wt}_c0_val"]
+    d = o[g[f"full_{wt}_c0_idx"]] - val
+    mxs = np.abs(d).max() / np.abs(val).max()
+    l2s = np.linalg.norm(d) / np.linalg.norm(val)
+    rn = np.linalg.norm(out[0].astype(np.float64), axis=1)
+    rnerr = np.abs(rn - g[f"full_{wt}_c0_rownorm"]).max() / g[f"full_{wt}_c0_rownorm"].max()
+    if wt == "f16":
+        assert mxs < 1e-3 and l2s < 1e-3 and rnerr < 1e-4, (mxs, l2s, rnerr)
+    else:
+        assert l2s < 2e-2 and rnerr < 2e-3, (mxs, l2s, rnerr)
