@@ -1,0 +1,253 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X encoder hot path (BASELINE.json metric: encoder audio-frames/s on 30 s clips).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config {q4k64,f16x1,f16x64,q80x64}]
+
+A "step" = one pass of the hot path (PCM -> log-mel -> conv -> 32 blocks -> pool+LN) over one batch of
+synthetic 30 s / 16 kHz clips per GPU, PCM already resident in HBM when the timed region starts.
+Default workload = BASELINE.json configs[2] ("batch=64 30 s clips, Q4_K quantized weights, 1xMI355X"); at N
+GPUs every rank runs its own 64 clips (weak scaling; N=8 is configs[3], batch=512 sharded 64/GPU). Weights are
+synthetic (deterministic splitmix64 generator at the real Qwen2-Audio encoder shapes), generated and quantized
+on rank 0, packed into the device layout and broadcast to every rank with one RCCL broadcast.
+
+Prints ONE JSON line on rank 0. Multi-GPU: torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes as C
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "qwen2-audio-whisper-ggml_amd")
+sys.path.insert(0, PKG)
+
+CONFIGS = {
+    # name: (ggml weight type, clips per GPU, BASELINE.json config it reproduces)
+    "q4k64": ("q4_k", 64, "configs[2]: batch=64 30 s clips, Q4_K quantized weights, 1xMI355X per rank"),
+    "f16x1": ("f16", 1, "configs[1]: single 30 s synthetic 16 kHz clip, fp16 weights, 1xMI355X per rank"),
+    "f16x64": ("f16", 64, "batch=64 30 s clips, fp16 weights (F16 path at the configs[2] batch)"),
+    "q80x64": ("q8_0", 64, "batch=64 30 s clips, Q8_0 weights (exact Q8_0 x Q8_0 contract)"),
+}
+T_MEL = 3000              # mel frames per 30 s clip (10 ms hop) -> the metric's "audio frame"
+N_SAMPLES = 480000
+# algorithmic work per clip: 2 273.77 GFLOP; weight GEMMs 1 887.44; attention 368.64; conv 17.69
+D, F, T, L = 1280, 5120, 1500, 32
+FLOP_FC1_PER_CLIP = 2.0 * T * F * D
+FLOP_WEIGHT_GEMMS_PER_CLIP = 2.0 * T * (3 * D * D + D * D + F * D + D * F) * L
+FLOP_PER_CLIP = FLOP_WEIGHT_GEMMS_PER_CLIP + 2 * 2.0 * T * T * D * L + 2.0 * (2 * T) * D * 384 + 2.0 * T * D * 3 * D
+PEAK_FP16_MFMA_TFLOPS = 2500.0    # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md, chip table)
+PROF_NAMES = ["mel", "conv1", "conv2", "layernorm", "gemm_qkv", "attention", "quant_act", "gemm_o", "gemm_fc1",
+              "gemm_fc2", "pool_ln"]
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    return ws, rank, local
+
+
+def make_model(wt: str, workdir: str, threads: int) -> str:
+    import q2a
+    base = os.path.join(workdir, "full-f16.bin")
+    if not os.path.exists(base):
+        subprocess.check_call([q2a.TOOL_PATH, "gen-model", base, "full", "f16", "0x51A2", str(threads)])
+    if wt == "f16":
+        return base
+    path = os.path.join(workdir, f"full-{wt}.bin")
+    if not os.path.exists(path):
+        subprocess.check_call([q2a.TOOL_PATH, "quantize", base, path, wt, str(threads)])
+    return path
+
+
+def synth_clips(first: int, n: int) -> np.ndarray:
+    host = C.CDLL(os.path.join(PKG, "lib", "libq2a_host.so"))
+    out = np.empty((n, N_SAMPLES), dtype=np.float32)
+    for i in range(n):
+        host.q2a_synth_clip(C.c_void_p(out[i].ctypes.data), C.c_int64(N_SAMPLES), C.c_int(first + i))
+    return out
+
+
+def cpu_baseline(model_path: str, workdir: str, threads: int, reps: int) -> dict | None:
+    """The reference ggml CPU path (oracle/_ref/ref_harness, compiled from /root/reference sources with
+    -O3 -march=x86-64-v3) on one synthetic 30 s clip per rep, on the host cores of this box."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness):
+        return None
+    clip = os.path.join(workdir, "clip0.f32")
+    synth_clips(0, 1)[0].tofile(clip)
+    outp = os.path.join(workdir, "ref_out.f32")
+    try:
+        r = subprocess.run([harness, "encode", model_path, clip, outp, str(threads), str(reps)], check=True,
+                           capture_output=True, text=True, timeout=600)
+    except Exception as ex:  # noqa: BLE001
+        log("cpu baseline failed:", ex)
+        return None
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    return {"value": round(T_MEL / info["mean_s"], 2), "unit": "audio-frames/s", "cores": threads,
+            "kind": "reference",
+            "sample": f"{reps} x one 30 s clip through whisper_full (ggml CPU backend, n_threads={threads}, "
+                      f"-O3 -march=x86-64-v3), mean {info['mean_s']:.2f} s/clip"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="q4k64", choices=sorted(CONFIGS))
+    ap.add_argument("--clips", type=int, default=0, help="override clips per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-reps", type=int, default=2)
+    ap.add_argument("--workdir", default=os.environ.get("Q2A_BENCH_DIR", os.path.join(tempfile.gettempdir(), "q2a_bench")))
+    args = ap.parse_args()
+
+    ws, rank, local = dist_env()
+    import torch
+    torch.cuda.set_device(local)
+    dist = None
+    if ws > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import q2a
+
+    wt, clips_per_gpu, workload = CONFIGS[args.config]
+    if args.clips:
+        clips_per_gpu = args.clips
+    threads = min(16, os.cpu_count() or 8)
+    os.makedirs(args.workdir, exist_ok=True)
+
+    # ---- model: rank 0 generates + quantizes + packs; one RCCL broadcast of the packed blob over xGMI
+    t0 = time.time()
+    size_t = torch.zeros(1, dtype=torch.int64, device="cuda")
+    model_path = None
+    blob_host = None
+    if rank == 0:
+        model_path = make_model(wt, args.workdir, threads)
+        t_gen = time.time() - t0
+        blob_host = q2a.pack_model(model_path)
+        size_t[0] = len(blob_host)
+    if dist is not None:
+        dist.broadcast(size_t, 0)
+    nbytes = int(size_t.item())
+    blob = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    if rank == 0:
+        blob.copy_(torch.frombuffer(bytearray(blob_host), dtype=torch.uint8))
+        del blob_host
+    torch.cuda.synchronize()
+    t_bcast = 0.0
+    if dist is not None:
+        dist.barrier()
+        tb = time.time()
+        dist.broadcast(blob, 0)
+        torch.cuda.synchronize()
+        t_bcast = time.time() - tb
+    eng = q2a.Engine(device=local, device_blob=blob.data_ptr(), blob_size=nbytes)
+    eng.reserve(clips_per_gpu)
+    t_setup = time.time() - t0
+
+    # ---- inputs resident in HBM before the timed region (each rank its own clips)
+    pcm = torch.from_numpy(synth_clips(rank * clips_per_gpu, clips_per_gpu)).cuda()
+    out = torch.empty((clips_per_gpu,) + eng.out_shape, dtype=torch.float32, device="cuda")
+    ns = [N_SAMPLES] * clips_per_gpu
+
+    def step():
+        eng.encode_device(pcm.data_ptr(), N_SAMPLES, ns, out.data_ptr())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    lib = q2a.lib()
+    lib.q2a_profile_enable(C.c_void_p(eng.h), 1)
+    prof_ms = (C.c_double * 11)()
+    prof_n = (C.c_int64 * 11)()
+    lib.q2a_profile_read(C.c_void_p(eng.h), prof_ms, prof_n, 11, 1)
+
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ts = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - ts
+    lib.q2a_profile_read(C.c_void_p(eng.h), prof_ms, prof_n, 11, 0)
+    lib.q2a_profile_enable(C.c_void_p(eng.h), 0)
+    assert torch.isfinite(out).all().item(), "non-finite encoder output"
+
+    el = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    if dist is not None:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    elapsed = float(el.item())
+    total_clips = clips_per_gpu * ws * args.steps
+    value = total_clips * T_MEL / elapsed
+
+    if rank != 0:
+        eng.close()
+        if dist is not None:
+            dist.destroy_process_group()
+        return
+
+    per_kernel = {PROF_NAMES[i]: {"ms_per_step": round(prof_ms[i] / args.steps, 3),
+                                  "launches_per_step": int(prof_n[i] // args.steps)} for i in range(11)}
+    # dominant kernel: the fc1 weight GEMM (largest single GEMM; its own kernel instantiation in rocprof)
+    fc1_avg_s = prof_ms[8] / max(1, prof_n[8]) / 1e3
+    fc1_flop = FLOP_FC1_PER_CLIP * clips_per_gpu
+    achieved = fc1_flop / fc1_avg_s / 1e12
+    gemm_ms = prof_ms[4] + prof_ms[7] + prof_ms[8] + prof_ms[9]
+    gemm_tf = FLOP_WEIGHT_GEMMS_PER_CLIP * clips_per_gpu * args.steps / (gemm_ms / 1e3) / 1e12
+
+    cpu = None
+    if ws == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(model_path, args.workdir, threads, args.cpu_reps)
+
+    res = {
+        "metric": "encoder audio-frames/sec (30 s clips) at 1/2/4/8 MI355X; MFMA util %",
+        "value": round(value, 1),
+        "unit": "audio-frames/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": {"q4_k": "q4_k x q8_k integer dots on fp16 MFMA (fp32 acc)", "f16": "fp16 MFMA (fp32 acc)",
+                  "q8_0": "q8_0 x q8_0 integer dots on fp16 MFMA (fp32 acc)"}[wt],
+        "data": "synthetic (deterministic 30 s / 16 kHz clips; random-init weights at Qwen2-Audio encoder shapes)",
+        "config": {"workload": workload, "model": "qwen2-audio-encoder L32 D1280 H20 F5120 (synthetic weights)",
+                   "weights": wt, "clips_per_gpu": clips_per_gpu, "global_batch": clips_per_gpu * ws,
+                   "seq_len": T_MEL, "parallelism": f"dp{ws}"},
+        "clips_per_s": round(total_clips / elapsed, 3),
+        "tflops_total": round(FLOP_PER_CLIP * total_clips / elapsed / 1e12, 1),
+        "roofline": {"bound": "mfma", "kernel": "gemm_fc1 (k_gemm<GELU, blk>), M=%d N=5120 K=1280" % (T * clips_per_gpu),
+                     "achieved": round(achieved, 1), "peak": PEAK_FP16_MFMA_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_FP16_MFMA_TFLOPS, 4), "traffic": None,
+                     "flop_per_launch": fc1_flop, "avg_launch_ms": round(fc1_avg_s * 1e3, 4),
+                     "all_weight_gemms_tflops": round(gemm_tf, 1)},
+        "cpu_baseline": cpu,
+        "per_kernel": per_kernel,
+        "setup_s": {"total": round(t_setup, 1), "rccl_weight_broadcast": round(t_bcast, 4), "weight_blob_bytes": nbytes},
+    }
+    print(json.dumps(res), flush=True)
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

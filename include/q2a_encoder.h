@@ -86,6 +86,15 @@ int q2a_encode_host(q2a_engine * e, const float * const * pcm, const int32_t * n
  * mel_cap floats) and *n_len. Runs the same kernels as the encoder on the engine's device. */
 int q2a_pcm_to_mel(q2a_engine * e, const float * pcm, int n_samples, float * mel_out, int64_t mel_cap, int * n_len);
 
+/* ---- per-kernel timing (HIP events recorded on the launch stream around every kernel of a class) ---- */
+enum {
+    Q2A_PROF_MEL = 0, Q2A_PROF_CONV1, Q2A_PROF_CONV2, Q2A_PROF_LN, Q2A_PROF_GEMM_QKV, Q2A_PROF_ATTN,
+    Q2A_PROF_QUANT, Q2A_PROF_GEMM_O, Q2A_PROF_GEMM_FC1, Q2A_PROF_GEMM_FC2, Q2A_PROF_POOL, Q2A_PROF_CLASSES
+};
+int q2a_profile_enable(q2a_engine * e, int on);
+/* accumulated milliseconds and launch counts per class (waits for the recorded events); reset != 0 clears */
+int q2a_profile_read(q2a_engine * e, double * ms, int64_t * counts, int n, int reset);
+
 /* ---- kernel-level entry points (device pointers), used by the parity tests ------------------------------ */
 /* Y[M][N] = X[M][K] . W[N][K]^T for one linear weight of the loaded model (layer `layer`, which = 0 qkv
  * (raw, no bias/scale), 1 out_proj, 2 fc1, 3 fc2), with ggml's activation conversion of X (fp16 / Q8_K / Q8_0). */

@@ -374,6 +374,14 @@ struct q2a_engine {
     float * hF = nullptr;
     int TP = 0;
 
+    // optional per-kernel-class timing with HIP events on the launch stream (q2a_profile_*)
+    bool prof = false;
+    struct rec { int cls; hipEvent_t a, b; };
+    std::vector<rec> pending;
+    std::vector<hipEvent_t> pool;
+    double prof_ms[Q2A_PROF_CLASSES] = {};
+    int64_t prof_n[Q2A_PROF_CLASSES] = {};
+
     template <class P> P g(int i) const { return (P) (blob + h.goff[i]); }
     template <class P> P lv(int l, int i) const { return (P) (blob + h.loff[l][i]); }
     const uint64_t * mat(int l, int w) const { return h.loff[l] + L_MAT0 + w * A_COUNT; }
@@ -493,6 +501,26 @@ q2a_gemm_args gemm_base(const q2a_engine * e, int l, int which, const q2a_half *
     return a;
 }
 
+hipEvent_t prof_event(q2a_engine * e) {
+    if (!e->pool.empty()) { hipEvent_t ev = e->pool.back(); e->pool.pop_back(); return ev; }
+    hipEvent_t ev = nullptr;
+    (void) hipEventCreate(&ev);
+    return ev;
+}
+
+// Launch `call` on stream s; when profiling, bracket it with an event pair attributed to class cls.
+#define PLAUNCH(e, s, cls, call)                                                      \
+    do {                                                                              \
+        q2a_engine::rec r_{cls, nullptr, nullptr};                                    \
+        if ((e)->prof) { r_.a = prof_event(e); r_.b = prof_event(e); (void) hipEventRecord(r_.a, s); } \
+        hipError_t e_ = (call);                                                       \
+        if (e_ != hipSuccess) {                                                       \
+            set_err("%s: %s", #call, hipGetErrorString(e_));                        \
+            return Q2A_ERR_HIP;                                                       \
+        }                                                                             \
+        if ((e)->prof) { (void) hipEventRecord(r_.b, s); (e)->pending.push_back(r_); } \
+    } while (0)
+
 int ln_mode(const q2a_engine * e) { return e->blk == 0 ? 0 : e->blk == 256 ? 1 : 2; }
 
 #define LAUNCH(x)                                                                     \
@@ -510,49 +538,49 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
     const int M = B * d.T;
     const int mode = ln_mode(e);
     q2a_ln_args ln{e->X, M, d.D, e->lv<const float *>(l, L_LN1W), e->lv<const float *>(l, L_LN1B), mode, e->actD, e->dyD, e->aextD};
-    LAUNCH(q2a_launch_layernorm(ln, s));
+    PLAUNCH(e, s, Q2A_PROF_LN, q2a_launch_layernorm(ln, s));
     {
         q2a_gemm_args a = gemm_base(e, l, 0, e->actD, M);
         a.bias = e->lv<const float *>(l, L_BQKV);
         a.qh = e->qh; a.ql = e->ql; a.kh = e->kh; a.kl = e->kl; a.vt = e->vt;
         a.qscale = 1.0f / sqrtf((float) (d.D / d.H));
-        LAUNCH(q2a_launch_gemm(a, Q2A_EPI_QKV, e->blk, s));
+        PLAUNCH(e, s, Q2A_PROF_GEMM_QKV, q2a_launch_gemm(a, Q2A_EPI_QKV, e->blk, s));
     }
     {
         q2a_attn_args at{e->qh, e->ql, e->kh, e->kl, e->vt, B, d.T, d.D, d.H, e->TP, nullptr, nullptr};
         if (mode == 0) at.outH = e->actD; else at.outF = e->attF;
-        LAUNCH(q2a_launch_attention(at, s));
+        PLAUNCH(e, s, Q2A_PROF_ATTN, q2a_launch_attention(at, s));
         if (mode) {
             q2a_quant_args qa{e->attF, M, d.D, mode, e->actD, e->dyD, e->aextD};
-            LAUNCH(q2a_launch_quant_act(qa, s));
+            PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_quant_act(qa, s));
         }
     }
     {
         q2a_gemm_args a = gemm_base(e, l, 1, e->actD, M);
         a.bias = e->lv<const float *>(l, L_BO);
         a.outF = e->X; a.ldo = d.D;
-        LAUNCH(q2a_launch_gemm(a, Q2A_EPI_RESID, e->blk, s));
+        PLAUNCH(e, s, Q2A_PROF_GEMM_O, q2a_launch_gemm(a, Q2A_EPI_RESID, e->blk, s));
     }
     q2a_ln_args ln2{e->X, M, d.D, e->lv<const float *>(l, L_LN2W), e->lv<const float *>(l, L_LN2B), mode, e->actD, e->dyD, e->aextD};
-    LAUNCH(q2a_launch_layernorm(ln2, s));
+    PLAUNCH(e, s, Q2A_PROF_LN, q2a_launch_layernorm(ln2, s));
     {
         q2a_gemm_args a = gemm_base(e, l, 2, e->actD, M);
         a.bias = e->lv<const float *>(l, L_B1);
         if (mode == 0) {
             a.outH = e->actF; a.ldo = d.F; a.o_rpg = M; a.o_gstride = 0; a.o_off = 0;
-            LAUNCH(q2a_launch_gemm(a, Q2A_EPI_GELU_H, 0, s));
+            PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_H, 0, s));
         } else {
             a.outF = e->hF; a.ldo = d.F;
-            LAUNCH(q2a_launch_gemm(a, Q2A_EPI_GELU_F, e->blk, s));
+            PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_F, e->blk, s));
             q2a_quant_args qa{e->hF, M, d.F, mode, e->actF, e->dyF, e->aextF};
-            LAUNCH(q2a_launch_quant_act(qa, s));
+            PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_quant_act(qa, s));
         }
     }
     {
         q2a_gemm_args a = gemm_base(e, l, 3, e->actF, M);
         a.bias = e->lv<const float *>(l, L_B2);
         a.outF = e->X; a.ldo = d.D;
-        LAUNCH(q2a_launch_gemm(a, Q2A_EPI_RESID, e->blk, s));
+        PLAUNCH(e, s, Q2A_PROF_GEMM_FC2, q2a_launch_gemm(a, Q2A_EPI_RESID, e->blk, s));
     }
     return Q2A_OK;
 }
@@ -569,7 +597,7 @@ int run_frontend(q2a_engine * e, const float * pcm, int64_t stride, int B, int m
     ma.n_mel = d.M; ma.n_bins = 201; ma.n_frames_win = d.TM; ma.max_frames = max_frames;
     ma.filters = e->g<const float *>(G_FILT); ma.tab = e->g<const float *>(G_TAB);
     ma.mel = e->mel; ma.clip_max = cmax; ma.xc1 = e->xc1;
-    LAUNCH(q2a_launch_mel(ma, s));
+    PLAUNCH(e, s, Q2A_PROF_MEL, q2a_launch_mel(ma, s));
     {   // conv1: implicit GEMM, A row t = xc1 rows t..t+2 of its clip (768 halves), K = 6M
         q2a_gemm_args a;
         memset(&a, 0, sizeof(a));
@@ -579,7 +607,7 @@ int run_frontend(q2a_engine * e, const float * pcm, int64_t stride, int B, int m
         a.bias = e->g<const float *>(G_CONV1_B);
         a.outH = e->y1; a.ldo = d.D; a.o_rpg = d.TM; a.o_gstride = d.TM + 1; a.o_off = 1;
         a.gelu_tab = e->g<const uint16_t *>(G_GELU);
-        LAUNCH(q2a_launch_gemm(a, Q2A_EPI_GELU_H, 0, s));
+        PLAUNCH(e, s, Q2A_PROF_CONV1, q2a_launch_gemm(a, Q2A_EPI_GELU_H, 0, s));
     }
     {   // conv2 (stride 2): A row t = y1 rows 2t..2t+2 (inputs 2t-1..2t+1), K = 3D; + pe
         q2a_gemm_args a;
@@ -590,7 +618,7 @@ int run_frontend(q2a_engine * e, const float * pcm, int64_t stride, int B, int m
         a.bias = e->g<const float *>(G_CONV2_B);
         a.outF = e->X; a.ldo = d.D; a.pe = e->g<const float *>(G_PE); a.T = d.T;
         a.gelu_tab = e->g<const uint16_t *>(G_GELU);
-        LAUNCH(q2a_launch_gemm(a, Q2A_EPI_CONV2, 0, s));
+        PLAUNCH(e, s, Q2A_PROF_CONV2, q2a_launch_gemm(a, Q2A_EPI_CONV2, 0, s));
     }
     return Q2A_OK;
 }
@@ -633,7 +661,7 @@ int encode_impl(q2a_engine * e, const float * pcm, int64_t stride, const int32_t
         if (rc) return rc;
     }
     q2a_pool_args pa{e->X, B, e->d.T, e->d.D, e->g<const float *>(G_LNP_W), e->g<const float *>(G_LNP_B), out, e->meta + 2 * B};
-    LAUNCH(q2a_launch_pool_ln(pa, s));
+    PLAUNCH(e, s, Q2A_PROF_POOL, q2a_launch_pool_ln(pa, s));
     return Q2A_OK;
 }
 
@@ -706,6 +734,8 @@ void q2a_close(q2a_engine * e) {
     (void) hipSetDevice(e->device);
     if (e->stream) (void) hipStreamSynchronize(e->stream);
     free_ws(e);
+    for (auto & r : e->pending) { (void) hipEventDestroy(r.a); (void) hipEventDestroy(r.b); }
+    for (auto ev : e->pool) (void) hipEventDestroy(ev);
     if (e->own_blob && e->blob) (void) hipFree(e->blob);
     if (e->stream) (void) hipStreamDestroy(e->stream);
     delete e;
@@ -802,6 +832,34 @@ int q2a_pcm_to_mel(q2a_engine * e, const float * pcm, int n_samples, float * mel
         mel_out[i] = (float) ((v + 4.0) / 4.0);
     }
     *n_len_out = n_len;
+    return Q2A_OK;
+}
+
+int q2a_profile_enable(q2a_engine * e, int on) {
+    if (!e) return Q2A_ERR_ARG;
+    e->prof = on != 0;
+    return Q2A_OK;
+}
+
+int q2a_profile_read(q2a_engine * e, double * ms, int64_t * counts, int n, int reset) {
+    if (!e || n < 0) return Q2A_ERR_ARG;
+    HIP_TRY(hipSetDevice(e->device));
+    for (auto & r : e->pending) {
+        HIP_TRY(hipEventSynchronize(r.b));
+        float t = 0.f;
+        HIP_TRY(hipEventElapsedTime(&t, r.a, r.b));
+        e->prof_ms[r.cls] += t;
+        e->prof_n[r.cls] += 1;
+        e->pool.push_back(r.a);
+        e->pool.push_back(r.b);
+    }
+    e->pending.clear();
+    for (int i = 0; i < n && i < Q2A_PROF_CLASSES; ++i) {
+        if (ms) ms[i] = e->prof_ms[i];
+        if (counts) counts[i] = e->prof_n[i];
+    }
+    if (reset)
+        for (int i = 0; i < Q2A_PROF_CLASSES; ++i) { e->prof_ms[i] = 0; e->prof_n[i] = 0; }
     return Q2A_OK;
 }
 
