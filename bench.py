@@ -211,6 +211,17 @@ def main():
     gemm_ms = prof_ms[4] + prof_ms[7] + prof_ms[8] + prof_ms[9]
     gemm_tf = FLOP_WEIGHT_GEMMS_PER_CLIP * clips_per_gpu * args.steps / (gemm_ms / 1e3) / 1e12
 
+    # HBM traffic of the same kernel from the committed rocprofv3 PMC passes of this workload (FETCH_SIZE and
+    # WRITE_SIZE in separate passes, FETCH_SIZE x2 gfx950 correction); null when no summary matches.
+    traffic, traffic_src = None, None
+    pmc_files = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith(f"_{args.config}_pmc_traffic.json")) \
+        if os.path.isdir(os.path.join(ROOT, "profiles")) else []
+    if pmc_files and clips_per_gpu == CONFIGS[args.config][1]:
+        with open(os.path.join(ROOT, "profiles", pmc_files[-1])) as f:
+            k = json.load(f)["kernels"].get("gemm_fc1", {})
+        if "hbm_bytes_per_launch_corrected" in k:
+            traffic, traffic_src = k["hbm_bytes_per_launch_corrected"], "profiles/" + pmc_files[-1]
+
     cpu = None
     if ws == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(model_path, args.workdir, threads, args.cpu_reps)
@@ -236,7 +247,8 @@ def main():
         "tflops_total": round(FLOP_PER_CLIP * total_clips / elapsed / 1e12, 1),
         "roofline": {"bound": "mfma", "kernel": "gemm_fc1 (k_gemm<GELU, blk>), M=%d N=5120 K=1280" % (T * clips_per_gpu),
                      "achieved": round(achieved, 1), "peak": PEAK_FP16_MFMA_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_FP16_MFMA_TFLOPS, 4), "traffic": None,
+                     "frac": round(achieved / PEAK_FP16_MFMA_TFLOPS, 4), "traffic": traffic,
+                     "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                      "flop_per_launch": fc1_flop, "avg_launch_ms": round(fc1_avg_s * 1e3, 4),
                      "all_weight_gemms_tflops": round(gemm_tf, 1)},
         "cpu_baseline": cpu,
