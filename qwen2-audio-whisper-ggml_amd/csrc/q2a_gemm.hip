@@ -10,11 +10,16 @@
 // only the fp32 summation order differs from ggml. For the k-quant formats the integer per-block sums are kept
 // in a fresh accumulator per K-block and combined with ggml's scale formula (ggml-quants.c:7795-7858).
 //
-// Tiling: 128x128x64 per 256-thread workgroup (2x2 waves, 64x64 per wave = 4x4 MFMA tiles), LDS operand images
-// filled by global_load_lds_dwordx4 (16 B/lane, lane-linear LDS destination) with the XOR swizzle applied on the
-// global SOURCE address and undone on the ds_read (cdna_hip_programming.md §5.4 rule 21), two LDS stages.
-// Workgroup -> tile order is XCD-aware (bijective remap; neighbouring N tiles of one A panel share an XCD L2).
+// Tiling (template): BM x BN x 64 per workgroup of WM x WN waves; each wave owns a (BM/WM) x (BN/WN) block of
+// 16x16 MFMA tiles. Large batches use 256x256 tiles with 8 waves (128x64 per wave: each A fragment feeds 4 MFMAs,
+// each W fragment 8), small ones 128x128 with 4 waves. LDS operand images are filled by global_load_lds_dwordx4
+// (16 B/lane, lane-linear destination) with the XOR swizzle applied on the global SOURCE address and undone on the
+// ds_read (cdna_hip_programming.md §5.4 rule 21); two LDS stages, the next stage's loads issued before the MFMAs
+// of the current one. Workgroups are remapped XCD-contiguously (bijective) and rasterised in groups of 8 M-tiles
+// per N column so the tiles resident on one XCD share A and W panels through its L2.
 #include "q2a_internal.h"
+
+#include <cstdlib>
 
 namespace {
 
@@ -23,8 +28,9 @@ typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void * lds_ptr_t;
 
-constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int BK = 64;
 constexpr int ROWB = BK * 2;   // bytes per LDS row (64 halves)
+constexpr int GROUP_M = 8;
 
 __device__ __forceinline__ float gelu_lut(float x, const uint16_t * tab) {
     // ggml_vec_gelu_f32 with GGML_GELU_FP16 (ggml.c:2556-2570)
@@ -80,144 +86,138 @@ __device__ __forceinline__ void epilogue_store(const q2a_gemm_args & p, int m, i
     }
 }
 
-// Stage one BM x BK A tile and one BN x BK W tile into LDS buffer `buf` (fp16 elements) for K offset k0.
-__device__ __forceinline__ void stage(const q2a_gemm_args & p, char * lds_buf, const int64_t * arow, const int64_t * wrow,
-                                      int k0, int wave, int lane) {
-    const int c = lane & 7;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = wave * 32 + i * 8 + (lane >> 3);
-        const int sc = c ^ (r & 7);
-        const q2a_half * src = p.A + arow[i] + k0 + sc * 8;
-        __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (lds_buf + (wave * 32 + i * 8) * ROWB), 16, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = wave * 32 + i * 8 + (lane >> 3);
-        const int sc = c ^ (r & 7);
-        const q2a_half * src = p.W + wrow[i] + k0 + sc * 8;
-        __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (lds_buf + (BM + wave * 32 + i * 8) * ROWB), 16, 0, 0);
-    }
-}
-
 __device__ __forceinline__ half8 frag(const char * img, int row, int chunk) {
     return *(const half8 *) (img + row * ROWB + ((chunk ^ (row & 7)) << 4));
 }
 
-template <int EPI, int BLK>
-__global__ __launch_bounds__(256, 2) void k_gemm(const q2a_gemm_args p) {
-    __shared__ __attribute__((aligned(16))) char lds[2][(BM + BN) * ROWB];   // 2 x 32 KiB
+template <int BM, int BN, int WM, int WN, int EPI, int BLK>
+__global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p) {
+    constexpr int NW = WM * WN;
+    constexpr int MI = BM / WM / 16, NJ = BN / WN / 16;   // 16x16 tiles per wave
+    constexpr int LA = BM / 8 / NW, LB = BN / 8 / NW;     // glds instructions per wave per stage
+    static_assert(LA >= 1 && LB >= 1, "tile too small for the wave count");
+    __shared__ __attribute__((aligned(16))) char lds[2][(BM + BN) * ROWB];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
+    const int wm = wave / WN, wn = wave % WN;
 
-    // XCD-aware bijective remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective")
+    // XCD-contiguous bijective remap, then grouped rasterisation (GROUP_M M-tiles per N column)
     const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, nwg = nbn * nbm;
     const int bid = blockIdx.x, xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
     const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
-    const int tn = wgid % nbn, tm = wgid / nbn;
+    const int gsize = GROUP_M * nbn, g = wgid / gsize, gr = wgid % gsize;
+    const int gm = min(GROUP_M, nbm - g * GROUP_M);
+    const int tm = g * GROUP_M + gr % gm, tn = gr / gm;
     const int m0 = tm * BM, n0 = tn * BN;
 
-    // per-lane source rows for the 4+4 glds instructions of this wave (rows past M clamp to M-1: loaded, never stored)
-    int64_t arow[4], wrow[4];
+    // per-lane source rows of this wave's glds instructions (rows past M clamp to M-1: loaded, never stored)
+    int64_t arow[LA], wrow[LB];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int r = wave * 32 + i * 8 + (lane >> 3);
-        arow[i] = a_row_off(p, min(m0 + r, p.M - 1));
-        wrow[i] = (int64_t) (n0 + r) * p.ldw;
+    for (int i = 0; i < LA; ++i) {
+        const int r = (wave * LA + i) * 8 + (lane >> 3);
+        arow[i] = a_row_off(p, min(m0 + r, p.M - 1)) + (((lane & 7) ^ (r & 7)) << 3);
     }
+#pragma unroll
+    for (int i = 0; i < LB; ++i) {
+        const int r = (wave * LB + i) * 8 + (lane >> 3);
+        wrow[i] = (int64_t) (n0 + r) * p.ldw + (((lane & 7) ^ (r & 7)) << 3);
+    }
+    auto stage = [&](char * buf, int k0) {
+#pragma unroll
+        for (int i = 0; i < LA; ++i)
+            __builtin_amdgcn_global_load_lds((const void *) (p.A + arow[i] + k0),
+                                             (lds_ptr_t) (buf + (wave * LA + i) * 8 * ROWB), 16, 0, 0);
+#pragma unroll
+        for (int i = 0; i < LB; ++i)
+            __builtin_amdgcn_global_load_lds((const void *) (p.W + wrow[i] + k0),
+                                             (lds_ptr_t) (buf + (BM + (wave * LB + i) * 8) * ROWB), 16, 0, 0);
+    };
 
-    f4 acc[4][4];
+    f4 acc[MI][NJ];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-    f4 blk[4][4];
+        for (int j = 0; j < NJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    f4 blk[BLK ? MI : 1][BLK ? NJ : 1];
     if (BLK) {
 #pragma unroll
-        for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < (BLK ? MI : 1); ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+            for (int j = 0; j < (BLK ? NJ : 1); ++j) blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
     }
 
     const int nk = p.K / BK;
-    stage(p, lds[0], arow, wrow, 0, wave, lane);
+    stage(lds[0], 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
 
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
-        if (kt + 1 < nk) stage(p, lds[cur ^ 1], arow, wrow, (kt + 1) * BK, wave, lane);
+        if (kt + 1 < nk) stage(lds[cur ^ 1], (kt + 1) * BK);
         const char * ia = lds[cur];
         const char * iw = lds[cur] + BM * ROWB;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int chunk = s * 4 + (lane >> 4);
-            half8 a[4], b[4];
+            half8 b[NJ];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) a[i] = frag(ia, wm * 64 + i * 16 + (lane & 15), chunk);
+            for (int j = 0; j < NJ; ++j) b[j] = frag(iw, wn * (BN / WN) + j * 16 + (lane & 15), chunk);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) b[j] = frag(iw, wn * 64 + j * 16 + (lane & 15), chunk);
-            if (BLK == 0) {
+            for (int i = 0; i < MI; ++i) {
+                const half8 a = frag(ia, wm * (BM / WM) + i * 16 + (lane & 15), chunk);
 #pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
-            } else {
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) blk[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], blk[i][j], 0, 0, 0);
+                for (int j = 0; j < NJ; ++j) {
+                    if (BLK == 0) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[j], acc[i][j], 0, 0, 0);
+                    else blk[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[j], blk[i][j], 0, 0, 0);
+                }
+            }
+            if (BLK) {
                 const int kpos = kt * BK + (s + 1) * 32;   // K consumed so far
                 if (kpos % BLK == 0) {
                     const int kb = kpos / BLK - 1;
-                    float dy[4][4], dx[4], dm[4];
+                    float dx[NJ], dm[NJ];
 #pragma unroll
-                    for (int i = 0; i < 4; ++i)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int m = min(m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r, p.M - 1);
-                            dy[i][r] = p.dy[(int64_t) m * p.nblk + kb];
-                        }
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+                    for (int j = 0; j < NJ; ++j) {
+                        const int n = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
                         dx[j] = p.dx[(int64_t) n * p.nblk + kb];
                         if (BLK == 256) dm[j] = p.dmin[(int64_t) n * p.nblk + kb];
                     }
+                    half4 we[NJ];
                     if (BLK == 256) {
-                        // min term S2 = sum_j m_j * bsum32_j with one 16x16x16 MFMA per tile on (hi,lo) split bsums
-                        half4 ae[4], we[4];
 #pragma unroll
-                        for (int i = 0; i < 4; ++i) {
-                            const int m = min(m0 + wm * 64 + i * 16 + (lane & 15), p.M - 1);
-                            ae[i] = *(const half4 *) (p.aext + ((int64_t) m * p.nblk + kb) * 16 + (lane >> 4) * 4);
-                        }
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+                        for (int j = 0; j < NJ; ++j) {
+                            const int n = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
                             we[j] = *(const half4 *) (p.wext + ((int64_t) n * p.nblk + kb) * 16 + (lane >> 4) * 4);
                         }
+                    }
 #pragma unroll
-                        for (int i = 0; i < 4; ++i)
+                    for (int i = 0; i < MI; ++i) {
+                        float dy[4];
 #pragma unroll
-                            for (int j = 0; j < 4; ++j) {
-                                f4 s2 = __builtin_amdgcn_mfma_f32_16x16x16f16(ae[i], we[j], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                        for (int r = 0; r < 4; ++r) {
+                            const int m = min(m0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r, p.M - 1);
+                            dy[r] = p.dy[(int64_t) m * p.nblk + kb];
+                        }
+                        half4 ae;
+                        if (BLK == 256) {
+                            // min term S2 = sum_j m_j * bsum32_j: one 16x16x16 MFMA per tile on (hi,lo)-split bsums
+                            const int m = min(m0 + wm * (BM / WM) + i * 16 + (lane & 15), p.M - 1);
+                            ae = *(const half4 *) (p.aext + ((int64_t) m * p.nblk + kb) * 16 + (lane >> 4) * 4);
+                        }
+#pragma unroll
+                        for (int j = 0; j < NJ; ++j) {
+                            if (BLK == 256) {
+                                const f4 s2 = __builtin_amdgcn_mfma_f32_16x16x16f16(ae, we[j], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
 #pragma unroll
                                 for (int r = 0; r < 4; ++r) {
-                                    acc[i][j][r] += (dy[i][r] * dx[j]) * blk[i][j][r];
-                                    acc[i][j][r] -= (dy[i][r] * dm[j]) * s2[r];
+                                    acc[i][j][r] += (dy[r] * dx[j]) * blk[i][j][r];
+                                    acc[i][j][r] -= (dy[r] * dm[j]) * s2[r];
                                 }
-                                blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+                            } else {
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) acc[i][j][r] += (dx[j] * dy[r]) * blk[i][j][r];
                             }
-                    } else {
-#pragma unroll
-                        for (int i = 0; i < 4; ++i)
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) {
-#pragma unroll
-                                for (int r = 0; r < 4; ++r) acc[i][j][r] += (dx[j] * dy[i][r]) * blk[i][j][r];
-                                blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-                            }
+                            blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+                        }
                     }
                 }
             }
@@ -228,33 +228,44 @@ __global__ __launch_bounds__(256, 2) void k_gemm(const q2a_gemm_args p) {
 
     // epilogue: C layout of 16x16 tiles: col = lane & 15, row = (lane >> 4) * 4 + r
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-            const int m = m0 + wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+            const int m = m0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
             if (m >= p.M) continue;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int n = n0 + wn * 64 + j * 16 + (lane & 15);
+            for (int j = 0; j < NJ; ++j) {
+                const int n = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
                 epilogue_store<EPI>(p, m, n, acc[i][j][r]);
             }
         }
 }
 
+template <int BM, int BN, int WM, int WN, int EPI, int BLK>
+hipError_t launch_cfg(const q2a_gemm_args & a, hipStream_t s) {
+    const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM);
+    hipLaunchKernelGGL((k_gemm<BM, BN, WM, WN, EPI, BLK>), dim3(nwg), dim3(WM * WN * 64), 0, s, a);
+    return hipGetLastError();
+}
+
 template <int EPI>
 hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
-    const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM);
-    if (blk == 0) hipLaunchKernelGGL((k_gemm<EPI, 0>), dim3(nwg), dim3(256), 0, s, a);
-    else if (blk == 256) hipLaunchKernelGGL((k_gemm<EPI, 256>), dim3(nwg), dim3(256), 0, s, a);
-    else if (blk == 32) hipLaunchKernelGGL((k_gemm<EPI, 32>), dim3(nwg), dim3(256), 0, s, a);
-    else return hipErrorInvalidValue;
-    return hipGetLastError();
+    // big M: 256-wide tiles on 8 waves (k-quant variants keep 128 rows: the per-block accumulators double the
+    // register footprint); small M (a single clip): 128x128 on 4 waves so the grid still covers the 256 CUs
+    static const int force = [] { const char * v = getenv("Q2A_GEMM_TILE"); return v ? atoi(v) : 0; }();  // 1 big, 2 small
+    bool big = (int64_t) ((a.M + 255) / 256) * (a.N / 256) >= 512 && a.N % 256 == 0;
+    if (force == 1 && a.N % 256 == 0) big = true;
+    if (force == 2) big = false;
+    if (blk == 0) return big ? launch_cfg<256, 256, 2, 4, EPI, 0>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 0>(a, s);
+    if (blk == 256) return big ? launch_cfg<128, 256, 2, 4, EPI, 256>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 256>(a, s);
+    if (blk == 32) return big ? launch_cfg<128, 256, 2, 4, EPI, 32>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 32>(a, s);
+    return hipErrorInvalidValue;
 }
 
 }  // namespace
 
 hipError_t q2a_launch_gemm(const q2a_gemm_args & a, int epi, int blk, hipStream_t s) {
-    if (a.N % BN != 0 || a.K % BK != 0 || a.M <= 0) return hipErrorInvalidValue;
+    if (a.N % 128 != 0 || a.K % BK != 0 || a.M <= 0) return hipErrorInvalidValue;
     if (blk && (a.K % blk != 0)) return hipErrorInvalidValue;
     switch (epi) {
         case Q2A_EPI_QKV: return launch_epi<Q2A_EPI_QKV>(a, blk, s);

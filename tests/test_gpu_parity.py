@@ -194,3 +194,41 @@ def test_encoder_full_size_vs_reference_samples(engines, make_clip, golden, wt):
         assert mxs < 1e-3 and l2s < 1e-3 and rnerr < 1e-4, (mxs, l2s, rnerr)
     else:
         assert l2s < 2e-2 and rnerr < 2e-3, (mxs, l2s, rnerr)
+
+
+# ---------------------------------------------------------------- big-tile GEMM configuration (256-wide tiles)
+@pytest.mark.parametrize("wt", ["f16", "q4_k", "q8_0"])
+@pytest.mark.parametrize("which", [0, 2])
+def test_linear_big_tiles_match_oracle(engines, make_model, wt, which):
+    """M large enough that the launcher picks the 256-wide tile / 8-wave kernels (the batched-serving shapes)."""
+    e = engines("tiny", wt)
+    mf = ggmlfile.read(make_model("tiny", wt))
+    D, F = 256, 1024
+    names = {0: ["self_attn.q_proj.weight", "self_attn.k_proj.weight", "self_attn.v_proj.weight"],
+             2: ["fc1.weight"]}[which]
+    w = np.concatenate([_tensor_raw(mf, f"layers.0.{n}") for n in names])
+    N = {0: 3 * D, 2: F}[which]
+    M = 45000 + 17
+    x = np.random.default_rng(100 + which).standard_normal((M, D)).astype(np.float32)
+    xd = torch.from_numpy(x).cuda()
+    yd = torch.empty((M, N), dtype=torch.float32, device="cuda")
+    e.test_linear(0, which, xd.data_ptr(), M, yd.data_ptr())
+    torch.cuda.synchronize()
+    ref = oracle_py.gemm(mf.wtype, w, x, N)
+    mx, l2 = rel_errors(yd.cpu().numpy(), ref)
+    assert mx < 1e-5 and l2 < 1e-6, (mx, l2)
+
+
+def test_encoder_full_size_batched_big_tiles(engines, make_clip, golden):
+    """22 clips in one batch (M = 33 000 rows: the big-tile kernels) — every clip must still match the reference."""
+    _, g = golden
+    e = engines("full", "f16")
+    clip = make_clip(0)
+    out, st = e.encode_host([clip] * 22)
+    for c in (0, 21):
+        o = out[c].reshape(-1)
+        val = g["full_f16_c0_val"]
+        d = o[g["full_f16_c0_idx"]] - val
+        mxs = np.abs(d).max() / np.abs(val).max()
+        l2s = np.linalg.norm(d) / np.linalg.norm(val)
+        assert mxs < 1e-3 and l2s < 1e-3, (c, mxs, l2s)
