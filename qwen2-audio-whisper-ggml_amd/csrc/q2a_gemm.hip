@@ -49,43 +49,6 @@ __device__ __forceinline__ int64_t a_row_off(const q2a_gemm_args & p, int m) {
     return ((int64_t) (m / p.a_rpg) * p.a_gstride + (int64_t) (m % p.a_rpg) * p.a_step) * p.lda;
 }
 
-template <int EPI>
-__device__ __forceinline__ void epilogue_store(const q2a_gemm_args & p, int m, int n, float v) {
-    if (EPI == Q2A_EPI_RESID) {
-        float * o = p.outF + (int64_t) m * p.ldo + n;
-        *o = (v + p.bias[n]) + *o;
-    } else if (EPI == Q2A_EPI_GELU_H) {
-        const int64_t row = (int64_t) (m / p.o_rpg) * p.o_gstride + (m % p.o_rpg) + p.o_off;
-        p.outH[row * p.ldo + n] = (_Float16) gelu_lut(v + p.bias[n], p.gelu_tab);
-    } else if (EPI == Q2A_EPI_GELU_F) {
-        p.outF[(int64_t) m * p.ldo + n] = gelu_lut(v + p.bias[n], p.gelu_tab);
-    } else if (EPI == Q2A_EPI_CONV2) {
-        const float g = gelu_lut(v + p.bias[n], p.gelu_tab);
-        p.outF[(int64_t) m * p.ldo + n] = p.pe[(int64_t) (m % p.T) * p.ldo + n] + g;
-    } else if (EPI == Q2A_EPI_STORE_F) {
-        p.outF[(int64_t) m * p.ldo + n] = v;
-    } else if (EPI == Q2A_EPI_QKV) {
-        const int part = n / p.D, c = n - part * p.D;
-        const float val = v + p.bias[n];
-        if (part == 0) {
-            const float q = val * p.qscale;   // ggml_scale after the bias add (qwen2-whisper.cpp:2054); exact 2^-3
-            const _Float16 hi = (_Float16) q;
-            const _Float16 lo = (_Float16) (q - (float) hi);
-            p.qh[(int64_t) m * p.D + c] = hi;
-            p.ql[(int64_t) m * p.D + c] = lo;
-        } else if (part == 1) {
-            const _Float16 hi = (_Float16) val;
-            const _Float16 lo = (_Float16) (val - (float) hi);
-            p.kh[(int64_t) m * p.D + c] = hi;
-            p.kl[(int64_t) m * p.D + c] = lo;
-        } else {
-            const int clip = m / p.T, t = m - clip * p.T;
-            const int h = c >> 6, d = c & 63;
-            p.vt[(((int64_t) clip * p.H + h) * 64 + d) * p.TP + t] = (_Float16) val;
-        }
-    }
-}
-
 __device__ __forceinline__ half8 frag(const char * img, int row, int chunk) {
     return *(const half8 *) (img + row * ROWB + ((chunk ^ (row & 7)) << 4));
 }
@@ -226,19 +189,104 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
         __syncthreads();
     }
 
-    // epilogue: C layout of 16x16 tiles: col = lane & 15, row = (lane >> 4) * 4 + r
+    // ---- epilogue. Per-element math (bias, scale, GELU) in registers, then an LDS transpose per wave so every
+    // global access is 16 B per lane along a row (8 B along t for V^T) instead of 2-4 B scattered stores
+    // (the 16x16 C layout gives each lane 4 rows of ONE column). The operand images are dead: reuse the LDS.
+    constexpr int WR = BM / WM, WC = BN / WN;        // rows x cols owned by a wave (WC == 64)
+    static_assert(WC == 64, "epilogue assumes 64 columns per wave");
+    constexpr int PR = 32;                           // rows per pass (two 16-row tiles)
+    const int rbase = m0 + wm * WR, cbase = n0 + wn * WC;
+    float bias_j[NJ];
+    int part = 0;
+    if (EPI == Q2A_EPI_QKV) part = cbase / p.D;     // q | k | v: uniform per wave (D % 64 == 0)
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+    for (int j = 0; j < NJ; ++j) bias_j[j] = (EPI == Q2A_EPI_STORE_F) ? 0.f : p.bias[cbase + j * 16 + (lane & 15)];
+    const float vscale = (EPI == Q2A_EPI_QKV && part == 0) ? p.qscale : 1.0f;
+    constexpr int WREG = 2 * PR * (WC + 8) * 2;                  // per-wave staging bytes (max of the layouts)
+    static_assert(PR * (WC + 4) * 4 <= WREG && NW * WREG <= (int) sizeof(lds), "epilogue staging exceeds LDS");
+    char * wl = &lds[0][0] + wave * WREG;
+    __syncthreads();
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int m = m0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r;
-            if (m >= p.M) continue;
+    for (int ps = 0; ps < WR / PR; ++ps) {
+        // 1) registers -> LDS
 #pragma unroll
-            for (int j = 0; j < NJ; ++j) {
-                const int n = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
-                epilogue_store<EPI>(p, m, n, acc[i][j][r]);
+        for (int ii = 0; ii < PR / 16; ++ii) {
+            const int i = ps * (PR / 16) + ii;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int rl = ii * 16 + (lane >> 4) * 4 + r, cl = j * 16 + (lane & 15);
+                    float v = acc[i][j][r];
+                    if (EPI != Q2A_EPI_STORE_F) v = v + bias_j[j];
+                    if (EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_GELU_F || EPI == Q2A_EPI_CONV2) v = gelu_lut(v, p.gelu_tab);
+                    if (EPI == Q2A_EPI_QKV) v = v * vscale;   // ggml_scale after the bias add (:2054), exact 2^-3
+                    if (EPI == Q2A_EPI_QKV && part == 2) {
+                        ((_Float16 *) wl)[cl * (PR + 4) + rl] = (_Float16) v;           // V^T image [col][row]
+                    } else if (EPI == Q2A_EPI_QKV) {
+                        const _Float16 hi = (_Float16) v;
+                        ((_Float16 *) wl)[rl * (WC + 8) + cl] = hi;
+                        ((_Float16 *) wl)[PR * (WC + 8) + rl * (WC + 8) + cl] = (_Float16) (v - (float) hi);
+                    } else if (EPI == Q2A_EPI_GELU_H) {
+                        ((_Float16 *) wl)[rl * (WC + 8) + cl] = (_Float16) v;
+                    } else {
+                        ((float *) wl)[rl * (WC + 4) + cl] = v;
+                    }
+                }
+        }
+        __syncthreads();
+        // 2) LDS -> global, 16 B per lane
+        const int prow = rbase + ps * PR;
+        if (EPI == Q2A_EPI_QKV && part == 2) {
+            // lane: column cl = lane, 4 consecutive rows per 8-B store; 8 row groups
+            const int c = cbase - 2 * p.D + lane, h = c >> 6, d = c & 63;
+#pragma unroll
+            for (int a = 0; a < PR / 4; ++a) {
+                const int m = prow + 4 * a;
+                if (m >= p.M) break;
+                const int clip = m / p.T, t = m - clip * p.T;
+                const uint2 v = *(const uint2 *) ((const _Float16 *) wl + lane * (PR + 4) + 4 * a);
+                *(uint2 *) (p.vt + (((int64_t) clip * p.H + h) * 64 + d) * p.TP + t) = v;
+            }
+        } else if (EPI == Q2A_EPI_QKV || EPI == Q2A_EPI_GELU_H) {
+#pragma unroll
+            for (int it = 0; it < PR / 8; ++it) {
+                const int rl = it * 8 + (lane >> 3), c8 = (lane & 7) * 8;
+                const int m = prow + rl;
+                if (m < p.M) {
+                    const uint4 v = *(const uint4 *) ((const _Float16 *) wl + rl * (WC + 8) + c8);
+                    if (EPI == Q2A_EPI_GELU_H) {
+                        const int64_t row = (int64_t) (m / p.o_rpg) * p.o_gstride + (m % p.o_rpg) + p.o_off;
+                        *(uint4 *) (p.outH + row * p.ldo + cbase + c8) = v;
+                    } else {
+                        const int c = cbase - part * p.D + c8;
+                        const uint4 lo = *(const uint4 *) ((const _Float16 *) wl + PR * (WC + 8) + rl * (WC + 8) + c8);
+                        *(uint4 *) ((part == 0 ? p.qh : p.kh) + (int64_t) m * p.D + c) = v;
+                        *(uint4 *) ((part == 0 ? p.ql : p.kl) + (int64_t) m * p.D + c) = lo;
+                    }
+                }
+            }
+        } else {
+#pragma unroll
+            for (int it = 0; it < PR / 4; ++it) {
+                const int rl = it * 4 + (lane >> 4), c4 = (lane & 15) * 4;
+                const int m = prow + rl;
+                if (m < p.M) {
+                    float4 v = *(const float4 *) ((const float *) wl + rl * (WC + 4) + c4);
+                    float * o = p.outF + (int64_t) m * p.ldo + cbase + c4;
+                    if (EPI == Q2A_EPI_RESID) {
+                        const float4 x = *(const float4 *) o;
+                        v.x = v.x + x.x; v.y = v.y + x.y; v.z = v.z + x.z; v.w = v.w + x.w;
+                    } else if (EPI == Q2A_EPI_CONV2) {
+                        const float4 pe = *(const float4 *) (p.pe + (int64_t) (m % p.T) * p.ldo + cbase + c4);
+                        v.x = pe.x + v.x; v.y = pe.y + v.y; v.z = pe.z + v.z; v.w = pe.w + v.w;
+                    }
+                    *(float4 *) o = v;
+                }
             }
         }
+        __syncthreads();
+    }
 }
 
 template <int BM, int BN, int WM, int WN, int EPI, int BLK>
