@@ -28,6 +28,7 @@ constexpr int VROW = 136;         // bytes per V^T image row (64 halves + 8 B pa
 constexpr int KIMG = KT * KROW;   // 9216
 constexpr int VIMG = 64 * VROW;   // 8704
 constexpr int STAGE = 2 * KIMG + VIMG;
+constexpr float L2E = 1.4426950408889634f;   // exp(x) = exp2(x * log2 e)
 
 __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
     __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
@@ -53,30 +54,34 @@ __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
 
     // staging: each thread moves 2 x 16 B of Kh, of Kl and of V^T per tile
     const q2a_half * vt_base = p.vt + ((int64_t) clip * p.H + h) * 64 * p.TP;
-    uint4 rk_h[2], rk_l[2], rv[2];
-    auto load_tile = [&](int t) {
-        const int kb0 = t * KT;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int c = tid + u * 256, r = c >> 3, ch = c & 7;
-            const int key = min(kb0 + r, T - 1);
-            rk_h[u] = *(const uint4 *) (p.kh + (rowbase + key) * D + h * 64 + ch * 8);
-            rk_l[u] = *(const uint4 *) (p.kl + (rowbase + key) * D + h * 64 + ch * 8);
-            rv[u] = *(const uint4 *) (vt_base + (int64_t) r * p.TP + kb0 + ch * 8);
-        }
-    };
-    auto store_tile = [&](int buf) {
-        char * st = lds + buf * STAGE;
-#pragma unroll
-        for (int u = 0; u < 2; ++u) {
-            const int c = tid + u * 256, r = c >> 3, ch = c & 7;
-            *(uint4 *) (st + r * KROW + ch * 16) = rk_h[u];
-            *(uint4 *) (st + KIMG + r * KROW + ch * 16) = rk_l[u];
-            uint2 * v = (uint2 *) (st + 2 * KIMG + r * VROW + ch * 16);
-            v[0] = make_uint2(rv[u].x, rv[u].y);
-            v[1] = make_uint2(rv[u].z, rv[u].w);
-        }
-    };
+    uint4 rk_h0, rk_h1, rk_l0, rk_l1, rv0, rv1;
+#define Q2A_LOAD_TILE(t_)                                                                           \
+    do {                                                                                            \
+        const int kb0_ = (t_) * KT;                                                                 \
+        const int c0_ = tid, c1_ = tid + 256;                                                       \
+        const int k0_ = min(kb0_ + (c0_ >> 3), T - 1), k1_ = min(kb0_ + (c1_ >> 3), T - 1);       \
+        rk_h0 = *(const uint4 *) (p.kh + (rowbase + k0_) * D + h * 64 + (c0_ & 7) * 8);              \
+        rk_h1 = *(const uint4 *) (p.kh + (rowbase + k1_) * D + h * 64 + (c1_ & 7) * 8);              \
+        rk_l0 = *(const uint4 *) (p.kl + (rowbase + k0_) * D + h * 64 + (c0_ & 7) * 8);              \
+        rk_l1 = *(const uint4 *) (p.kl + (rowbase + k1_) * D + h * 64 + (c1_ & 7) * 8);              \
+        rv0 = *(const uint4 *) (vt_base + (int64_t) (c0_ >> 3) * p.TP + kb0_ + (c0_ & 7) * 8);      \
+        rv1 = *(const uint4 *) (vt_base + (int64_t) (c1_ >> 3) * p.TP + kb0_ + (c1_ & 7) * 8);      \
+    } while (0)
+#define Q2A_STORE_ONE(st_, c_, kh_, kl_, v_)                                                        \
+    do {                                                                                            \
+        const int r_ = (c_) >> 3, ch_ = (c_) & 7;                                                   \
+        *(uint4 *) ((st_) + r_ * KROW + ch_ * 16) = (kh_);                                          \
+        *(uint4 *) ((st_) + KIMG + r_ * KROW + ch_ * 16) = (kl_);                                   \
+        uint2 * vv_ = (uint2 *) ((st_) + 2 * KIMG + r_ * VROW + ch_ * 16);                          \
+        vv_[0] = make_uint2((v_).x, (v_).y);                                                        \
+        vv_[1] = make_uint2((v_).z, (v_).w);                                                        \
+    } while (0)
+#define Q2A_STORE_TILE(buf_)                                                                        \
+    do {                                                                                            \
+        char * st__ = lds + (buf_) * STAGE;                                                         \
+        Q2A_STORE_ONE(st__, tid, rk_h0, rk_l0, rv0);                                                \
+        Q2A_STORE_ONE(st__, tid + 256, rk_h1, rk_l1, rv1);                                          \
+    } while (0)
 
     f16v o[2];
 #pragma unroll
@@ -86,58 +91,70 @@ __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
     float m_run = -1e30f, l_run = 0.f;
 
     const int ntiles = (T + KT - 1) / KT;
-    load_tile(0);
-    store_tile(0);
+    Q2A_LOAD_TILE(0);
+    Q2A_STORE_TILE(0);
     __syncthreads();
 
     for (int t = 0; t < ntiles; ++t) {
         const int cur = t & 1;
-        if (t + 1 < ntiles) load_tile(t + 1);
+        if (t + 1 < ntiles) Q2A_LOAD_TILE(t + 1);
         const char * kh_img = lds + cur * STAGE;
         const char * kl_img = kh_img + KIMG;
         const char * vt_img = kh_img + 2 * KIMG;
+        // S^T for both 32-key halves of the tile (24 MFMAs), then ONE online-softmax update per 64 keys
+        f16v sc[2];
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
-            f16v s;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) s[r] = 0.f;
+            for (int r = 0; r < 16; ++r) sc[kb][r] = 0.f;
             const int krow = kb * 32 + col;
 #pragma unroll
             for (int st = 0; st < 4; ++st) {
                 const int off = krow * KROW + (2 * st + hi) * 16;
                 const half8 ah = *(const half8 *) (kh_img + off);
                 const half8 al = *(const half8 *) (kl_img + off);
-                s = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, qh[st], s, 0, 0, 0);
-                s = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, qh[st], s, 0, 0, 0);
-                s = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ql[st], s, 0, 0, 0);
+                sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, qh[st], sc[kb], 0, 0, 0);
+                sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, qh[st], sc[kb], 0, 0, 0);
+                sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ql[st], sc[kb], 0, 0, 0);
             }
-            // mask keys >= T (row of reg r = (r&3) + 8(r>>2) + 4hi)
-            const int key0 = t * KT + kb * 32;
-            float mx = -1e30f;
+        }
+        if (t == ntiles - 1) {   // keys >= T exist only in the last tile (row of reg r = (r&3) + 8(r>>2) + 4hi)
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (t * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi >= T) sc[kb][r] = -1e30f;
+        }
+        float mx = sc[0][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sc[0][r]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[1][r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float m_new = fmaxf(m_run, mx);
+        const float nm = -m_new * L2E;
+        const float alpha = __builtin_amdgcn_exp2f(fmaf(m_run, L2E, nm));
+        float ls = 0.f;
+        half8 pf[2][2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const int key = key0 + (r & 3) + 8 * (r >> 2) + 4 * hi;
-                if (key >= T) s[r] = -1e30f;
-                mx = fmaxf(mx, s[r]);
-            }
-            mx = fmaxf(mx, __shfl_xor(mx, 32));
-            const float m_new = fmaxf(m_run, mx);
-            const float alpha = __expf(m_run - m_new);
-            float ls = 0.f;
-            half8 pf[2];
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const float pv = __expf(s[r] - m_new);
+                const float pv = __builtin_amdgcn_exp2f(fmaf(sc[kb][r], L2E, nm));
                 ls += pv;
-                pf[r >> 3][r & 7] = (_Float16) pv;
+                pf[kb][r >> 3][r & 7] = (_Float16) pv;
             }
-            l_run = l_run * alpha + ls;
-            m_run = m_new;
+        l_run = l_run * alpha + ls;
+        m_run = m_new;
+        if (__any(alpha != 1.0f)) {   // the running max moved for some query of this wave
 #pragma unroll
             for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-            // O^T[d][q] += V^T[d][keys] . P^T[keys][q]
+        }
+        // O^T[d][q] += V^T[d][keys] . P^T[keys][q]
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int dt = 0; dt < 2; ++dt) {
                 const char * vrow = vt_img + (dt * 32 + col) * VROW;
@@ -147,12 +164,11 @@ __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
                     const half4 v0 = *(const half4 *) (vrow + kbyte);
                     const half4 v1 = *(const half4 *) (vrow + kbyte + 16);
                     const half8 va = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, pf[sp], o[dt], 0, 0, 0);
+                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, pf[kb][sp], o[dt], 0, 0, 0);
                 }
             }
-        }
         // buffer cur^1 was last read in iteration t-1, before the barrier that ended it
-        if (t + 1 < ntiles) store_tile(cur ^ 1);
+        if (t + 1 < ntiles) Q2A_STORE_TILE(cur ^ 1);
         __syncthreads();
     }
 

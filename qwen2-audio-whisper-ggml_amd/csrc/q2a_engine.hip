@@ -138,7 +138,7 @@ inline void scale_min_k4(int j, const uint8_t * q, uint8_t * dd, uint8_t * mm) {
 // Expand rows [r0, r1) of a ggml weight matrix into the blob arrays (rows offset by dst_row0).
 // F16: copied. Q4_K: W' = sc_j * q (exact small integers), DX = d, DMIN = dmin, WEXT = (64 m_j, m_j).
 // Q8_0: W' = q, DX = d. Q4_0: W' = q - 8, DX = d.
-void expand_rows(const uint8_t * src, int wtype, int K, int r0, int r1, uint8_t * blob, const uint64_t * a, int dst_row0) {
+void expand_rows(const uint8_t * src, int wtype, int K, int Ntot, int r0, int r1, uint8_t * blob, const uint64_t * a, int dst_row0) {
     uint16_t * W = (uint16_t *) (blob + a[A_W]);
     const size_t rs = q2a_row_size(wtype, K);
     for (int r = r0; r < r1; ++r) {
@@ -148,19 +148,20 @@ void expand_rows(const uint8_t * src, int wtype, int K, int r0, int r1, uint8_t 
         if (wtype == Q2A_TYPE_F16) {
             memcpy(wr, row, (size_t) K * 2);
         } else if (wtype == Q2A_TYPE_Q4_K) {
+            // block-major scale arrays: [nb][Ntot] / [nb][Ntot][16] so a tile's block scales are contiguous
             const int nb = K / 256;
-            float * dx = (float *) (blob + a[A_DX]) + (size_t) n * nb;
-            float * dm = (float *) (blob + a[A_DMIN]) + (size_t) n * nb;
-            uint16_t * we = (uint16_t *) (blob + a[A_WEXT]) + (size_t) n * nb * 16;
+            float * dx = (float *) (blob + a[A_DX]);
+            float * dm = (float *) (blob + a[A_DMIN]);
+            uint16_t * we = (uint16_t *) (blob + a[A_WEXT]);
             for (int b = 0; b < nb; ++b) {
                 const q2a_block_q4_K * x = (const q2a_block_q4_K *) row + b;
-                dx[b] = q2a_fp16_to_fp32(x->d);
-                dm[b] = q2a_fp16_to_fp32(x->dmin);
+                dx[(size_t) b * Ntot + n] = q2a_fp16_to_fp32(x->d);
+                dm[(size_t) b * Ntot + n] = q2a_fp16_to_fp32(x->dmin);
                 for (int j = 0; j < 8; ++j) {
                     uint8_t sc, m;
                     scale_min_k4(j, x->scales, &sc, &m);
-                    we[b * 16 + 2 * j + 0] = q2a_fp32_to_fp16(64.0f * m);
-                    we[b * 16 + 2 * j + 1] = q2a_fp32_to_fp16((float) m);
+                    we[((size_t) b * Ntot + n) * 16 + 2 * j + 0] = q2a_fp32_to_fp16(64.0f * m);
+                    we[((size_t) b * Ntot + n) * 16 + 2 * j + 1] = q2a_fp32_to_fp16((float) m);
                     const uint8_t * q = x->qs + 32 * (j / 2);
                     for (int l = 0; l < 32; ++l) {
                         const int v = (j & 1) ? (q[l] >> 4) : (q[l] & 0xF);
@@ -170,18 +171,18 @@ void expand_rows(const uint8_t * src, int wtype, int K, int r0, int r1, uint8_t 
             }
         } else if (wtype == Q2A_TYPE_Q8_0) {
             const int nb = K / 32;
-            float * dx = (float *) (blob + a[A_DX]) + (size_t) n * nb;
+            float * dx = (float *) (blob + a[A_DX]);
             for (int b = 0; b < nb; ++b) {
                 const q2a_block_q8_0 * x = (const q2a_block_q8_0 *) row + b;
-                dx[b] = q2a_fp16_to_fp32(x->d);
+                dx[(size_t) b * Ntot + n] = q2a_fp16_to_fp32(x->d);
                 for (int l = 0; l < 32; ++l) wr[b * 32 + l] = q2a_fp32_to_fp16((float) x->qs[l]);
             }
         } else if (wtype == Q2A_TYPE_Q4_0) {
             const int nb = K / 32;
-            float * dx = (float *) (blob + a[A_DX]) + (size_t) n * nb;
+            float * dx = (float *) (blob + a[A_DX]);
             for (int b = 0; b < nb; ++b) {
                 const q2a_block_q4_0 * x = (const q2a_block_q4_0 *) row + b;
-                dx[b] = q2a_fp16_to_fp32(x->d);
+                dx[(size_t) b * Ntot + n] = q2a_fp16_to_fp32(x->d);
                 for (int l = 0; l < 16; ++l) {
                     wr[b * 32 + l] = q2a_fp32_to_fp16((float) ((x->qs[l] & 0xF) - 8));
                     wr[b * 32 + 16 + l] = q2a_fp32_to_fp16((float) ((x->qs[l] >> 4) - 8));
@@ -258,7 +259,7 @@ int pack(const char * path, std::vector<uint8_t> & out) {
     q2a_make_mel_tables((float *) (blob + h.goff[G_TAB]));
     q2a_make_gelu_table((uint16_t *) (blob + h.goff[G_GELU]));
 
-    struct job { const uint8_t * src; int K, r0, r1; const uint64_t * a; int dst0; };
+    struct job { const uint8_t * src; int K, Ntot, r0, r1; const uint64_t * a; int dst0; };
     std::vector<job> jobs;
     for (int l = 0; l < d.L; ++l) {
         const std::string p = "layers." + std::to_string(l) + ".";
@@ -291,12 +292,12 @@ int pack(const char * path, std::vector<uint8_t> & out) {
         cpy(lo[L_LN2W], l2w, (size_t) d.D * 4);
         cpy(lo[L_LN2B], l2b, (size_t) d.D * 4);
         const uint64_t * a0 = lo + L_MAT0;
-        jobs.push_back({wq, d.D, 0, d.D, a0, 0});
-        jobs.push_back({wk, d.D, 0, d.D, a0, d.D});
-        jobs.push_back({wv, d.D, 0, d.D, a0, 2 * d.D});
-        jobs.push_back({wo, d.D, 0, d.D, lo + L_MAT0 + A_COUNT, 0});
-        jobs.push_back({w1, d.D, 0, d.F, lo + L_MAT0 + 2 * A_COUNT, 0});
-        jobs.push_back({w2, d.F, 0, d.D, lo + L_MAT0 + 3 * A_COUNT, 0});
+        jobs.push_back({wq, d.D, 3 * d.D, 0, d.D, a0, 0});
+        jobs.push_back({wk, d.D, 3 * d.D, 0, d.D, a0, d.D});
+        jobs.push_back({wv, d.D, 3 * d.D, 0, d.D, a0, 2 * d.D});
+        jobs.push_back({wo, d.D, d.D, 0, d.D, lo + L_MAT0 + A_COUNT, 0});
+        jobs.push_back({w1, d.D, d.F, 0, d.F, lo + L_MAT0 + 2 * A_COUNT, 0});
+        jobs.push_back({w2, d.F, d.D, 0, d.D, lo + L_MAT0 + 3 * A_COUNT, 0});
     }
     const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::thread> th;
@@ -304,7 +305,7 @@ int pack(const char * path, std::vector<uint8_t> & out) {
         th.emplace_back([&, t]() {
             for (const job & j : jobs) {
                 const int n = j.r1 - j.r0;
-                expand_rows(j.src, wtype, j.K, j.r0 + n * t / nt, j.r0 + n * (t + 1) / nt, blob, j.a, j.dst0);
+                expand_rows(j.src, wtype, j.K, j.Ntot, j.r0 + n * t / nt, j.r0 + n * (t + 1) / nt, blob, j.a, j.dst0);
             }
         });
     for (auto & x : th) x.join();
@@ -373,6 +374,7 @@ struct q2a_engine {
     float * attF = nullptr;
     float * hF = nullptr;
     int TP = 0;
+    int dy_ld = 0;
 
     // optional per-kernel-class timing with HIP events on the launch stream (q2a_profile_*)
     bool prof = false;
@@ -440,11 +442,13 @@ int reserve(q2a_engine * e, int B) {
     const size_t o_kl = take((size_t) BT * d.D * 2);
     const size_t o_vt = take((size_t) B * d.H * 64 * e->TP * 2);
     size_t o_dyD = 0, o_dyF = 0, o_aD = 0, o_aF = 0, o_att = 0, o_hF = 0;
+    const int64_t MP = (BT + 255) / 256 * 256;   // padded row stride of the block-major scale arrays
+    e->dy_ld = (int) MP;
     if (quant) {
-        o_dyD = take((size_t) BT * (d.D / 32) * 4);
-        o_dyF = take((size_t) BT * (d.F / 32) * 4);
-        o_aD = take((size_t) BT * (d.D / 256 + 1) * 16 * 2);
-        o_aF = take((size_t) BT * (d.F / 256 + 1) * 16 * 2);
+        o_dyD = take((size_t) MP * (d.D / 32) * 4);
+        o_dyF = take((size_t) MP * (d.F / 32) * 4);
+        o_aD = take((size_t) MP * (d.D / 256 + 1) * 16 * 2);
+        o_aF = take((size_t) MP * (d.F / 256 + 1) * 16 * 2);
         o_att = take((size_t) BT * d.D * 4);
         o_hF = take((size_t) BT * d.F * 4);
     }
@@ -492,6 +496,7 @@ q2a_gemm_args gemm_base(const q2a_engine * e, int l, int which, const q2a_half *
         a.nblk = K / e->blk;
         a.dx = (const float *) (e->blob + m[A_DX]);
         a.dy = K == e->d.D ? e->dyD : e->dyF;
+        a.dy_ld = e->dy_ld;
         if (e->blk == 256) {
             a.dmin = (const float *) (e->blob + m[A_DMIN]);
             a.wext = (const q2a_half *) (e->blob + m[A_WEXT]);
@@ -537,7 +542,7 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
     const dims & d = e->d;
     const int M = B * d.T;
     const int mode = ln_mode(e);
-    q2a_ln_args ln{e->X, M, d.D, e->lv<const float *>(l, L_LN1W), e->lv<const float *>(l, L_LN1B), mode, e->actD, e->dyD, e->aextD};
+    q2a_ln_args ln{e->X, M, d.D, e->lv<const float *>(l, L_LN1W), e->lv<const float *>(l, L_LN1B), mode, e->actD, e->dyD, e->aextD, e->dy_ld};
     PLAUNCH(e, s, Q2A_PROF_LN, q2a_launch_layernorm(ln, s));
     {
         q2a_gemm_args a = gemm_base(e, l, 0, e->actD, M);
@@ -551,7 +556,7 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         if (mode == 0) at.outH = e->actD; else at.outF = e->attF;
         PLAUNCH(e, s, Q2A_PROF_ATTN, q2a_launch_attention(at, s));
         if (mode) {
-            q2a_quant_args qa{e->attF, M, d.D, mode, e->actD, e->dyD, e->aextD};
+            q2a_quant_args qa{e->attF, M, d.D, mode, e->actD, e->dyD, e->aextD, e->dy_ld};
             PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_quant_act(qa, s));
         }
     }
@@ -561,7 +566,7 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         a.outF = e->X; a.ldo = d.D;
         PLAUNCH(e, s, Q2A_PROF_GEMM_O, q2a_launch_gemm(a, Q2A_EPI_RESID, e->blk, s));
     }
-    q2a_ln_args ln2{e->X, M, d.D, e->lv<const float *>(l, L_LN2W), e->lv<const float *>(l, L_LN2B), mode, e->actD, e->dyD, e->aextD};
+    q2a_ln_args ln2{e->X, M, d.D, e->lv<const float *>(l, L_LN2W), e->lv<const float *>(l, L_LN2B), mode, e->actD, e->dyD, e->aextD, e->dy_ld};
     PLAUNCH(e, s, Q2A_PROF_LN, q2a_launch_layernorm(ln2, s));
     {
         q2a_gemm_args a = gemm_base(e, l, 2, e->actD, M);
@@ -572,7 +577,7 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         } else {
             a.outF = e->hF; a.ldo = d.F;
             PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_F, e->blk, s));
-            q2a_quant_args qa{e->hF, M, d.F, mode, e->actF, e->dyF, e->aextF};
+            q2a_quant_args qa{e->hF, M, d.F, mode, e->actF, e->dyF, e->aextF, e->dy_ld};
             PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_quant_act(qa, s));
         }
     }
@@ -879,7 +884,7 @@ int q2a_test_linear(q2a_engine * e, int layer, int which, const float * x, int M
         hipLaunchKernelGGL(k_to_half, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, A, n);
         LAUNCH(hipGetLastError());
     } else {
-        q2a_quant_args qa{x, M, K, mode, A, K == d.D ? e->dyD : e->dyF, K == d.D ? e->aextD : e->aextF};
+        q2a_quant_args qa{x, M, K, mode, A, K == d.D ? e->dyD : e->dyF, K == d.D ? e->aextD : e->aextF, e->dy_ld};
         LAUNCH(q2a_launch_quant_act(qa, s));
     }
     q2a_gemm_args a = gemm_base(e, layer, which, A, M);

@@ -218,9 +218,12 @@ __device__ __forceinline__ void quant_q80_block(float4 y, int lane, q2a_half * c
     if ((lane & 7) == 0) *dy_out = (float) (_Float16) d;    // block d is stored as fp16 (GGML_FP32_TO_FP16)
 }
 
+// Rows are [M*nseg][D] (a quantizer run splits a long row into nseg segments of D); the block scales are
+// written block-major: block bf of logical row m (= row / nseg) goes to dy[bf * ld + m] (aext likewise x16).
 template <int MODE, bool LN>
 __global__ __launch_bounds__(256) void k_rownorm(const float * __restrict__ X, int M, int D, const float * __restrict__ g,
-                                                 const float * __restrict__ b, q2a_half * outH, float * dy, q2a_half * aext) {
+                                                 const float * __restrict__ b, q2a_half * outH, float * dy, q2a_half * aext,
+                                                 int nseg, int ld) {
     const int lane = threadIdx.x & 63;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (row >= M) return;
@@ -274,14 +277,15 @@ __global__ __launch_bounds__(256) void k_rownorm(const float * __restrict__ X, i
             y.w = (y.w * scale) * gg.w + bb.w;
         }
         q2a_half * o = outH + (int64_t) row * D + 4 * c;
+        const int m = row / nseg, seg = row - m * nseg;
         if (MODE == 0) {
             o[0] = (_Float16) y.x; o[1] = (_Float16) y.y; o[2] = (_Float16) y.z; o[3] = (_Float16) y.w;
         } else if (MODE == 1) {
-            const int nb = D / 256;
-            quant_q8k_block(y, lane, o, dy + (int64_t) row * nb + u, aext + ((int64_t) row * nb + u) * 16);
+            const int bf = seg * (D / 256) + u;
+            quant_q8k_block(y, lane, o, dy + (int64_t) bf * ld + m, aext + ((int64_t) bf * ld + m) * 16);
         } else {
-            const int nb = D / 32;
-            quant_q80_block(y, lane, o, dy + (int64_t) row * nb + (4 * c) / 32);
+            const int bf = seg * (D / 32) + (4 * c) / 32;
+            quant_q80_block(y, lane, o, dy + (int64_t) bf * ld + m);
         }
     }
 }
@@ -354,9 +358,9 @@ hipError_t q2a_launch_layernorm(const q2a_ln_args & a, hipStream_t s) {
     if (a.mode == 1 && a.D % 256) return hipErrorInvalidValue;
     if (a.mode == 2 && a.D % 32) return hipErrorInvalidValue;
     const dim3 grid((a.M + 3) / 4), blk(256);
-    if (a.mode == 0) hipLaunchKernelGGL((k_rownorm<0, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext);
-    else if (a.mode == 1) hipLaunchKernelGGL((k_rownorm<1, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext);
-    else hipLaunchKernelGGL((k_rownorm<2, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext);
+    if (a.mode == 0) hipLaunchKernelGGL((k_rownorm<0, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
+    else if (a.mode == 1) hipLaunchKernelGGL((k_rownorm<1, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
+    else hipLaunchKernelGGL((k_rownorm<2, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     return hipGetLastError();
 }
 
@@ -368,9 +372,9 @@ hipError_t q2a_launch_quant_act(const q2a_quant_args & a, hipStream_t s) {
     const dim3 grid((a.M * nseg + 3) / 4), blk(256);
     // view X as [M*nseg][seg]: contiguous, and the block structure (256 / 32) never straddles a segment
     if (a.mode == 1) {
-        hipLaunchKernelGGL((k_rownorm<1, false>), grid, blk, 0, s, a.X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext);
+        hipLaunchKernelGGL((k_rownorm<1, false>), grid, blk, 0, s, a.X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext, nseg, a.dy_ld);
     } else if (a.mode == 2) {
-        hipLaunchKernelGGL((k_rownorm<2, false>), grid, blk, 0, s, a.X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext);
+        hipLaunchKernelGGL((k_rownorm<2, false>), grid, blk, 0, s, a.X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext, nseg, a.dy_ld);
     } else {
         return hipErrorInvalidValue;
     }

@@ -59,7 +59,17 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
     constexpr int MI = BM / WM / 16, NJ = BN / WN / 16;   // 16x16 tiles per wave
     constexpr int LA = BM / 8 / NW, LB = BN / 8 / NW;     // glds instructions per wave per stage
     static_assert(LA >= 1 && LB >= 1, "tile too small for the wave count");
-    __shared__ __attribute__((aligned(16))) char lds[2][(BM + BN) * ROWB];
+    // k-quant block scales of the tile, staged through LDS (block-major global layout => contiguous per block):
+    //   BLK=256: dy[BM] f32 | aext[BM][16] f16 | dx[BN] f32 | dmin[BN] f32 | wext[BN][16] f16   (one buffer)
+    //   BLK=32 : dy[2][BM] f32 | dx[2][BN] f32 for the two 32-blocks of a K-step            (two buffers)
+    constexpr int SB = BLK == 256 ? (BM * 4 + BM * 32 + BN * 8 + BN * 32) : BLK == 32 ? 2 * (BM * 4 + BN * 4) : 0;
+    constexpr int NSB = BLK == 32 ? 2 : 1;
+    constexpr int NT = NW * 64;
+    constexpr int SCH = (SB / 16 + NT - 1) / NT;          // 16-B scale chunks per thread
+    constexpr int OPB = (BM + BN) * ROWB;                 // one operand stage (A image | W image)
+    __shared__ __attribute__((aligned(16))) char lds_raw[2 * OPB + (BLK ? NSB * SB : 0)];
+#define LDS_STAGE(b_) (lds_raw + (b_) * OPB)
+    char * sbuf = lds_raw + 2 * OPB;                      // scale staging (only when BLK)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave / WN, wn = wave % WN;
 
@@ -95,6 +105,40 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                                              (lds_ptr_t) (buf + (BM + (wave * LB + i) * 8) * ROWB), 16, 0, 0);
     };
 
+    // scale chunk c of K-block group g (BLK=256: block g; BLK=32: blocks 2g, 2g+1) -> global source
+    auto scale_src = [&](int c, int g) -> const uint4 * {
+        if (BLK == 256) {
+            if (c < BM / 4) return (const uint4 *) (p.dy + (int64_t) g * p.dy_ld + m0) + c;
+            c -= BM / 4;
+            if (c < BM * 2) return (const uint4 *) (p.aext + ((int64_t) g * p.dy_ld + m0) * 16) + c;
+            c -= BM * 2;
+            if (c < BN / 4) return (const uint4 *) (p.dx + (int64_t) g * p.N + n0) + c;
+            c -= BN / 4;
+            if (c < BN / 4) return (const uint4 *) (p.dmin + (int64_t) g * p.N + n0) + c;
+            c -= BN / 4;
+            return (const uint4 *) (p.wext + ((int64_t) g * p.N + n0) * 16) + c;
+        } else {
+            if (c < BM / 2) return (const uint4 *) (p.dy + (int64_t) (2 * g + c / (BM / 4)) * p.dy_ld + m0) + c % (BM / 4);
+            c -= BM / 2;
+            return (const uint4 *) (p.dx + (int64_t) (2 * g + c / (BN / 4)) * p.N + n0) + c % (BN / 4);
+        }
+    };
+    uint4 sreg[BLK ? SCH : 1];
+    auto scale_load = [&](int g) {
+#pragma unroll
+        for (int u = 0; u < SCH; ++u) {
+            const int c = tid + u * NT;
+            if (c < SB / 16) sreg[u] = *scale_src(c, g);
+        }
+    };
+    auto scale_store = [&](int buf) {
+#pragma unroll
+        for (int u = 0; u < SCH; ++u) {
+            const int c = tid + u * NT;
+            if (c < SB / 16) *(uint4 *) (sbuf + buf * SB + c * 16) = sreg[u];
+        }
+    };
+
     f4 acc[MI][NJ];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
@@ -109,15 +153,21 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
     }
 
     const int nk = p.K / BK;
-    stage(lds[0], 0);
+    stage(LDS_STAGE(0), 0);
+    if (BLK == 32) scale_load(0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (BLK == 32) scale_store(0);
     __syncthreads();
 
     for (int kt = 0; kt < nk; ++kt) {
         const int cur = kt & 1;
-        if (kt + 1 < nk) stage(lds[cur ^ 1], (kt + 1) * BK);
-        const char * ia = lds[cur];
-        const char * iw = lds[cur] + BM * ROWB;
+        if (kt + 1 < nk) stage(LDS_STAGE(cur ^ 1), (kt + 1) * BK);
+        // Q4_K: block kt/4's scales are fetched at its first K-step and land in LDS at its end (3 steps early);
+        // Q8_0: the next K-step's two blocks are fetched one step ahead into the other buffer.
+        const bool sload = BLK == 256 ? (kt % 4 == 0) : (BLK == 32 && kt + 1 < nk);
+        if (sload) scale_load(BLK == 256 ? kt / 4 : kt + 1);
+        const char * ia = LDS_STAGE(cur);
+        const char * iw = LDS_STAGE(cur) + BM * ROWB;
 #pragma unroll
         for (int s = 0; s < 2; ++s) {
             const int chunk = s * 4 + (lane >> 4);
@@ -136,35 +186,32 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
             if (BLK) {
                 const int kpos = kt * BK + (s + 1) * 32;   // K consumed so far
                 if (kpos % BLK == 0) {
-                    const int kb = kpos / BLK - 1;
+                    const char * sb = BLK == 256 ? sbuf : sbuf + cur * SB;
+                    const int sub = BLK == 256 ? 0 : s;                    // which of the K-step's two 32-blocks
+                    const float * s_dy = (const float *) sb + (BLK == 256 ? 0 : sub * BM);
+                    const q2a_half * s_ae = (const q2a_half *) (sb + BM * 4);
+                    const float * s_dx = (const float *) (sb + (BLK == 256 ? BM * 36 : 2 * BM * 4)) + (BLK == 256 ? 0 : sub * BN);
+                    const float * s_dm = (const float *) (sb + BM * 36 + BN * 4);
+                    const q2a_half * s_we = (const q2a_half *) (sb + BM * 36 + BN * 8);
                     float dx[NJ], dm[NJ];
+                    half4 we[NJ];
 #pragma unroll
                     for (int j = 0; j < NJ; ++j) {
-                        const int n = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
-                        dx[j] = p.dx[(int64_t) n * p.nblk + kb];
-                        if (BLK == 256) dm[j] = p.dmin[(int64_t) n * p.nblk + kb];
-                    }
-                    half4 we[NJ];
-                    if (BLK == 256) {
-#pragma unroll
-                        for (int j = 0; j < NJ; ++j) {
-                            const int n = n0 + wn * (BN / WN) + j * 16 + (lane & 15);
-                            we[j] = *(const half4 *) (p.wext + ((int64_t) n * p.nblk + kb) * 16 + (lane >> 4) * 4);
+                        const int n = wn * (BN / WN) + j * 16 + (lane & 15);
+                        dx[j] = s_dx[n];
+                        if (BLK == 256) {
+                            dm[j] = s_dm[n];
+                            we[j] = *(const half4 *) (s_we + n * 16 + (lane >> 4) * 4);
                         }
                     }
 #pragma unroll
                     for (int i = 0; i < MI; ++i) {
-                        float dy[4];
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const int m = min(m0 + wm * (BM / WM) + i * 16 + (lane >> 4) * 4 + r, p.M - 1);
-                            dy[r] = p.dy[(int64_t) m * p.nblk + kb];
-                        }
+                        const float4 dyv = *(const float4 *) (s_dy + wm * (BM / WM) + i * 16 + (lane >> 4) * 4);
+                        const float dy[4] = {dyv.x, dyv.y, dyv.z, dyv.w};
                         half4 ae;
                         if (BLK == 256) {
                             // min term S2 = sum_j m_j * bsum32_j: one 16x16x16 MFMA per tile on (hi,lo)-split bsums
-                            const int m = min(m0 + wm * (BM / WM) + i * 16 + (lane & 15), p.M - 1);
-                            ae = *(const half4 *) (p.aext + ((int64_t) m * p.nblk + kb) * 16 + (lane >> 4) * 4);
+                            ae = *(const half4 *) (s_ae + (wm * (BM / WM) + i * 16 + (lane & 15)) * 16 + (lane >> 4) * 4);
                         }
 #pragma unroll
                         for (int j = 0; j < NJ; ++j) {
@@ -186,6 +233,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
             }
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (sload) scale_store(BLK == 256 ? 0 : cur ^ 1);
         __syncthreads();
     }
 
@@ -203,8 +251,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
     for (int j = 0; j < NJ; ++j) bias_j[j] = (EPI == Q2A_EPI_STORE_F) ? 0.f : p.bias[cbase + j * 16 + (lane & 15)];
     const float vscale = (EPI == Q2A_EPI_QKV && part == 0) ? p.qscale : 1.0f;
     constexpr int WREG = 2 * PR * (WC + 8) * 2;                  // per-wave staging bytes (max of the layouts)
-    static_assert(PR * (WC + 4) * 4 <= WREG && NW * WREG <= (int) sizeof(lds), "epilogue staging exceeds LDS");
-    char * wl = &lds[0][0] + wave * WREG;
+    static_assert(PR * (WC + 4) * 4 <= WREG && NW * WREG <= 2 * OPB, "epilogue staging exceeds LDS");
+    char * wl = lds_raw + wave * WREG;
     __syncthreads();
 #pragma unroll
     for (int ps = 0; ps < WR / PR; ++ps) {
@@ -287,6 +335,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
         }
         __syncthreads();
     }
+#undef LDS_STAGE
 }
 
 template <int BM, int BN, int WM, int WN, int EPI, int BLK>

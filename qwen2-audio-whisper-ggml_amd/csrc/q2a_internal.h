@@ -38,13 +38,15 @@ struct q2a_gemm_args {
     int D, H, TP;
     float qscale;
     const uint16_t * gelu_tab;        // 65536-entry fp16 table: fp16(gelu_f32(fp16 x)) (ggml.c:3797-3806)
-    // blocked (k-quant) accumulation: acc += dy[m][b]*dx[n][b]*S1 - dy[m][b]*dmin[n][b]*S2 per K-block b
-    const float * dy;                 // [M][nblk]
-    const float * dx;                 // [N][nblk]
-    const float * dmin;               // [N][nblk] (Q4_K only)
-    const q2a_half * aext;            // [M][nblk][16] bsum hi/lo pairs (Q4_K only)
-    const q2a_half * wext;            // [N][nblk][16] (64*m_j, m_j) pairs (Q4_K only)
+    // blocked (k-quant) accumulation: acc += dy[b][m]*dx[b][n]*S1 - dy[b][m]*dmin[b][n]*S2 per K-block b.
+    // All block arrays are block-major so one block's scales for a tile are contiguous (staged through LDS).
+    const float * dy;                 // [nblk][dy_ld]
+    const float * dx;                 // [nblk][N]
+    const float * dmin;               // [nblk][N] (Q4_K only)
+    const q2a_half * aext;            // [nblk][dy_ld][16] bsum hi/lo pairs (Q4_K only)
+    const q2a_half * wext;            // [nblk][N][16] (64*m_j, m_j) pairs (Q4_K only)
     int nblk;
+    int dy_ld;                        // row stride of dy/aext (M rounded up to 256)
 };
 
 // blk: 0 (plain fp16 GEMM), 256 (Q4_K x Q8_K), 32 (Q8_0/Q4_0 x Q8_0)
@@ -87,8 +89,9 @@ struct q2a_ln_args {
     const float * b;
     int mode;
     q2a_half * outH;
-    float * dy;
-    q2a_half * aext;
+    float * dy;          // block-major [D/blk][dy_ld]
+    q2a_half * aext;     // block-major [D/256][dy_ld][16]
+    int dy_ld;
 };
 hipError_t q2a_launch_layernorm(const q2a_ln_args & a, hipStream_t s);
 
@@ -100,6 +103,7 @@ struct q2a_quant_args {
     q2a_half * outH;
     float * dy;
     q2a_half * aext;
+    int dy_ld;
 };
 hipError_t q2a_launch_quant_act(const q2a_quant_args & a, hipStream_t s);
 
