@@ -574,6 +574,10 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         if (mode == 0) {
             a.outH = e->actF; a.ldo = d.F; a.o_rpg = M; a.o_gstride = 0; a.o_off = 0;
             PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_H, 0, s));
+        } else if (mode == 1 && q2a_gemm_wide_tiles(M, d.F, e->blk)) {
+            // fused fc1 + GELU + Q8_K quantization of the fc2 input (one Q8_K block per 256-column tile)
+            a.outH = e->actF; a.ldo = d.F; a.qdy = e->dyF; a.qaext = e->aextF;
+            PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_Q8K, e->blk, s));
         } else {
             a.outF = e->hF; a.ldo = d.F;
             PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_F, e->blk, s));

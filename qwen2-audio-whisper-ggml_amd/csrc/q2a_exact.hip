@@ -2,6 +2,7 @@
 // -ffp-contract=off): log-mel frontend, LayerNorm (+ activation quantizers), AvgPool + final LayerNorm.
 // All are HBM/latency-bound; they are fused so that each tensor is read once and written once.
 #include "q2a_internal.h"
+#include "q2a_quant.h"
 
 #include <math.h>
 
@@ -166,60 +167,6 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 
-// quantize one 256-block (one float4 per lane) to Q8_K codes; writes codes, d and the bsum hi/lo operand
-__device__ __forceinline__ void quant_q8k_block(float4 y, int lane, q2a_half * codes, float * dy_out, q2a_half * aext) {
-    // max |x| and the signed value of its FIRST occurrence (strict '>' scan, :3793-3798)
-    float av[4] = {fabsf(y.x), fabsf(y.y), fabsf(y.z), fabsf(y.w)};
-    float vv[4] = {y.x, y.y, y.z, y.w};
-    float amax = av[0], mx = vv[0];
-    int idx = lane * 4;
-    for (int e = 1; e < 4; ++e)
-        if (av[e] > amax) { amax = av[e]; mx = vv[e]; idx = lane * 4 + e; }
-    for (int o = 32; o > 0; o >>= 1) {
-        const float a2 = __shfl_xor(amax, o), m2 = __shfl_xor(mx, o);
-        const int i2 = __shfl_xor(idx, o);
-        if (a2 > amax || (a2 == amax && i2 < idx)) { amax = a2; mx = m2; idx = i2; }
-    }
-    int q[4] = {0, 0, 0, 0};
-    float d = 0.f;
-    if (amax != 0.f) {
-        const float iscale = -127.f / mx;
-        for (int e = 0; e < 4; ++e) q[e] = min(127, (int) rintf(iscale * vv[e]));
-        d = 1 / iscale;
-    }
-    for (int e = 0; e < 4; ++e) codes[e] = (_Float16) (float) q[e];
-    if (lane == 0) *dy_out = d;
-    // bsums over 16 = 4 lanes, then bsum32_j = lanes 8j..8j+7
-    int s = q[0] + q[1] + q[2] + q[3];
-    s += __shfl_xor(s, 1);
-    s += __shfl_xor(s, 2);
-    s += __shfl_xor(s, 4);
-    if ((lane & 7) == 0) {
-        const int j = lane >> 3;
-        const int hi = (s >= 0) ? (s >> 6) : -((-s + 63) >> 6);   // floor(s / 64)
-        const int lo = s - 64 * hi;
-        aext[2 * j + 0] = (_Float16) (float) hi;
-        aext[2 * j + 1] = (_Float16) (float) lo;
-    }
-}
-
-// quantize one 32-block (8 lanes x float4) to Q8_0 codes with the x86 AVX2 semantics
-__device__ __forceinline__ void quant_q80_block(float4 y, int lane, q2a_half * codes, float * dy_out) {
-    float amax = fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w)));
-    amax = fmaxf(amax, __shfl_xor(amax, 1));
-    amax = fmaxf(amax, __shfl_xor(amax, 2));
-    amax = fmaxf(amax, __shfl_xor(amax, 4));
-    const float d = amax / 127.f;
-    const float id = (amax != 0.0f) ? 127.f / amax : 0.0f;
-    codes[0] = (_Float16) rintf(y.x * id);
-    codes[1] = (_Float16) rintf(y.y * id);
-    codes[2] = (_Float16) rintf(y.z * id);
-    codes[3] = (_Float16) rintf(y.w * id);
-    if ((lane & 7) == 0) *dy_out = (float) (_Float16) d;    // block d is stored as fp16 (GGML_FP32_TO_FP16)
-}
-
-// Rows are [M*nseg][D] (a quantizer run splits a long row into nseg segments of D); the block scales are
-// written block-major: block bf of logical row m (= row / nseg) goes to dy[bf * ld + m] (aext likewise x16).
 template <int MODE, bool LN>
 __global__ __launch_bounds__(256) void k_rownorm(const float * __restrict__ X, int M, int D, const float * __restrict__ g,
                                                  const float * __restrict__ b, q2a_half * outH, float * dy, q2a_half * aext,

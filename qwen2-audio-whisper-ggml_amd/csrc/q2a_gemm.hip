@@ -18,6 +18,7 @@
 // of the current one. Workgroups are remapped XCD-contiguously (bijective) and rasterised in groups of 8 M-tiles
 // per N column so the tiles resident on one XCD share A and W panels through its L2.
 #include "q2a_internal.h"
+#include "q2a_quant.h"
 
 #include <cstdlib>
 
@@ -237,6 +238,51 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
         __syncthreads();
     }
 
+    if constexpr (EPI == Q2A_EPI_GELU_Q8K) {
+        // fc1 + GELU + Q8_K quantization of the produced activation (the conversion ggml applies before fc2,
+        // quantize_row_q8_K_ref): the 256-column tile is exactly one Q8_K block per row. Stage 64 rows x 256 f32
+        // through LDS per pass, then one wave quantizes one row (a float4 per lane) exactly like k_rownorm.
+        static_assert(BN == 256 && WN == 4, "Q8_K epilogue needs a 256-column tile");
+        constexpr int RS = 260;                               // padded row stride (floats)
+        constexpr int PRQ = 64;
+        static_assert(PRQ * RS * 4 <= 2 * OPB, "Q8_K staging exceeds LDS");
+        float * tl = (float *) lds_raw;
+        const int kb = n0 / 256;
+        float bias_j[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bias_j[j] = p.bias[n0 + wn * 64 + j * 16 + (lane & 15)];
+        __syncthreads();
+#pragma unroll
+        for (int ps = 0; ps < BM / PRQ; ++ps) {
+            if (wm * (BM / WM) / PRQ == ps || (BM / WM) > PRQ) {
+#pragma unroll
+                for (int i = 0; i < MI; ++i) {
+                    const int rw = wm * (BM / WM) + i * 16;          // tile row of this 16-row block
+                    if (rw < ps * PRQ || rw >= (ps + 1) * PRQ) continue;
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            tl[(rw - ps * PRQ + (lane >> 4) * 4 + r) * RS + wn * 64 + j * 16 + (lane & 15)] =
+                                gelu_lut(acc[i][j][r] + bias_j[j], p.gelu_tab);
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int rr = 0; rr < PRQ / NW; ++rr) {
+                const int rl = wave * (PRQ / NW) + rr;
+                const int m = m0 + ps * PRQ + rl;
+                if (m < p.M) {
+                    const float4 y = *(const float4 *) (tl + rl * RS + 4 * lane);
+                    quant_q8k_block(y, lane, p.outH + (int64_t) m * p.ldo + n0 + 4 * lane, p.qdy + (int64_t) kb * p.dy_ld + m,
+                                    p.qaext + ((int64_t) kb * p.dy_ld + m) * 16);
+                }
+            }
+            __syncthreads();
+        }
+        return;
+    }
+
     // ---- epilogue. Per-element math (bias, scale, GELU) in registers, then an LDS transpose per wave so every
     // global access is 16 B per lane along a row (8 B along t for V^T) instead of 2-4 B scattered stores
     // (the 16x16 C layout gives each lane 4 rows of ONE column). The operand images are dead: reuse the LDS.
@@ -345,18 +391,28 @@ hipError_t launch_cfg(const q2a_gemm_args & a, hipStream_t s) {
     return hipGetLastError();
 }
 
-template <int EPI>
-hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
+bool wide_tiles(int M, int N) {
     // big M: 256-wide tiles on 8 waves (k-quant variants keep 128 rows: the per-block accumulators double the
     // register footprint); small M (a single clip): 128x128 on 4 waves so the grid still covers the 256 CUs
     static const int force = [] { const char * v = getenv("Q2A_GEMM_TILE"); return v ? atoi(v) : 0; }();  // 1 big, 2 small
-    bool big = (int64_t) ((a.M + 255) / 256) * (a.N / 256) >= 512 && a.N % 256 == 0;
-    if (force == 1 && a.N % 256 == 0) big = true;
+    bool big = (int64_t) ((M + 255) / 256) * (N / 256) >= 512 && N % 256 == 0;
+    if (force == 1 && N % 256 == 0) big = true;
     if (force == 2) big = false;
-    if (blk == 0) return big ? launch_cfg<256, 256, 2, 4, EPI, 0>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 0>(a, s);
-    if (blk == 256) return big ? launch_cfg<128, 256, 2, 4, EPI, 256>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 256>(a, s);
-    if (blk == 32) return big ? launch_cfg<128, 256, 2, 4, EPI, 32>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 32>(a, s);
-    return hipErrorInvalidValue;
+    return big;
+}
+
+template <int EPI>
+hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
+    const bool big = wide_tiles(a.M, a.N);
+    if constexpr (EPI == Q2A_EPI_GELU_Q8K) {
+        if (!big || blk != 256) return hipErrorInvalidValue;
+        return launch_cfg<128, 256, 2, 4, EPI, 256>(a, s);
+    } else {
+        if (blk == 0) return big ? launch_cfg<256, 256, 2, 4, EPI, 0>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 0>(a, s);
+        if (blk == 256) return big ? launch_cfg<128, 256, 2, 4, EPI, 256>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 256>(a, s);
+        if (blk == 32) return big ? launch_cfg<128, 256, 2, 4, EPI, 32>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 32>(a, s);
+        return hipErrorInvalidValue;
+    }
 }
 
 }  // namespace
@@ -371,6 +427,9 @@ hipError_t q2a_launch_gemm(const q2a_gemm_args & a, int epi, int blk, hipStream_
         case Q2A_EPI_CONV2: return launch_epi<Q2A_EPI_CONV2>(a, blk, s);
         case Q2A_EPI_GELU_F: return launch_epi<Q2A_EPI_GELU_F>(a, blk, s);
         case Q2A_EPI_STORE_F: return launch_epi<Q2A_EPI_STORE_F>(a, blk, s);
+        case Q2A_EPI_GELU_Q8K: return launch_epi<Q2A_EPI_GELU_Q8K>(a, blk, s);
         default: return hipErrorInvalidValue;
     }
 }
+
+bool q2a_gemm_wide_tiles(int M, int N, int blk) { (void) blk; return wide_tiles(M, N); }

@@ -15,6 +15,8 @@ enum q2a_epi {
     Q2A_EPI_CONV2 = 3,      // outF[m][n] = gelu_lut(acc + bias[n]) + pe[m % T][n] (conv2 + positional add)
     Q2A_EPI_GELU_F = 4,     // outF[m][n] = gelu_lut(acc + bias[n])               (fc1 on the quantized paths)
     Q2A_EPI_STORE_F = 5,    // outF[m][n] = acc                                   (unit tests)
+    Q2A_EPI_GELU_Q8K = 6,   // gelu_lut(acc + bias) quantized to Q8_K in-tile: codes -> outH, d -> dy, bsums -> aext
+                            // (fc1 on the Q4_K path; needs the 256-column tile = one Q8_K block per row)
 };
 
 struct q2a_gemm_args {
@@ -45,12 +47,16 @@ struct q2a_gemm_args {
     const float * dmin;               // [nblk][N] (Q4_K only)
     const q2a_half * aext;            // [nblk][dy_ld][16] bsum hi/lo pairs (Q4_K only)
     const q2a_half * wext;            // [nblk][N][16] (64*m_j, m_j) pairs (Q4_K only)
+    float * qdy;                      // Q2A_EPI_GELU_Q8K outputs: block-major d [N/256][dy_ld] and
+    q2a_half * qaext;                 //   bsum operand [N/256][dy_ld][16] of the produced activation
     int nblk;
     int dy_ld;                        // row stride of dy/aext (M rounded up to 256)
 };
 
 // blk: 0 (plain fp16 GEMM), 256 (Q4_K x Q8_K), 32 (Q8_0/Q4_0 x Q8_0)
 hipError_t q2a_launch_gemm(const q2a_gemm_args & a, int epi, int blk, hipStream_t s);
+// true when the launcher will use the 256-column tile configuration for this shape (Q2A_EPI_GELU_Q8K needs it)
+bool q2a_gemm_wide_tiles(int M, int N, int blk);
 
 struct q2a_attn_args {
     const q2a_half *qh, *ql, *kh, *kl, *vt;

@@ -228,3 +228,23 @@ def test_encoder_full_size_batched_big_tiles(engines, make_clip, golden):
         val = g["full_f16_c0_val"]
         mxs, l2s = rel_errors(o[g["full_f16_c0_idx"]], val)
         assert mxs < 1e-3 and l2s < 1e-3, (c, mxs, l2s)
+
+
+# ---------------------------------------------------------------- one encoder block at batched (wide-tile) shapes
+@pytest.mark.parametrize("wt,tol_l2", [("f16", 1e-4), ("q4_k", 2e-3), ("q8_0", 2e-3)])
+def test_block_batched_matches_oracle_layer0(engines, make_model, make_clip, wt, tol_l2):
+    """Layer 0 on 30 copies of the oracle's layer-0 input (M = 45 000 rows: wide tiles, and for Q4_K the fused
+    fc1 + GELU + Q8_K epilogue) against the oracle's own layer-0 output."""
+    e = engines("tiny", wt)
+    mf = ggmlfile.read(make_model("tiny", wt))
+    o = oracle_py.Oracle(mf)
+    _, dumps = o.encode(o.mel_window(o.log_mel(make_clip(0))), dump=True)
+    x0 = dumps["conv_out"]
+    B = 30
+    x = torch.from_numpy(np.tile(x0, (B, 1))).cuda()
+    e.test_block(0, x.data_ptr(), B)
+    torch.cuda.synchronize()
+    out = x.cpu().numpy().reshape(B, 1500, -1)
+    for c in (0, B - 1):
+        mx, l2 = rel_errors(out[c], dumps["x2"])
+        assert l2 < tol_l2, (c, mx, l2)
