@@ -360,6 +360,7 @@ struct q2a_engine {
     float * out_stage = nullptr;     // unused (outputs are written straight to the user buffer)
     int32_t * meta = nullptr;        // device: nsamp | seek | clip_ok | clip_max
     int32_t * meta_host = nullptr;   // pinned
+    hipEvent_t meta_evt = nullptr;   // last async upload out of meta_host (host rewrites wait on it)
     float * mel = nullptr;
     q2a_half * xc1 = nullptr;
     q2a_half * y1 = nullptr;
@@ -375,6 +376,7 @@ struct q2a_engine {
     float * hF = nullptr;
     int TP = 0;
     int dy_ld = 0;
+    bool fuse_q8k = getenv("Q2A_FUSE_Q8K") != nullptr;   // fc1 epilogue quantization (experimental)
 
     // optional per-kernel-class timing with HIP events on the launch stream (q2a_profile_*)
     bool prof = false;
@@ -398,6 +400,7 @@ int engine_init(q2a_engine * e, int device) {
     e->device = device;
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&e->meta_evt, hipEventDisableTiming));
     return Q2A_OK;
 }
 
@@ -556,7 +559,7 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         if (mode == 0) at.outH = e->actD; else at.outF = e->attF;
         PLAUNCH(e, s, Q2A_PROF_ATTN, q2a_launch_attention(at, s));
         if (mode) {
-            q2a_quant_args qa{e->attF, M, d.D, mode, e->actD, e->dyD, e->aextD, e->dy_ld};
+            q2a_quant_args qa{e->attF, nullptr, M, d.D, mode, e->actD, e->dyD, e->aextD, e->dy_ld};
             PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_quant_act(qa, s));
         }
     }
@@ -574,14 +577,16 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         if (mode == 0) {
             a.outH = e->actF; a.ldo = d.F; a.o_rpg = M; a.o_gstride = 0; a.o_off = 0;
             PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_H, 0, s));
-        } else if (mode == 1 && q2a_gemm_wide_tiles(M, d.F, e->blk)) {
+        } else if (mode == 1 && e->fuse_q8k && q2a_gemm_wide_tiles(M, d.F, e->blk)) {
             // fused fc1 + GELU + Q8_K quantization of the fc2 input (one Q8_K block per 256-column tile)
             a.outH = e->actF; a.ldo = d.F; a.qdy = e->dyF; a.qaext = e->aextF;
             PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_Q8K, e->blk, s));
         } else {
-            a.outF = e->hF; a.ldo = d.F;
-            PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_F, e->blk, s));
-            q2a_quant_args qa{e->hF, M, d.F, mode, e->actF, e->dyF, e->aextF, e->dy_ld};
+            // GELU output is exactly fp16-valued (LUT): keep it as fp16, then quantize for fc2
+            q2a_half * hH = (q2a_half *) e->hF;
+            a.outH = hH; a.ldo = d.F; a.o_rpg = M; a.o_gstride = 0; a.o_off = 0;
+            PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_H, e->blk, s));
+            q2a_quant_args qa{nullptr, hH, M, d.F, mode, e->actF, e->dyF, e->aextF, e->dy_ld};
             PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_quant_act(qa, s));
         }
     }
@@ -636,6 +641,7 @@ int run_frontend(q2a_engine * e, const float * pcm, int64_t stride, int B, int m
 int prepare_meta(q2a_engine * e, const int32_t * n_samples, int B, int offset_ms, int32_t * status, int & max_frames,
                  int64_t max_valid, hipStream_t s) {
     int32_t * mh = e->meta_host;
+    HIP_TRY(hipEventSynchronize(e->meta_evt));   // the previous call's upload out of mh may still be queued
     max_frames = 0;
     const int seek = offset_ms / 10;
     for (int c = 0; c < B; ++c) {
@@ -650,6 +656,7 @@ int prepare_meta(q2a_engine * e, const int32_t * n_samples, int B, int offset_ms
         max_frames = std::max(max_frames, (int) (((int64_t) mh[c] + 480000) / 160));
     }
     HIP_TRY(hipMemcpyAsync(e->meta, mh, (size_t) B * 3 * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipEventRecord(e->meta_evt, s));
     return Q2A_OK;
 }
 
@@ -746,6 +753,7 @@ void q2a_close(q2a_engine * e) {
     for (auto & r : e->pending) { (void) hipEventDestroy(r.a); (void) hipEventDestroy(r.b); }
     for (auto ev : e->pool) (void) hipEventDestroy(ev);
     if (e->own_blob && e->blob) (void) hipFree(e->blob);
+    if (e->meta_evt) (void) hipEventDestroy(e->meta_evt);
     if (e->stream) (void) hipStreamDestroy(e->stream);
     delete e;
 }
@@ -815,8 +823,10 @@ int q2a_pcm_to_mel(q2a_engine * e, const float * pcm, int n_samples, float * mel
     int32_t cmax = 0;
     for (int f0 = 0; f0 < n_len && rc == Q2A_OK; f0 += d.TM) {
         int32_t * mh = e->meta_host;
+        if (hipEventSynchronize(e->meta_evt) != hipSuccess) { rc = Q2A_ERR_HIP; break; }
         mh[0] = n_samples; mh[1] = f0; mh[2] = 1;
         if (hipMemcpyAsync(e->meta, mh, 12, hipMemcpyHostToDevice, s) != hipSuccess) { rc = Q2A_ERR_HIP; break; }
+        if (hipEventRecord(e->meta_evt, s) != hipSuccess) { rc = Q2A_ERR_HIP; break; }
         if (hipMemsetAsync(e->meta + 3, 0x80, 4, s) != hipSuccess) { rc = Q2A_ERR_HIP; break; }
         q2a_mel_args ma;
         ma.pcm = dpcm; ma.pcm_stride = n_samples; ma.n_samples = e->meta; ma.seek = e->meta + 1; ma.n_clips = 1;
@@ -888,7 +898,7 @@ int q2a_test_linear(q2a_engine * e, int layer, int which, const float * x, int M
         hipLaunchKernelGGL(k_to_half, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, A, n);
         LAUNCH(hipGetLastError());
     } else {
-        q2a_quant_args qa{x, M, K, mode, A, K == d.D ? e->dyD : e->dyF, K == d.D ? e->aextD : e->aextF, e->dy_ld};
+        q2a_quant_args qa{x, nullptr, M, K, mode, A, K == d.D ? e->dyD : e->dyF, K == d.D ? e->aextD : e->aextF, e->dy_ld};
         LAUNCH(q2a_launch_quant_act(qa, s));
     }
     q2a_gemm_args a = gemm_base(e, layer, which, A, M);

@@ -167,7 +167,7 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 
-template <int MODE, bool LN>
+template <int MODE, bool LN, bool HIN = false>
 __global__ __launch_bounds__(256) void k_rownorm(const float * __restrict__ X, int M, int D, const float * __restrict__ g,
                                                  const float * __restrict__ b, q2a_half * outH, float * dy, q2a_half * aext,
                                                  int nseg, int ld) {
@@ -204,6 +204,17 @@ __global__ __launch_bounds__(256) void k_rownorm(const float * __restrict__ X, i
         s2 = wave_sum_d(s2);
         const float variance = (float) (s2 / D);
         scale = 1.0f / sqrtf(variance + 1e-5f);
+    } else if (HIN) {   // fp16 rows (e.g. the GELU output, exactly fp16-valued by the LUT)
+        typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+        const h4_t * xh = (const h4_t *) ((const q2a_half *) X + (int64_t) row * D);
+#pragma unroll
+        for (int u = 0; u < MAXC; ++u) {
+            const int c = lane + 64 * u;
+            if (c < nch) {
+                const h4_t h = xh[c];
+                v[u] = make_float4((float) h[0], (float) h[1], (float) h[2], (float) h[3]);
+            }
+        }
     } else {
 #pragma unroll
         for (int u = 0; u < MAXC; ++u) {
@@ -318,10 +329,15 @@ hipError_t q2a_launch_quant_act(const q2a_quant_args & a, hipStream_t s) {
     const int nseg = a.K / seg;
     const dim3 grid((a.M * nseg + 3) / 4), blk(256);
     // view X as [M*nseg][seg]: contiguous, and the block structure (256 / 32) never straddles a segment
-    if (a.mode == 1) {
-        hipLaunchKernelGGL((k_rownorm<1, false>), grid, blk, 0, s, a.X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext, nseg, a.dy_ld);
+    const float * X = a.XH ? (const float *) a.XH : a.X;
+    if (a.mode == 1 && a.XH) {
+        hipLaunchKernelGGL((k_rownorm<1, false, true>), grid, blk, 0, s, X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext, nseg, a.dy_ld);
+    } else if (a.mode == 2 && a.XH) {
+        hipLaunchKernelGGL((k_rownorm<2, false, true>), grid, blk, 0, s, X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext, nseg, a.dy_ld);
+    } else if (a.mode == 1) {
+        hipLaunchKernelGGL((k_rownorm<1, false>), grid, blk, 0, s, X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext, nseg, a.dy_ld);
     } else if (a.mode == 2) {
-        hipLaunchKernelGGL((k_rownorm<2, false>), grid, blk, 0, s, a.X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext, nseg, a.dy_ld);
+        hipLaunchKernelGGL((k_rownorm<2, false>), grid, blk, 0, s, X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext, nseg, a.dy_ld);
     } else {
         return hipErrorInvalidValue;
     }

@@ -104,6 +104,7 @@ hipError_t q2a_launch_layernorm(const q2a_ln_args & a, hipStream_t s);
 // activation quantizer for F32 rows (attention output / gelu output on the quantized paths): modes 1, 2
 struct q2a_quant_args {
     const float * X;
+    const q2a_half * XH;   // fp16 input instead of X when non-NULL
     int M, K;
     int mode;
     q2a_half * outH;
