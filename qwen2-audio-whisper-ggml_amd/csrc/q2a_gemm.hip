@@ -54,7 +54,102 @@ __device__ __forceinline__ half8 frag(const char * img, int row, int chunk) {
     return *(const half8 *) (img + row * ROWB + ((chunk ^ (row & 7)) << 4));
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, int BLK>
+// ---- 8-phase pipelined main loop (256x256 tile, 8 waves as 2(M) x 4(N), 128x64 per wave, plain fp16 GEMM).
+// LDS holds 8 half-tile images of 128 rows x 64 K (16 KiB each): two K-step buffers E/O x {A_q0, A_q1, B_q0, B_q1}
+// where A_qX = the X-th 64-row half of each M-wave's 128 rows and B_qX = the X-th 32-column half of each N-wave's
+// 64 columns, so a wave's output quadrant (qm, qn) reads exactly A_q{qm} and B_q{qn}. One K-step = 4 phases, one
+// quadrant each (16 MFMAs); every phase issues one half-tile of glds (2 instructions per thread) and waits with a
+// counted vmcnt(10), so five half-tiles stay in flight across the raw barriers: a staged image is first read six
+// phases after its issue, and each slot is restaged the phase after its last read ("GEMM pipeline").
+__device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&acc)[8][4], char * lds_raw, int m0, int n0,
+                                                int lane, int wave, int wm, int wn) {
+    constexpr int HT = 128 * ROWB;                        // one half-tile image (16 KiB)
+    // per-lane element offsets of this thread's two glds rows in each image (image row ir = i*64 + wave*8 + lane/8)
+    uint32_t aoff[2][2], woff[2][2];
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int ir = i * 64 + wave * 8 + (lane >> 3);
+            const int sw = ((lane & 7) ^ (ir & 7)) << 3;
+            const int am = m0 + (ir >> 6) * 128 + x * 64 + (ir & 63);
+            aoff[x][i] = (uint32_t) (a_row_off(p, min(am, p.M - 1)) + sw);
+            const int wr = n0 + (ir >> 5) * 64 + x * 32 + (ir & 31);
+            woff[x][i] = (uint32_t) ((int64_t) wr * p.ldw + sw);
+        }
+    const int nk = p.K / BK;
+    // image h of buffer b: h = 0 A_q0, 1 A_q1, 2 B_q0, 3 B_q1
+    auto stage = [&](int b, int h, int kt) {
+        const int k0 = min(kt, nk - 1) * BK;               // past the end: harmless re-load into a free slot
+        char * dst = lds_raw + (b * 4 + h) * HT + wave * 8 * ROWB;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const q2a_half * src = h < 2 ? p.A + aoff[h][i] + k0 : p.W + woff[h - 2][i] + k0;
+            __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (dst + i * 64 * ROWB), 16, 0, 0);
+        }
+    };
+    half8 af[4][2], bf[2][2][2];
+    auto read_a = [&](int b, int qm) {
+        const char * img = lds_raw + (b * 4 + qm) * HT;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) af[i][s2] = frag(img, wm * 64 + i * 16 + (lane & 15), s2 * 4 + (lane >> 4));
+    };
+    auto read_b = [&](int b, int qn) {
+        const char * img = lds_raw + (b * 4 + 2 + qn) * HT;
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) bf[qn][j][s2] = frag(img, wn * 32 + j * 16 + (lane & 15), s2 * 4 + (lane >> 4));
+    };
+    auto mma = [&](int qm, int qn) {
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[qm * 4 + i][qn * 2 + j] =
+                        __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][s2], bf[qn][j][s2], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+    };
+#define Q2A_PHASE_BEGIN()                                       \
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");           \
+    __builtin_amdgcn_s_barrier();                               \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          \
+    __builtin_amdgcn_s_setprio(1)
+#define Q2A_PHASE_END()                                         \
+    __builtin_amdgcn_s_setprio(0);                              \
+    asm volatile("" ::: "memory");                              \
+    __builtin_amdgcn_s_barrier();                               \
+    asm volatile("" ::: "memory")
+
+    // prologue: the images "phases 2..8 of iteration -1" would have staged
+    stage(0, 0, 0); stage(0, 2, 0); stage(0, 3, 0); stage(0, 1, 0);
+    stage(1, 0, 1); stage(1, 2, 1); stage(1, 3, 1);
+    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+
+    for (int kt = 0; kt < nk; kt += 2) {
+        // K-step kt in buffer 0
+        read_b(0, 0); read_a(0, 0); stage(1, 1, kt + 1); Q2A_PHASE_BEGIN(); mma(0, 0); Q2A_PHASE_END();
+        read_b(0, 1);               stage(0, 0, kt + 2); Q2A_PHASE_BEGIN(); mma(0, 1); Q2A_PHASE_END();
+        read_a(0, 1);               stage(0, 2, kt + 2); Q2A_PHASE_BEGIN(); mma(1, 1); Q2A_PHASE_END();
+                                    stage(0, 3, kt + 2); Q2A_PHASE_BEGIN(); mma(1, 0); Q2A_PHASE_END();
+        // K-step kt+1 in buffer 1
+        read_b(1, 0); read_a(1, 0); stage(0, 1, kt + 2); Q2A_PHASE_BEGIN(); mma(0, 0); Q2A_PHASE_END();
+        read_b(1, 1);               stage(1, 0, kt + 3); Q2A_PHASE_BEGIN(); mma(0, 1); Q2A_PHASE_END();
+        read_a(1, 1);               stage(1, 2, kt + 3); Q2A_PHASE_BEGIN(); mma(1, 1); Q2A_PHASE_END();
+                                    stage(1, 3, kt + 3); Q2A_PHASE_BEGIN(); mma(1, 0); Q2A_PHASE_END();
+    }
+#undef Q2A_PHASE_BEGIN
+#undef Q2A_PHASE_END
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tail re-loads still land in LDS: drain before the epilogue
+    __syncthreads();
+}
+
+template <int BM, int BN, int WM, int WN, int EPI, int BLK, int PIPE>
 __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p) {
     constexpr int NW = WM * WN;
     constexpr int MI = BM / WM / 16, NJ = BN / WN / 16;   // 16x16 tiles per wave
@@ -83,159 +178,163 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
     const int tm = g * GROUP_M + gr % gm, tn = gr / gm;
     const int m0 = tm * BM, n0 = tn * BN;
 
-    // per-lane source rows of this wave's glds instructions (rows past M clamp to M-1: loaded, never stored)
-    int64_t arow[LA], wrow[LB];
-#pragma unroll
-    for (int i = 0; i < LA; ++i) {
-        const int r = (wave * LA + i) * 8 + (lane >> 3);
-        arow[i] = a_row_off(p, min(m0 + r, p.M - 1)) + (((lane & 7) ^ (r & 7)) << 3);
-    }
-#pragma unroll
-    for (int i = 0; i < LB; ++i) {
-        const int r = (wave * LB + i) * 8 + (lane >> 3);
-        wrow[i] = (int64_t) (n0 + r) * p.ldw + (((lane & 7) ^ (r & 7)) << 3);
-    }
-    auto stage = [&](char * buf, int k0) {
-#pragma unroll
-        for (int i = 0; i < LA; ++i)
-            __builtin_amdgcn_global_load_lds((const void *) (p.A + arow[i] + k0),
-                                             (lds_ptr_t) (buf + (wave * LA + i) * 8 * ROWB), 16, 0, 0);
-#pragma unroll
-        for (int i = 0; i < LB; ++i)
-            __builtin_amdgcn_global_load_lds((const void *) (p.W + wrow[i] + k0),
-                                             (lds_ptr_t) (buf + (BM + (wave * LB + i) * 8) * ROWB), 16, 0, 0);
-    };
-
-    // scale chunk c of K-block group g (BLK=256: block g; BLK=32: blocks 2g, 2g+1) -> global source
-    auto scale_src = [&](int c, int g) -> const uint4 * {
-        if (BLK == 256) {
-            if (c < BM / 4) return (const uint4 *) (p.dy + (int64_t) g * p.dy_ld + m0) + c;
-            c -= BM / 4;
-            if (c < BM * 2) return (const uint4 *) (p.aext + ((int64_t) g * p.dy_ld + m0) * 16) + c;
-            c -= BM * 2;
-            if (c < BN / 4) return (const uint4 *) (p.dx + (int64_t) g * p.N + n0) + c;
-            c -= BN / 4;
-            if (c < BN / 4) return (const uint4 *) (p.dmin + (int64_t) g * p.N + n0) + c;
-            c -= BN / 4;
-            return (const uint4 *) (p.wext + ((int64_t) g * p.N + n0) * 16) + c;
-        } else {
-            if (c < BM / 2) return (const uint4 *) (p.dy + (int64_t) (2 * g + c / (BM / 4)) * p.dy_ld + m0) + c % (BM / 4);
-            c -= BM / 2;
-            return (const uint4 *) (p.dx + (int64_t) (2 * g + c / (BN / 4)) * p.N + n0) + c % (BN / 4);
-        }
-    };
-    uint4 sreg[BLK ? SCH : 1];
-    auto scale_load = [&](int g) {
-#pragma unroll
-        for (int u = 0; u < SCH; ++u) {
-            const int c = tid + u * NT;
-            if (c < SB / 16) sreg[u] = *scale_src(c, g);
-        }
-    };
-    auto scale_store = [&](int buf) {
-#pragma unroll
-        for (int u = 0; u < SCH; ++u) {
-            const int c = tid + u * NT;
-            if (c < SB / 16) *(uint4 *) (sbuf + buf * SB + c * 16) = sreg[u];
-        }
-    };
-
     f4 acc[MI][NJ];
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-    f4 blk[BLK ? MI : 1][BLK ? NJ : 1];
-    if (BLK) {
-#pragma unroll
-        for (int i = 0; i < (BLK ? MI : 1); ++i)
-#pragma unroll
-            for (int j = 0; j < (BLK ? NJ : 1); ++j) blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-    }
-
-    const int nk = p.K / BK;
-    stage(LDS_STAGE(0), 0);
-    if (BLK == 32) scale_load(0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (BLK == 32) scale_store(0);
-    __syncthreads();
-
-    for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nk) stage(LDS_STAGE(cur ^ 1), (kt + 1) * BK);
-        // Q4_K: block kt/4's scales are fetched at its first K-step and land in LDS at its end (3 steps early);
-        // Q8_0: the next K-step's two blocks are fetched one step ahead into the other buffer.
-        const bool sload = BLK == 256 ? (kt % 4 == 0) : (BLK == 32 && kt + 1 < nk);
-        if (sload) scale_load(BLK == 256 ? kt / 4 : kt + 1);
-        const char * ia = LDS_STAGE(cur);
-        const char * iw = LDS_STAGE(cur) + BM * ROWB;
-#pragma unroll
-        for (int s = 0; s < 2; ++s) {
-            const int chunk = s * 4 + (lane >> 4);
-            half8 b[NJ];
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) b[j] = frag(iw, wn * (BN / WN) + j * 16 + (lane & 15), chunk);
-#pragma unroll
-            for (int i = 0; i < MI; ++i) {
-                const half8 a = frag(ia, wm * (BM / WM) + i * 16 + (lane & 15), chunk);
-#pragma unroll
-                for (int j = 0; j < NJ; ++j) {
-                    if (BLK == 0) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[j], acc[i][j], 0, 0, 0);
-                    else blk[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[j], blk[i][j], 0, 0, 0);
-                }
-            }
-            if (BLK) {
-                const int kpos = kt * BK + (s + 1) * 32;   // K consumed so far
-                if (kpos % BLK == 0) {
-                    const char * sb = BLK == 256 ? sbuf : sbuf + cur * SB;
-                    const int sub = BLK == 256 ? 0 : s;                    // which of the K-step's two 32-blocks
-                    const float * s_dy = (const float *) sb + (BLK == 256 ? 0 : sub * BM);
-                    const q2a_half * s_ae = (const q2a_half *) (sb + BM * 4);
-                    const float * s_dx = (const float *) (sb + (BLK == 256 ? BM * 36 : 2 * BM * 4)) + (BLK == 256 ? 0 : sub * BN);
-                    const float * s_dm = (const float *) (sb + BM * 36 + BN * 4);
-                    const q2a_half * s_we = (const q2a_half *) (sb + BM * 36 + BN * 8);
-                    float dx[NJ], dm[NJ];
-                    half4 we[NJ];
-#pragma unroll
-                    for (int j = 0; j < NJ; ++j) {
-                        const int n = wn * (BN / WN) + j * 16 + (lane & 15);
-                        dx[j] = s_dx[n];
-                        if (BLK == 256) {
-                            dm[j] = s_dm[n];
-                            we[j] = *(const half4 *) (s_we + n * 16 + (lane >> 4) * 4);
-                        }
-                    }
-#pragma unroll
-                    for (int i = 0; i < MI; ++i) {
-                        const float4 dyv = *(const float4 *) (s_dy + wm * (BM / WM) + i * 16 + (lane >> 4) * 4);
-                        const float dy[4] = {dyv.x, dyv.y, dyv.z, dyv.w};
-                        half4 ae;
-                        if (BLK == 256) {
-                            // min term S2 = sum_j m_j * bsum32_j: one 16x16x16 MFMA per tile on (hi,lo)-split bsums
-                            ae = *(const half4 *) (s_ae + (wm * (BM / WM) + i * 16 + (lane & 15)) * 16 + (lane >> 4) * 4);
-                        }
-#pragma unroll
-                        for (int j = 0; j < NJ; ++j) {
-                            if (BLK == 256) {
-                                const f4 s2 = __builtin_amdgcn_mfma_f32_16x16x16f16(ae, we[j], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-#pragma unroll
-                                for (int r = 0; r < 4; ++r) {
-                                    acc[i][j][r] += (dy[r] * dx[j]) * blk[i][j][r];
-                                    acc[i][j][r] -= (dy[r] * dm[j]) * s2[r];
-                                }
-                            } else {
-#pragma unroll
-                                for (int r = 0; r < 4; ++r) acc[i][j][r] += (dx[j] * dy[r]) * blk[i][j][r];
-                            }
-                            blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-                        }
-                    }
-                }
-            }
+    if constexpr (PIPE == 1) {
+        mainloop_8phase(p, acc, lds_raw, m0, n0, lane, wave, wm, wn);
+    } else {
+        // per-lane source rows of this wave's glds instructions (rows past M clamp to M-1: loaded, never stored)
+        int64_t arow[LA], wrow[LB];
+    #pragma unroll
+        for (int i = 0; i < LA; ++i) {
+            const int r = (wave * LA + i) * 8 + (lane >> 3);
+            arow[i] = a_row_off(p, min(m0 + r, p.M - 1)) + (((lane & 7) ^ (r & 7)) << 3);
         }
+    #pragma unroll
+        for (int i = 0; i < LB; ++i) {
+            const int r = (wave * LB + i) * 8 + (lane >> 3);
+            wrow[i] = (int64_t) (n0 + r) * p.ldw + (((lane & 7) ^ (r & 7)) << 3);
+        }
+        auto stage = [&](char * buf, int k0) {
+    #pragma unroll
+            for (int i = 0; i < LA; ++i)
+                __builtin_amdgcn_global_load_lds((const void *) (p.A + arow[i] + k0),
+                                                 (lds_ptr_t) (buf + (wave * LA + i) * 8 * ROWB), 16, 0, 0);
+    #pragma unroll
+            for (int i = 0; i < LB; ++i)
+                __builtin_amdgcn_global_load_lds((const void *) (p.W + wrow[i] + k0),
+                                                 (lds_ptr_t) (buf + (BM + (wave * LB + i) * 8) * ROWB), 16, 0, 0);
+        };
+
+        // scale chunk c of K-block group g (BLK=256: block g; BLK=32: blocks 2g, 2g+1) -> global source
+        auto scale_src = [&](int c, int g) -> const uint4 * {
+            if (BLK == 256) {
+                if (c < BM / 4) return (const uint4 *) (p.dy + (int64_t) g * p.dy_ld + m0) + c;
+                c -= BM / 4;
+                if (c < BM * 2) return (const uint4 *) (p.aext + ((int64_t) g * p.dy_ld + m0) * 16) + c;
+                c -= BM * 2;
+                if (c < BN / 4) return (const uint4 *) (p.dx + (int64_t) g * p.N + n0) + c;
+                c -= BN / 4;
+                if (c < BN / 4) return (const uint4 *) (p.dmin + (int64_t) g * p.N + n0) + c;
+                c -= BN / 4;
+                return (const uint4 *) (p.wext + ((int64_t) g * p.N + n0) * 16) + c;
+            } else {
+                if (c < BM / 2) return (const uint4 *) (p.dy + (int64_t) (2 * g + c / (BM / 4)) * p.dy_ld + m0) + c % (BM / 4);
+                c -= BM / 2;
+                return (const uint4 *) (p.dx + (int64_t) (2 * g + c / (BN / 4)) * p.N + n0) + c % (BN / 4);
+            }
+        };
+        uint4 sreg[BLK ? SCH : 1];
+        auto scale_load = [&](int g) {
+    #pragma unroll
+            for (int u = 0; u < SCH; ++u) {
+                const int c = tid + u * NT;
+                if (c < SB / 16) sreg[u] = *scale_src(c, g);
+            }
+        };
+        auto scale_store = [&](int buf) {
+    #pragma unroll
+            for (int u = 0; u < SCH; ++u) {
+                const int c = tid + u * NT;
+                if (c < SB / 16) *(uint4 *) (sbuf + buf * SB + c * 16) = sreg[u];
+            }
+        };
+
+        f4 blk[BLK ? MI : 1][BLK ? NJ : 1];
+        if (BLK) {
+    #pragma unroll
+            for (int i = 0; i < (BLK ? MI : 1); ++i)
+    #pragma unroll
+                for (int j = 0; j < (BLK ? NJ : 1); ++j) blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+        }
+
+        const int nk = p.K / BK;
+        stage(LDS_STAGE(0), 0);
+        if (BLK == 32) scale_load(0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (sload) scale_store(BLK == 256 ? 0 : cur ^ 1);
+        if (BLK == 32) scale_store(0);
         __syncthreads();
+
+        for (int kt = 0; kt < nk; ++kt) {
+            const int cur = kt & 1;
+            if (kt + 1 < nk) stage(LDS_STAGE(cur ^ 1), (kt + 1) * BK);
+            // Q4_K: block kt/4's scales are fetched at its first K-step and land in LDS at its end (3 steps early);
+            // Q8_0: the next K-step's two blocks are fetched one step ahead into the other buffer.
+            const bool sload = BLK == 256 ? (kt % 4 == 0) : (BLK == 32 && kt + 1 < nk);
+            if (sload) scale_load(BLK == 256 ? kt / 4 : kt + 1);
+            const char * ia = LDS_STAGE(cur);
+            const char * iw = LDS_STAGE(cur) + BM * ROWB;
+    #pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const int chunk = s * 4 + (lane >> 4);
+                half8 b[NJ];
+    #pragma unroll
+                for (int j = 0; j < NJ; ++j) b[j] = frag(iw, wn * (BN / WN) + j * 16 + (lane & 15), chunk);
+    #pragma unroll
+                for (int i = 0; i < MI; ++i) {
+                    const half8 a = frag(ia, wm * (BM / WM) + i * 16 + (lane & 15), chunk);
+    #pragma unroll
+                    for (int j = 0; j < NJ; ++j) {
+                        if (BLK == 0) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[j], acc[i][j], 0, 0, 0);
+                        else blk[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[j], blk[i][j], 0, 0, 0);
+                    }
+                }
+                if (BLK) {
+                    const int kpos = kt * BK + (s + 1) * 32;   // K consumed so far
+                    if (kpos % BLK == 0) {
+                        const char * sb = BLK == 256 ? sbuf : sbuf + cur * SB;
+                        const int sub = BLK == 256 ? 0 : s;                    // which of the K-step's two 32-blocks
+                        const float * s_dy = (const float *) sb + (BLK == 256 ? 0 : sub * BM);
+                        const q2a_half * s_ae = (const q2a_half *) (sb + BM * 4);
+                        const float * s_dx = (const float *) (sb + (BLK == 256 ? BM * 36 : 2 * BM * 4)) + (BLK == 256 ? 0 : sub * BN);
+                        const float * s_dm = (const float *) (sb + BM * 36 + BN * 4);
+                        const q2a_half * s_we = (const q2a_half *) (sb + BM * 36 + BN * 8);
+                        float dx[NJ], dm[NJ];
+                        half4 we[NJ];
+    #pragma unroll
+                        for (int j = 0; j < NJ; ++j) {
+                            const int n = wn * (BN / WN) + j * 16 + (lane & 15);
+                            dx[j] = s_dx[n];
+                            if (BLK == 256) {
+                                dm[j] = s_dm[n];
+                                we[j] = *(const half4 *) (s_we + n * 16 + (lane >> 4) * 4);
+                            }
+                        }
+    #pragma unroll
+                        for (int i = 0; i < MI; ++i) {
+                            const float4 dyv = *(const float4 *) (s_dy + wm * (BM / WM) + i * 16 + (lane >> 4) * 4);
+                            const float dy[4] = {dyv.x, dyv.y, dyv.z, dyv.w};
+                            half4 ae;
+                            if (BLK == 256) {
+                                // min term S2 = sum_j m_j * bsum32_j: one 16x16x16 MFMA per tile on (hi,lo)-split bsums
+                                ae = *(const half4 *) (s_ae + (wm * (BM / WM) + i * 16 + (lane & 15)) * 16 + (lane >> 4) * 4);
+                            }
+    #pragma unroll
+                            for (int j = 0; j < NJ; ++j) {
+                                if (BLK == 256) {
+                                    const f4 s2 = __builtin_amdgcn_mfma_f32_16x16x16f16(ae, we[j], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    #pragma unroll
+                                    for (int r = 0; r < 4; ++r) {
+                                        acc[i][j][r] += (dy[r] * dx[j]) * blk[i][j][r];
+                                        acc[i][j][r] -= (dy[r] * dm[j]) * s2[r];
+                                    }
+                                } else {
+    #pragma unroll
+                                    for (int r = 0; r < 4; ++r) acc[i][j][r] += (dx[j] * dy[r]) * blk[i][j][r];
+                                }
+                                blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+                            }
+                        }
+                    }
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            if (sload) scale_store(BLK == 256 ? 0 : cur ^ 1);
+            __syncthreads();
+        }
     }
 
     if constexpr (EPI == Q2A_EPI_GELU_Q8K) {
@@ -384,10 +483,10 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
 #undef LDS_STAGE
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, int BLK>
+template <int BM, int BN, int WM, int WN, int EPI, int BLK, int PIPE = 0>
 hipError_t launch_cfg(const q2a_gemm_args & a, hipStream_t s) {
     const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM);
-    hipLaunchKernelGGL((k_gemm<BM, BN, WM, WN, EPI, BLK>), dim3(nwg), dim3(WM * WN * 64), 0, s, a);
+    hipLaunchKernelGGL((k_gemm<BM, BN, WM, WN, EPI, BLK, PIPE>), dim3(nwg), dim3(WM * WN * 64), 0, s, a);
     return hipGetLastError();
 }
 
@@ -404,11 +503,19 @@ bool wide_tiles(int M, int N) {
 template <int EPI>
 hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
     const bool big = wide_tiles(a.M, a.N);
+    static const bool pipe8 = [] { const char * v = getenv("Q2A_GEMM_PIPE"); return v ? atoi(v) != 0 : true; }();
     if constexpr (EPI == Q2A_EPI_GELU_Q8K) {
         if (!big || blk != 256) return hipErrorInvalidValue;
         return launch_cfg<128, 256, 2, 4, EPI, 256>(a, s);
     } else {
-        if (blk == 0) return big ? launch_cfg<256, 256, 2, 4, EPI, 0>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 0>(a, s);
+        if (blk == 0) {
+            // 8-phase pipeline needs an even number (>= 2) of 64-deep K-steps
+            // (it addresses operands with 32-bit element offsets)
+            const int64_t last = (int64_t) ((a.M - 1) / a.a_rpg) * a.a_gstride + (int64_t) ((a.M - 1) % a.a_rpg) * a.a_step;
+            const bool fits = (last + 1) * a.lda < (1ll << 32) && (int64_t) a.N * a.ldw < (1ll << 32);
+            if (big && pipe8 && fits && (a.K / BK) % 2 == 0) return launch_cfg<256, 256, 2, 4, EPI, 0, 1>(a, s);
+            return big ? launch_cfg<256, 256, 2, 4, EPI, 0>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 0>(a, s);
+        }
         if (blk == 256) return big ? launch_cfg<128, 256, 2, 4, EPI, 256>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 256>(a, s);
         if (blk == 32) return big ? launch_cfg<128, 256, 2, 4, EPI, 32>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 32>(a, s);
         return hipErrorInvalidValue;
