@@ -46,13 +46,14 @@ void set_err(const char * fmt, ...) {
 // packed device blob: 16 KiB self-describing header + 256-B aligned sections
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t BLOB_MAGIC = 0x42413251u;   // "Q2AB"
-constexpr uint32_t BLOB_VERSION = 1;
+constexpr uint32_t BLOB_VERSION = 2;
 constexpr int MAX_LAYERS = 64;
-constexpr size_t HEADER_BYTES = 16384;
+constexpr size_t HEADER_BYTES = 32768;
 
 enum { G_CONV1_W, G_CONV1_B, G_CONV2_W, G_CONV2_B, G_PE, G_LNP_W, G_LNP_B, G_FILT, G_TAB, G_GELU, G_COUNT };
-// per-matrix arrays: W (fp16 [N][K]), DX (f32 [N][nblk]), DMIN (f32 [N][nblk]), WEXT (fp16 [N][nblk][16])
-enum { A_W, A_DX, A_DMIN, A_WEXT, A_COUNT };
+// per-matrix arrays: W (fp16 [N][K]); block-major DX, DMIN, BETA = DX_{b-1}/DX_b, GAMMA = DMIN_b/DX_b (f32 [nblk][N]),
+// WEXT (fp16 [nblk][N][16])
+enum { A_W, A_DX, A_DMIN, A_WEXT, A_BETA, A_GAMMA, A_COUNT };
 enum { L_BQKV, L_BO, L_B1, L_B2, L_LN1W, L_LN1B, L_LN2W, L_LN2B, L_MAT0, L_COUNT = L_MAT0 + 4 * A_COUNT };
 
 struct blob_header {
@@ -120,6 +121,8 @@ bool plan(blob_header & h, const q2a_hparams & hp, int wtype) {
             if (h.blk == 256) {
                 a[A_DMIN] = take((uint64_t) N * (K / 256) * 4);
                 a[A_WEXT] = take((uint64_t) N * (K / 256) * 16 * 2);
+                a[A_BETA] = take((uint64_t) N * (K / 256) * 4);
+                a[A_GAMMA] = take((uint64_t) N * (K / 256) * 4);
             }
         }
     }
@@ -152,11 +155,21 @@ void expand_rows(const uint8_t * src, int wtype, int K, int Ntot, int r0, int r1
             const int nb = K / 256;
             float * dx = (float *) (blob + a[A_DX]);
             float * dm = (float *) (blob + a[A_DMIN]);
+            float * be = (float *) (blob + a[A_BETA]);
+            float * ga = (float *) (blob + a[A_GAMMA]);
             uint16_t * we = (uint16_t *) (blob + a[A_WEXT]);
+            float dprev = 1.0f;
             for (int b = 0; b < nb; ++b) {
                 const q2a_block_q4_K * x = (const q2a_block_q4_K *) row + b;
-                dx[(size_t) b * Ntot + n] = q2a_fp16_to_fp32(x->d);
+                // d = 0: the block's d*sc*q terms vanish; store dx = 1 with zero weights instead (same products,
+                // and the block-ratio rescaling of the 8-phase kernel never divides by zero)
+                const float d = q2a_fp16_to_fp32(x->d);
+                const float deff = d != 0.0f ? d : 1.0f;
+                dx[(size_t) b * Ntot + n] = deff;
                 dm[(size_t) b * Ntot + n] = q2a_fp16_to_fp32(x->dmin);
+                be[(size_t) b * Ntot + n] = dprev / deff;
+                ga[(size_t) b * Ntot + n] = q2a_fp16_to_fp32(x->dmin) / deff;
+                dprev = deff;
                 for (int j = 0; j < 8; ++j) {
                     uint8_t sc, m;
                     scale_min_k4(j, x->scales, &sc, &m);
@@ -165,7 +178,7 @@ void expand_rows(const uint8_t * src, int wtype, int K, int Ntot, int r0, int r1
                     const uint8_t * q = x->qs + 32 * (j / 2);
                     for (int l = 0; l < 32; ++l) {
                         const int v = (j & 1) ? (q[l] >> 4) : (q[l] & 0xF);
-                        wr[b * 256 + 32 * j + l] = q2a_fp32_to_fp16((float) (sc * v));
+                        wr[b * 256 + 32 * j + l] = q2a_fp32_to_fp16(d != 0.0f ? (float) (sc * v) : 0.0f);
                     }
                 }
             }
@@ -503,6 +516,8 @@ q2a_gemm_args gemm_base(const q2a_engine * e, int l, int which, const q2a_half *
         if (e->blk == 256) {
             a.dmin = (const float *) (e->blob + m[A_DMIN]);
             a.wext = (const q2a_half *) (e->blob + m[A_WEXT]);
+            a.beta = (const float *) (e->blob + m[A_BETA]);
+            a.gamma = (const float *) (e->blob + m[A_GAMMA]);
             a.aext = K == e->d.D ? e->aextD : e->aextF;
         }
     }

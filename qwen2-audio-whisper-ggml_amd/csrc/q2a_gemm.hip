@@ -54,13 +54,26 @@ __device__ __forceinline__ half8 frag(const char * img, int row, int chunk) {
     return *(const half8 *) (img + row * ROWB + ((chunk ^ (row & 7)) << 4));
 }
 
-// ---- 8-phase pipelined main loop (256x256 tile, 8 waves as 2(M) x 4(N), 128x64 per wave, plain fp16 GEMM).
+// ---- 8-phase pipelined main loop (256x256 tile, 8 waves as 2(M) x 4(N), 128x64 per wave).
 // LDS holds 8 half-tile images of 128 rows x 64 K (16 KiB each): two K-step buffers E/O x {A_q0, A_q1, B_q0, B_q1}
 // where A_qX = the X-th 64-row half of each M-wave's 128 rows and B_qX = the X-th 32-column half of each N-wave's
 // 64 columns, so a wave's output quadrant (qm, qn) reads exactly A_q{qm} and B_q{qn}. One K-step = 4 phases, one
 // quadrant each (16 MFMAs); every phase issues one half-tile of glds (2 instructions per thread) and waits with a
-// counted vmcnt(10), so five half-tiles stay in flight across the raw barriers: a staged image is first read six
+// counted vmcnt, so five phases of loads stay in flight across the raw barriers: a staged image is first read six
 // phases after its issue, and each slot is restaged the phase after its last read ("GEMM pipeline").
+//
+// BLK = 256 (Q4_K weights x Q8_K activations) keeps ONE accumulator per output in units of the current block's
+// scale u_b = dy_b[m] * dx_b[n]: at the start of block b, acc <- acc * (dy_{b-1}/dy_b)[m] * (dx_{b-1}/dx_b)[n]
+// - (dmin_b/dx_b)[n] * S2_b (the min term, one 16x16x16 MFMA on the (hi,lo)-split bsums), then the block's MFMAs
+// add its exact integer sum; after the last block acc * u_last. Algebraically ggml's sum_b (d*isum - dmin*summs)
+// (ggml-quants.c:7795-7858); the per-block separation of the integer sums is kept, only the fp32 combination
+// order differs. The 21 KiB of block scales are staged by glds once per block (phase 2), with the vmcnt counts of
+// the following five phases raised by those 3 instructions. Zero scales never occur (quantizers store d = 1 for
+// an all-zero activation block, the pack stores dx = 1 and zero weights for a d = 0 weight block).
+constexpr int SBUF_OFF = 8 * 128 * ROWB;     // 128 KiB: scale staging after the 8 operand images
+constexpr int SBUF_BYTES = 24 * 1024;       // 21 pieces of 1 KiB (+3 pad slots for the uniform 3 glds per thread)
+
+template <int BLK>
 __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&acc)[8][4], char * lds_raw, int m0, int n0,
                                                 int lane, int wave, int wm, int wn) {
     constexpr int HT = 128 * ROWB;                        // one half-tile image (16 KiB)
@@ -88,20 +101,108 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (dst + i * 64 * ROWB), 16, 0, 0);
         }
     };
+    // block scales of Q4_K block kb -> LDS pieces: 0 dy_{kb-1} | 1 dy_kb | 2 beta | 3 gamma | 4 dx | 5-12 aext | 13-20 wext
+    char * sbuf = lds_raw + SBUF_OFF;
+    // this wave's three pieces: wave-uniform base/stride per piece (SGPRs), picked once
+    const char * sb_base[3];
+    int64_t sb_stride[3];
+    bool sb_prev[3];
+#pragma unroll
+    for (int u = 0; u < 3; ++u) {
+        const int pc = wave * 3 + u;
+        sb_prev[u] = pc == 0;
+        if (pc <= 1 || pc >= 21) { sb_base[u] = (const char *) (p.dy + m0); sb_stride[u] = (int64_t) p.dy_ld * 4; }
+        else if (pc == 2) { sb_base[u] = (const char *) (p.beta + n0); sb_stride[u] = (int64_t) p.N * 4; }
+        else if (pc == 3) { sb_base[u] = (const char *) (p.gamma + n0); sb_stride[u] = (int64_t) p.N * 4; }
+        else if (pc == 4) { sb_base[u] = (const char *) (p.dx + n0); sb_stride[u] = (int64_t) p.N * 4; }
+        else if (pc < 13) { sb_base[u] = (const char *) (p.aext + (int64_t) m0 * 16) + (pc - 5) * 1024; sb_stride[u] = (int64_t) p.dy_ld * 32; }
+        else { sb_base[u] = (const char *) (p.wext + (int64_t) n0 * 16) + (pc - 13) * 1024; sb_stride[u] = (int64_t) p.N * 32; }
+    }
+    auto stage_scales = [&](int kb) {
+        kb = min(kb, p.K / 256 - 1);
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int k = sb_prev[u] ? max(kb - 1, 0) : kb;
+            const char * src = sb_base[u] + k * sb_stride[u] + lane * 16;
+            __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (sbuf + (wave * 3 + u) * 1024), 16, 0, 0);
+        }
+    };
+    // start of block kb: acc <- acc * alpha[m] * beta[n] - gamma[n] * S2[m][n]
+    // LDS reads below go through integer AS3 addresses (no IR link to the glds destination array): hipcc would
+    // otherwise guard each read of the scale buffer with a vmcnt(0) that drains the whole pipeline
+    typedef const __attribute__((address_space(3))) float * lds_fp;
+    typedef const __attribute__((address_space(3))) f4 * lds_f4p;
+    typedef const __attribute__((address_space(3))) half4 * lds_h4p;
+    const uint32_t lds0 = (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) char *) lds_raw;
+    const uint32_t sb0 = lds0 + SBUF_OFF;
+    // start of block kb: acc <- acc * alpha[m] * beta[n] - gamma[n] * S2[m][n]. The scale-buffer reads are inline
+    // asm with an explicit lgkmcnt wait tied to their results: a compiler-visible LDS read of this array gets a
+    // vmcnt(0) guard against the in-flight glds that would drain the whole pipeline once per block.
+    auto block_start = [&]() {
+        const uint32_t s_dy = sb0 + (wm * 128 + (lane >> 4) * 4) * 4;                       // piece 0 | piece 1 at +1024
+        const uint32_t s_ae = sb0 + 5 * 1024 + (wm * 128 + (lane & 15)) * 32 + (lane >> 4) * 8;
+        const uint32_t s_cn = sb0 + 2048 + (wn * 64 + (lane & 15)) * 4;                      // beta | gamma at +1024
+        const uint32_t s_we = sb0 + 13 * 1024 + (wn * 64 + (lane & 15)) * 32 + (lane >> 4) * 8;
+        float bet[4], gam[4];
+        half4 we[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(bet[j]) : "v"(s_cn), "i"(j * 64));
+            asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(gam[j]) : "v"(s_cn), "i"(1024 + j * 64));
+            asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(we[j]) : "v"(s_we), "i"(j * 512));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bet[0]), "+v"(bet[1]), "+v"(bet[2]), "+v"(bet[3]), "+v"(gam[0]),
+                     "+v"(gam[1]), "+v"(gam[2]), "+v"(gam[3]), "+v"(we[0]), "+v"(we[1]), "+v"(we[2]), "+v"(we[3]));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            f4 yp, yc;
+            half4 ae;
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(yp) : "v"(s_dy), "i"(i * 64));
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(yc) : "v"(s_dy), "i"(1024 + i * 64));
+            asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(ae) : "v"(s_ae), "i"(i * 512));
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(yp), "+v"(yc), "+v"(ae));
+            const float al[4] = {yp[0] * __builtin_amdgcn_rcpf(yc[0]), yp[1] * __builtin_amdgcn_rcpf(yc[1]),
+                                 yp[2] * __builtin_amdgcn_rcpf(yc[2]), yp[3] * __builtin_amdgcn_rcpf(yc[3])};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const f4 s2 = __builtin_amdgcn_mfma_f32_16x16x16f16(ae, we[j], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] * (al[r] * bet[j]) - gam[j] * s2[r];
+            }
+            __builtin_amdgcn_sched_barrier(0);   // one row block at a time: bounds the live min-term results
+        }
+    };
+    // fragment reads: 8 per-lane LDS byte addresses ([buffer][k-half]) + compile-time offsets, re-laundered every
+    // phase so the compiler cannot hoist one address register per (image, tile) out of the loop
+    uint32_t abase[2][2], bbase[2][2];
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+        const uint32_t lb = (lane & 15) * ROWB + ((((lane >> 4) | (s2 << 2)) ^ (lane & 7)) << 4);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+            abase[b][s2] = lds0 + b * 4 * HT + wm * 64 * ROWB + lb;
+            bbase[b][s2] = lds0 + (b * 4 + 2) * HT + wn * 32 * ROWB + lb;
+        }
+    }
+    auto launder = [&]() {
+        asm volatile("" : "+v"(abase[0][0]), "+v"(abase[0][1]), "+v"(abase[1][0]), "+v"(abase[1][1]),
+                          "+v"(bbase[0][0]), "+v"(bbase[0][1]), "+v"(bbase[1][0]), "+v"(bbase[1][1]));
+    };
+    typedef const __attribute__((address_space(3))) half8 * lds_h8p;
     half8 af[4][2], bf[2][2][2];
     auto read_a = [&](int b, int qm) {
-        const char * img = lds_raw + (b * 4 + qm) * HT;
+        launder();
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) af[i][s2] = frag(img, wm * 64 + i * 16 + (lane & 15), s2 * 4 + (lane >> 4));
+            for (int s2 = 0; s2 < 2; ++s2) af[i][s2] = *(lds_h8p) (uintptr_t) (abase[b][s2] + qm * HT + i * 16 * ROWB);
     };
     auto read_b = [&](int b, int qn) {
-        const char * img = lds_raw + (b * 4 + 2 + qn) * HT;
+        launder();
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) bf[qn][j][s2] = frag(img, wn * 32 + j * 16 + (lane & 15), s2 * 4 + (lane >> 4));
+            for (int s2 = 0; s2 < 2; ++s2) bf[qn][j][s2] = *(lds_h8p) (uintptr_t) (bbase[b][s2] + qn * HT + j * 16 * ROWB);
     };
     auto mma = [&](int qm, int qn) {
 #pragma unroll
@@ -113,40 +214,66 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
                     acc[qm * 4 + i][qn * 2 + j] =
                         __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][s2], bf[qn][j][s2], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
     };
-#define Q2A_PHASE_BEGIN()                                       \
-    asm volatile("s_waitcnt vmcnt(10)" ::: "memory");           \
+#define Q2A_PB(N)                                               \
+    asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory");       \
     __builtin_amdgcn_s_barrier();                               \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          \
     __builtin_amdgcn_s_setprio(1)
-#define Q2A_PHASE_END()                                         \
+#define Q2A_PE()                                                \
     __builtin_amdgcn_s_setprio(0);                              \
     asm volatile("" ::: "memory");                              \
     __builtin_amdgcn_s_barrier();                               \
     asm volatile("" ::: "memory")
+// the four phases of one K-step in buffer B; S1..S4 = the stage statements issued in each phase
+#define Q2A_KSTEP(B, S1, S2, S3, S4, V1, V2, V3, V4)                                      \
+    read_b(B, 0); read_a(B, 0); S1; Q2A_PB(V1); mma(0, 0); Q2A_PE();                      \
+    read_b(B, 1);               S2; Q2A_PB(V2); mma(0, 1); Q2A_PE();                      \
+    read_a(B, 1);               S3; Q2A_PB(V3); mma(1, 1); Q2A_PE();                      \
+                                S4; Q2A_PB(V4); mma(1, 0); Q2A_PE()
 
-    // prologue: the images "phases 2..8 of iteration -1" would have staged
+    // prologue: the images "phases 2..8 of iteration -1" would have staged (block 0's scales before them)
+    if constexpr (BLK == 256) stage_scales(0);
     stage(0, 0, 0); stage(0, 2, 0); stage(0, 3, 0); stage(0, 1, 0);
     stage(1, 0, 1); stage(1, 2, 1); stage(1, 3, 1);
     asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
 
-    for (int kt = 0; kt < nk; kt += 2) {
-        // K-step kt in buffer 0
-        read_b(0, 0); read_a(0, 0); stage(1, 1, kt + 1); Q2A_PHASE_BEGIN(); mma(0, 0); Q2A_PHASE_END();
-        read_b(0, 1);               stage(0, 0, kt + 2); Q2A_PHASE_BEGIN(); mma(0, 1); Q2A_PHASE_END();
-        read_a(0, 1);               stage(0, 2, kt + 2); Q2A_PHASE_BEGIN(); mma(1, 1); Q2A_PHASE_END();
-                                    stage(0, 3, kt + 2); Q2A_PHASE_BEGIN(); mma(1, 0); Q2A_PHASE_END();
-        // K-step kt+1 in buffer 1
-        read_b(1, 0); read_a(1, 0); stage(0, 1, kt + 2); Q2A_PHASE_BEGIN(); mma(0, 0); Q2A_PHASE_END();
-        read_b(1, 1);               stage(1, 0, kt + 3); Q2A_PHASE_BEGIN(); mma(0, 1); Q2A_PHASE_END();
-        read_a(1, 1);               stage(1, 2, kt + 3); Q2A_PHASE_BEGIN(); mma(1, 1); Q2A_PHASE_END();
-                                    stage(1, 3, kt + 3); Q2A_PHASE_BEGIN(); mma(1, 0); Q2A_PHASE_END();
+    if constexpr (BLK == 0) {
+        for (int kt = 0; kt < nk; kt += 2) {
+            Q2A_KSTEP(0, stage(1, 1, kt + 1), stage(0, 0, kt + 2), stage(0, 2, kt + 2), stage(0, 3, kt + 2), 10, 10, 10, 10);
+            Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 10, 10, 10, 10);
+        }
+    } else {
+        static_assert(BLK == 256, "8-phase k-quant loop is Q4_K only");
+        for (int kt = 0; kt < nk; kt += 4) {
+            block_start();
+            asm volatile("" ::: "memory");
+            Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
+                      stage(0, 3, kt + 2), 10, 13, 13, 13);
+            Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 13, 13, 10, 10);
+            Q2A_KSTEP(0, stage(1, 1, kt + 3), stage(0, 0, kt + 4), stage(0, 2, kt + 4), stage(0, 3, kt + 4), 10, 10, 10, 10);
+            Q2A_KSTEP(1, stage(0, 1, kt + 4), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5), 10, 10, 10, 10);
+        }
     }
-#undef Q2A_PHASE_BEGIN
-#undef Q2A_PHASE_END
+#undef Q2A_KSTEP
+#undef Q2A_PB
+#undef Q2A_PE
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tail re-loads still land in LDS: drain before the epilogue
     __syncthreads();
+    if constexpr (BLK == 256) {
+        // acc is in units of the last block's scale: multiply by dy_last[m] * dx_last[n]
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const float dxn = *(lds_fp) (uintptr_t) (sb0 + 4096 + (wn * 64 + j * 16 + (lane & 15)) * 4);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const f4 yc = *(lds_f4p) (uintptr_t) (sb0 + 1024 + (wm * 128 + i * 16 + (lane >> 4) * 4) * 4);
+#pragma unroll
+                for (int r = 0; r < 4; ++r) acc[i][j][r] *= yc[r] * dxn;
+            }
+        }
+    }
 }
 
 template <int BM, int BN, int WM, int WN, int EPI, int BLK, int PIPE>
@@ -163,10 +290,11 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
     constexpr int NT = NW * 64;
     constexpr int SCH = (SB / 16 + NT - 1) / NT;          // 16-B scale chunks per thread
     constexpr int OPB = (BM + BN) * ROWB;                 // one operand stage (A image | W image)
-    __shared__ __attribute__((aligned(16))) char lds_raw[2 * OPB + (BLK ? NSB * SB : 0)];
+    constexpr int LDS_BYTES = PIPE ? (BLK ? SBUF_OFF + SBUF_BYTES : 2 * OPB) : 2 * OPB + (BLK ? NSB * SB : 0);
+    __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES];
 #define LDS_STAGE(b_) (lds_raw + (b_) * OPB)
     char * sbuf = lds_raw + 2 * OPB;                      // scale staging (only when BLK)
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
 
     // XCD-contiguous bijective remap, then grouped rasterisation (GROUP_M M-tiles per N column)
@@ -184,7 +312,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
     if constexpr (PIPE == 1) {
-        mainloop_8phase(p, acc, lds_raw, m0, n0, lane, wave, wm, wn);
+        mainloop_8phase<BLK>(p, acc, lds_raw, m0, n0, lane, wave, wm, wn);
     } else {
         // per-lane source rows of this wave's glds instructions (rows past M clamp to M-1: loaded, never stored)
         int64_t arow[LA], wrow[LB];
@@ -516,7 +644,12 @@ hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
             if (big && pipe8 && fits && (a.K / BK) % 2 == 0) return launch_cfg<256, 256, 2, 4, EPI, 0, 1>(a, s);
             return big ? launch_cfg<256, 256, 2, 4, EPI, 0>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 0>(a, s);
         }
-        if (blk == 256) return big ? launch_cfg<128, 256, 2, 4, EPI, 256>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 256>(a, s);
+        if (blk == 256) {
+            const int64_t last = (int64_t) ((a.M - 1) / a.a_rpg) * a.a_gstride + (int64_t) ((a.M - 1) % a.a_rpg) * a.a_step;
+            const bool fits = (last + 1) * a.lda < (1ll << 32) && (int64_t) a.N * a.ldw < (1ll << 32);
+            if (big && pipe8 && fits && a.beta && (a.K / BK) % 4 == 0) return launch_cfg<256, 256, 2, 4, EPI, 256, 1>(a, s);
+            return big ? launch_cfg<128, 256, 2, 4, EPI, 256>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 256>(a, s);
+        }
         if (blk == 32) return big ? launch_cfg<128, 256, 2, 4, EPI, 32>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 32>(a, s);
         return hipErrorInvalidValue;
     }

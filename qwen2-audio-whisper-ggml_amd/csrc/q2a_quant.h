@@ -23,7 +23,8 @@ __device__ __forceinline__ void quant_q8k_block(float4 y, int lane, q2a_half * c
         if (a2 > amax || (a2 == amax && i2 < idx)) { amax = a2; mx = m2; idx = i2; }
     }
     int q[4] = {0, 0, 0, 0};
-    float d = 0.f;
+    float d = 1.f;   // all-zero block (ggml stores 0): the codes are 0 so d never contributes; a nonzero d keeps
+                     // the block-ratio rescaling of the wide Q4_K GEMM finite
     if (amax != 0.f) {
         const float iscale = -127.f / mx;
         for (int e = 0; e < 4; ++e) q[e] = min(127, (int) rintf(iscale * vv[e]));

@@ -217,17 +217,21 @@ def test_linear_big_tiles_match_oracle(engines, make_model, wt, which):
     assert mx < 1e-5 and l2 < 1e-6, (mx, l2)
 
 
-def test_encoder_full_size_batched_big_tiles(engines, make_clip, golden):
-    """22 clips in one batch (M = 33 000 rows: the big-tile kernels) — every clip must still match the reference."""
+@pytest.mark.parametrize("wt,tol", [("f16", 1e-3), ("q4_k", 2e-2)])
+def test_encoder_full_size_batched_big_tiles(engines, make_clip, golden, wt, tol):
+    """22 clips in one batch (M = 33 000 rows: the 8-phase 256x256 kernels) — every clip must still match the
+    reference. Q4_K tolerance: activation re-quantization makes faithful implementations differ by ~1.4e-2 at full
+    size (the CPU oracle itself sits 1.34e-2 / 1.38e-2 from ggml, DESIGN.md "Parity")."""
     _, g = golden
-    e = engines("full", "f16")
+    e = engines("full", wt)
     clip = make_clip(0)
     out, st = e.encode_host([clip] * 22)
     for c in (0, 21):
         o = out[c].reshape(-1)
-        val = g["full_f16_c0_val"]
-        mxs, l2s = rel_errors(o[g["full_f16_c0_idx"]], val)
-        assert mxs < 1e-3 and l2s < 1e-3, (c, mxs, l2s)
+        val = g[f"full_{wt}_c0_val"]
+        mxs, l2s = rel_errors(o[g[f"full_{wt}_c0_idx"]], val)
+        assert mxs < tol and l2s < tol, (c, mxs, l2s)
+    assert np.array_equal(out[0], out[21])
 
 
 # ---------------------------------------------------------------- one encoder block at batched (wide-tile) shapes
