@@ -50,7 +50,7 @@ constexpr uint32_t BLOB_VERSION = 2;
 constexpr int MAX_LAYERS = 64;
 constexpr size_t HEADER_BYTES = 32768;
 
-enum { G_CONV1_W, G_CONV1_B, G_CONV2_W, G_CONV2_B, G_PE, G_LNP_W, G_LNP_B, G_FILT, G_TAB, G_GELU, G_COUNT };
+enum { G_CONV1_W, G_CONV1_B, G_CONV2_W, G_CONV2_B, G_PE, G_LNP_W, G_LNP_B, G_FILT, G_TAB, G_GELU, G_GELU_C, G_COUNT };
 // per-matrix arrays: W (fp16 [N][K]); block-major DX, DMIN, BETA = DX_{b-1}/DX_b, GAMMA = DMIN_b/DX_b (f32 [nblk][N]),
 // WEXT (fp16 [nblk][N][16])
 enum { A_W, A_DX, A_DMIN, A_WEXT, A_BETA, A_GAMMA, A_COUNT };
@@ -102,6 +102,7 @@ bool plan(blob_header & h, const q2a_hparams & hp, int wtype) {
     h.goff[G_FILT] = take((uint64_t) d.M * 201 * 4);
     h.goff[G_TAB] = take(1200 * 4);
     h.goff[G_GELU] = take(65536 * 2);
+    h.goff[G_GELU_C] = take(Q2A_GELU_C_BYTES);
     for (int l = 0; l < d.L; ++l) {
         uint64_t * lo = h.loff[l];
         lo[L_BQKV] = take((uint64_t) 3 * d.D * 4);
@@ -271,6 +272,12 @@ int pack(const char * path, std::vector<uint8_t> & out) {
     cpy(h.goff[G_FILT], (const uint8_t *) mf->filters, (size_t) d.M * 201 * 4);
     q2a_make_mel_tables((float *) (blob + h.goff[G_TAB]));
     q2a_make_gelu_table((uint16_t *) (blob + h.goff[G_GELU]));
+    {   // compact |x| <= 10 image of the table for the LDS-resident epilogue lookups: [+0 .. +10] | [-0 .. -10]
+        const uint16_t * t = (const uint16_t *) (blob + h.goff[G_GELU]);
+        uint16_t * c = (uint16_t *) (blob + h.goff[G_GELU_C]);
+        memset(c, 0, Q2A_GELU_C_BYTES);
+        for (int i = 0; i < Q2A_GELU_C_HALF; ++i) { c[i] = t[i]; c[Q2A_GELU_C_HALF + i] = t[0x8000 + i]; }
+    }
 
     struct job { const uint8_t * src; int K, Ntot, r0, r1; const uint64_t * a; int dst0; };
     std::vector<job> jobs;
@@ -507,6 +514,7 @@ q2a_gemm_args gemm_base(const q2a_engine * e, int l, int which, const q2a_half *
     a.W = (const q2a_half *) (e->blob + m[A_W]); a.ldw = K;
     a.M = M; a.N = N; a.K = K;
     a.gelu_tab = e->g<const uint16_t *>(G_GELU);
+    a.gelu_c = e->g<const uint16_t *>(G_GELU_C);
     a.T = e->d.T; a.D = e->d.D; a.H = e->d.H; a.TP = e->TP;
     if (e->blk) {
         a.nblk = K / e->blk;
@@ -636,6 +644,7 @@ int run_frontend(q2a_engine * e, const float * pcm, int64_t stride, int B, int m
         a.bias = e->g<const float *>(G_CONV1_B);
         a.outH = e->y1; a.ldo = d.D; a.o_rpg = d.TM; a.o_gstride = d.TM + 1; a.o_off = 1;
         a.gelu_tab = e->g<const uint16_t *>(G_GELU);
+        a.gelu_c = e->g<const uint16_t *>(G_GELU_C);
         PLAUNCH(e, s, Q2A_PROF_CONV1, q2a_launch_gemm(a, Q2A_EPI_GELU_H, 0, s));
     }
     {   // conv2 (stride 2): A row t = y1 rows 2t..2t+2 (inputs 2t-1..2t+1), K = 3D; + pe
@@ -647,6 +656,7 @@ int run_frontend(q2a_engine * e, const float * pcm, int64_t stride, int B, int m
         a.bias = e->g<const float *>(G_CONV2_B);
         a.outF = e->X; a.ldo = d.D; a.pe = e->g<const float *>(G_PE); a.T = d.T;
         a.gelu_tab = e->g<const uint16_t *>(G_GELU);
+        a.gelu_c = e->g<const uint16_t *>(G_GELU_C);
         PLAUNCH(e, s, Q2A_PROF_CONV2, q2a_launch_gemm(a, Q2A_EPI_CONV2, 0, s));
     }
     return Q2A_OK;

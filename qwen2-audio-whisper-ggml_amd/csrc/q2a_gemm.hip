@@ -46,6 +46,19 @@ __device__ __forceinline__ float gelu_lut(float x, const uint16_t * tab) {
     return (float) gh;
 }
 
+// same lookup against the compact |x| <= 10 table staged in LDS
+__device__ __forceinline__ float gelu_lut_c(float x, const uint16_t * lut) {
+    if (x <= -10.0f) return 0.0f;
+    if (x >= 10.0f) return x;
+    const _Float16 h = (_Float16) x;
+    uint16_t u;
+    __builtin_memcpy(&u, &h, 2);
+    const uint16_t g = lut[(u & 0x7FFF) + ((u & 0x8000) ? Q2A_GELU_C_HALF : 0)];
+    _Float16 gh;
+    __builtin_memcpy(&gh, &g, 2);
+    return (float) gh;
+}
+
 __device__ __forceinline__ int64_t a_row_off(const q2a_gemm_args & p, int m) {
     return ((int64_t) (m / p.a_rpg) * p.a_gstride + (int64_t) (m % p.a_rpg) * p.a_step) * p.lda;
 }
@@ -73,7 +86,7 @@ __device__ __forceinline__ half8 frag(const char * img, int row, int chunk) {
 constexpr int SBUF_OFF = 8 * 128 * ROWB;     // 128 KiB: scale staging after the 8 operand images
 constexpr int SBUF_BYTES = 24 * 1024;       // 21 pieces of 1 KiB (+3 pad slots for the uniform 3 glds per thread)
 
-template <int BLK>
+template <int BLK, bool LUT>
 __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&acc)[8][4], char * lds_raw, int m0, int n0,
                                                 int lane, int wave, int wm, int wn) {
     constexpr int HT = 128 * ROWB;                        // one half-tile image (16 KiB)
@@ -93,12 +106,27 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     const int nk = p.K / BK;
     // image h of buffer b: h = 0 A_q0, 1 A_q1, 2 B_q0, 3 B_q1
     auto stage = [&](int b, int h, int kt) {
-        const int k0 = min(kt, nk - 1) * BK;               // past the end: harmless re-load into a free slot
+        const int k0 = kt * BK;
         char * dst = lds_raw + (b * 4 + h) * HT + wave * 8 * ROWB;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const q2a_half * src = h < 2 ? p.A + aoff[h][i] + k0 : p.W + woff[h - 2][i] + k0;
+            uint32_t o = h < 2 ? aoff[h][i] : woff[h - 2][i];
+            asm volatile("" : "+v"(o));                    // 32-bit offset kept; the 64-bit address is formed here
+            const q2a_half * src = (h < 2 ? p.A : p.W) + o + k0;
             __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (dst + i * 64 * ROWB), 16, 0, 0);
+        }
+    };
+    // the last iteration's stages past the end of K: slots 0..4 receive the compact GELU table for the epilogue
+    // lookups when it needs one, everything else a harmless re-load of the last K-step (keeps the vmcnt counts)
+    auto stage_tail = [&](int b, int h) {
+        if (LUT && b * 4 + h < 5) {
+            char * dst = lds_raw + (b * 4 + h) * HT + wave * 8 * ROWB;
+            const char * src = (const char *) p.gelu_c + (b * 4 + h) * HT + wave * 8 * ROWB + lane * 16;
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+                __builtin_amdgcn_global_load_lds((const void *) (src + i * 64 * ROWB), (lds_ptr_t) (dst + i * 64 * ROWB), 16, 0, 0);
+        } else {
+            stage(b, h, nk - 1);
         }
     };
     // block scales of Q4_K block kb -> LDS pieces: 0 dy_{kb-1} | 1 dy_kb | 2 beta | 3 gamma | 4 dx | 5-12 aext | 13-20 wext
@@ -120,10 +148,12 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     }
     auto stage_scales = [&](int kb) {
         kb = min(kb, p.K / 256 - 1);
+        uint32_t l16 = lane * 16;
+        asm volatile("" : "+v"(l16));                      // per-lane part added at the use: no hoisted 64-bit VGPR pointers
 #pragma unroll
         for (int u = 0; u < 3; ++u) {
             const int k = sb_prev[u] ? max(kb - 1, 0) : kb;
-            const char * src = sb_base[u] + k * sb_stride[u] + lane * 16;
+            const char * src = sb_base[u] + k * sb_stride[u] + l16;
             __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (sbuf + (wave * 3 + u) * 1024), 16, 0, 0);
         }
     };
@@ -240,13 +270,17 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     asm volatile("" ::: "memory");
 
     if constexpr (BLK == 0) {
-        for (int kt = 0; kt < nk; kt += 2) {
+        int kt = 0;
+        for (; kt < nk - 2; kt += 2) {
             Q2A_KSTEP(0, stage(1, 1, kt + 1), stage(0, 0, kt + 2), stage(0, 2, kt + 2), stage(0, 3, kt + 2), 10, 10, 10, 10);
             Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 10, 10, 10, 10);
         }
+        Q2A_KSTEP(0, stage(1, 1, kt + 1), stage_tail(0, 0), stage_tail(0, 2), stage_tail(0, 3), 10, 10, 10, 10);
+        Q2A_KSTEP(1, stage_tail(0, 1), stage_tail(1, 0), stage_tail(1, 2), stage_tail(1, 3), 10, 10, 10, 10);
     } else {
         static_assert(BLK == 256, "8-phase k-quant loop is Q4_K only");
-        for (int kt = 0; kt < nk; kt += 4) {
+        int kt = 0;
+        for (; kt < nk - 4; kt += 4) {
             block_start();
             asm volatile("" ::: "memory");
             Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
@@ -255,6 +289,14 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             Q2A_KSTEP(0, stage(1, 1, kt + 3), stage(0, 0, kt + 4), stage(0, 2, kt + 4), stage(0, 3, kt + 4), 10, 10, 10, 10);
             Q2A_KSTEP(1, stage(0, 1, kt + 4), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5), 10, 10, 10, 10);
         }
+        // last block: its scales stay in place for the final multiply (the scale re-stage keeps the vmcnt counts)
+        block_start();
+        asm volatile("" ::: "memory");
+        Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4)), stage(0, 2, kt + 2),
+                  stage(0, 3, kt + 2), 10, 13, 13, 13);
+        Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 13, 13, 10, 10);
+        Q2A_KSTEP(0, stage(1, 1, kt + 3), stage_tail(0, 0), stage_tail(0, 2), stage_tail(0, 3), 10, 10, 10, 10);
+        Q2A_KSTEP(1, stage_tail(0, 1), stage_tail(1, 0), stage_tail(1, 2), stage_tail(1, 3), 10, 10, 10, 10);
     }
 #undef Q2A_KSTEP
 #undef Q2A_PB
@@ -290,7 +332,14 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
     constexpr int NT = NW * 64;
     constexpr int SCH = (SB / 16 + NT - 1) / NT;          // 16-B scale chunks per thread
     constexpr int OPB = (BM + BN) * ROWB;                 // one operand stage (A image | W image)
-    constexpr int LDS_BYTES = PIPE ? (BLK ? SBUF_OFF + SBUF_BYTES : 2 * OPB) : 2 * OPB + (BLK ? NSB * SB : 0);
+    // GELU epilogues of the 8-phase kernel look the table up in LDS (staged into operand slots 0..4 = [0, 80 KiB)),
+    // so their transpose staging moves behind it
+    constexpr bool LUT_EPI = PIPE && (EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_GELU_F || EPI == Q2A_EPI_CONV2);
+    constexpr int EPI_OFF = LUT_EPI ? Q2A_GELU_C_BYTES : 0;
+    constexpr int EPI_WREG = 2 * 32 * (BN / WN + 8) * 2;
+    constexpr int LDS_MAIN = PIPE ? (BLK ? SBUF_OFF + SBUF_BYTES : 2 * OPB) : 2 * OPB + (BLK ? NSB * SB : 0);
+    constexpr int LDS_BYTES = LDS_MAIN > EPI_OFF + NW * EPI_WREG ? LDS_MAIN : EPI_OFF + NW * EPI_WREG;
+    static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
     __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES];
 #define LDS_STAGE(b_) (lds_raw + (b_) * OPB)
     char * sbuf = lds_raw + 2 * OPB;                      // scale staging (only when BLK)
@@ -312,7 +361,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
     if constexpr (PIPE == 1) {
-        mainloop_8phase<BLK>(p, acc, lds_raw, m0, n0, lane, wave, wm, wn);
+        mainloop_8phase<BLK, LUT_EPI>(p, acc, lds_raw, m0, n0, lane, wave, wm, wn);
     } else {
         // per-lane source rows of this wave's glds instructions (rows past M clamp to M-1: loaded, never stored)
         int64_t arow[LA], wrow[LB];
@@ -524,8 +573,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
     for (int j = 0; j < NJ; ++j) bias_j[j] = (EPI == Q2A_EPI_STORE_F) ? 0.f : p.bias[cbase + j * 16 + (lane & 15)];
     const float vscale = (EPI == Q2A_EPI_QKV && part == 0) ? p.qscale : 1.0f;
     constexpr int WREG = 2 * PR * (WC + 8) * 2;                  // per-wave staging bytes (max of the layouts)
-    static_assert(PR * (WC + 4) * 4 <= WREG && NW * WREG <= 2 * OPB, "epilogue staging exceeds LDS");
-    char * wl = lds_raw + wave * WREG;
+    static_assert(PR * (WC + 4) * 4 <= WREG && WREG == EPI_WREG, "epilogue staging layout");
+    char * wl = lds_raw + EPI_OFF + wave * WREG;
+    const uint16_t * lut = (const uint16_t *) lds_raw;
     __syncthreads();
 #pragma unroll
     for (int ps = 0; ps < WR / PR; ++ps) {
@@ -540,7 +590,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                     const int rl = ii * 16 + (lane >> 4) * 4 + r, cl = j * 16 + (lane & 15);
                     float v = acc[i][j][r];
                     if (EPI != Q2A_EPI_STORE_F) v = v + bias_j[j];
-                    if (EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_GELU_F || EPI == Q2A_EPI_CONV2) v = gelu_lut(v, p.gelu_tab);
+                    if (LUT_EPI) v = gelu_lut_c(v, lut);
+                    else if (EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_GELU_F || EPI == Q2A_EPI_CONV2) v = gelu_lut(v, p.gelu_tab);
                     if (EPI == Q2A_EPI_QKV) v = v * vscale;   // ggml_scale after the bias add (:2054), exact 2^-3
                     if (EPI == Q2A_EPI_QKV && part == 2) {
                         ((_Float16 *) wl)[cl * (PR + 4) + rl] = (_Float16) v;           // V^T image [col][row]

@@ -19,6 +19,12 @@ enum q2a_epi {
                             // (fc1 on the Q4_K path; needs the 256-column tile = one Q8_K block per row)
 };
 
+// compact GELU table: entries for fp16 bits 0x0000..0x4900 (+0..+10) then 0x8000..0xC900 (-0..-10), padded to
+// five 16 KiB glds images
+constexpr int Q2A_GELU_C_HALF = 0x4901;
+constexpr int Q2A_GELU_C_BYTES = 5 * 16384;
+static_assert(2 * Q2A_GELU_C_HALF * 2 <= Q2A_GELU_C_BYTES, "compact GELU table size");
+
 struct q2a_gemm_args {
     // A: fp16 [rows][lda]; logical row m lives at row  (m / a_rpg) * a_gstride + (m % a_rpg) * a_step
     const q2a_half * A;
@@ -40,6 +46,7 @@ struct q2a_gemm_args {
     int D, H, TP;
     float qscale;
     const uint16_t * gelu_tab;        // 65536-entry fp16 table: fp16(gelu_f32(fp16 x)) (ggml.c:3797-3806)
+    const uint16_t * gelu_c;          // compact |x| <= 10 image of it (Q2A_GELU_C_BYTES, staged into LDS by the 8-phase GEMM)
     // blocked (k-quant) accumulation: acc += dy[b][m]*dx[b][n]*S1 - dy[b][m]*dmin[b][n]*S2 per K-block b.
     // All block arrays are block-major so one block's scales for a tile are contiguous (staged through LDS).
     const float * dy;                 // [nblk][dy_ld]
