@@ -396,7 +396,9 @@ struct q2a_engine {
     float * hF = nullptr;
     int TP = 0;
     int dy_ld = 0;
-    bool fuse_q8k = getenv("Q2A_FUSE_Q8K") != nullptr;   // fc1 epilogue quantization (experimental)
+    // fc1 epilogue quantization (Q2A_FUSE_Q8K=1): correct, but at present no faster than the fp16 GELU output
+    // plus the bandwidth-bound quantizer, so off by default
+    int fuse_q8k = [] { const char * v = getenv("Q2A_FUSE_Q8K"); return v ? atoi(v) : -1; }();
 
     // optional per-kernel-class timing with HIP events on the launch stream (q2a_profile_*)
     bool prof = false;
@@ -600,7 +602,8 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         if (mode == 0) {
             a.outH = e->actF; a.ldo = d.F; a.o_rpg = M; a.o_gstride = 0; a.o_off = 0;
             PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_H, 0, s));
-        } else if (mode == 1 && e->fuse_q8k && q2a_gemm_wide_tiles(M, d.F, e->blk)) {
+        } else if (mode == 1 && q2a_gemm_wide_tiles(M, d.F, e->blk) &&
+                   e->fuse_q8k == 1 && q2a_gemm_pipe8(a, e->blk)) {
             // fused fc1 + GELU + Q8_K quantization of the fc2 input (one Q8_K block per 256-column tile)
             a.outH = e->actF; a.ldo = d.F; a.qdy = e->dyF; a.qaext = e->aextF;
             PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_Q8K, e->blk, s));

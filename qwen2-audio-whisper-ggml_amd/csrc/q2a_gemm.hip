@@ -169,6 +169,9 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     // asm with an explicit lgkmcnt wait tied to their results: a compiler-visible LDS read of this array gets a
     // vmcnt(0) guard against the in-flight glds that would drain the whole pipeline once per block.
     auto block_start = [&]() {
+#ifdef Q2A_DIAG_NO_RESCALE
+        return;   // timing diagnostic only (wrong results)
+#endif
         const uint32_t s_dy = sb0 + (wm * 128 + (lane >> 4) * 4) * 4;                       // piece 0 | piece 1 at +1024
         const uint32_t s_ae = sb0 + 5 * 1024 + (wm * 128 + (lane & 15)) * 32 + (lane >> 4) * 8;
         const uint32_t s_cn = sb0 + 2048 + (wn * 64 + (lane & 15)) * 4;                      // beta | gamma at +1024
@@ -334,7 +337,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
     constexpr int OPB = (BM + BN) * ROWB;                 // one operand stage (A image | W image)
     // GELU epilogues of the 8-phase kernel look the table up in LDS (staged into operand slots 0..4 = [0, 80 KiB)),
     // so their transpose staging moves behind it
-    constexpr bool LUT_EPI = PIPE && (EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_GELU_F || EPI == Q2A_EPI_CONV2);
+    constexpr bool LUT_EPI = PIPE && (EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_GELU_F || EPI == Q2A_EPI_CONV2 ||
+                                      EPI == Q2A_EPI_GELU_Q8K);
     constexpr int EPI_OFF = LUT_EPI ? Q2A_GELU_C_BYTES : 0;
     constexpr int EPI_WREG = 2 * 32 * (BN / WN + 8) * 2;
     constexpr int LDS_MAIN = PIPE ? (BLK ? SBUF_OFF + SBUF_BYTES : 2 * OPB) : 2 * OPB + (BLK ? NSB * SB : 0);
@@ -514,7 +518,54 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
         }
     }
 
-    if constexpr (EPI == Q2A_EPI_GELU_Q8K) {
+    if constexpr (EPI == Q2A_EPI_GELU_Q8K && PIPE == 1) {
+        // fc1 + GELU + Q8_K quantization of the produced activation (quantize_row_q8_K_ref, the conversion ggml
+        // applies to the fc2 input): the 256-column tile is exactly one Q8_K block per row. Per pass, the four
+        // waves of one M-half write gelu values (exact fp16) of their 128 rows into LDS behind the GELU table;
+        // then every wave quantizes 16 whole rows (a half4 per lane) and writes codes, d and the bsum operand.
+        constexpr int RSH = 256 + 8;                                  // padded row stride (halves)
+        static_assert(BN == 256 && WN == 4 && WM == 2 && BM == 256, "Q8_K epilogue layout");
+        static_assert(Q2A_GELU_C_BYTES + 128 * RSH * 2 <= LDS_BYTES, "Q8_K staging exceeds LDS");
+        _Float16 * tl = (_Float16 *) (lds_raw + Q2A_GELU_C_BYTES);
+        const uint16_t * lut = (const uint16_t *) lds_raw;
+        const int kb = n0 / 256;
+        float bias_j[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bias_j[j] = p.bias[n0 + wn * 64 + j * 16 + (lane & 15)];
+        __syncthreads();   // the staging overlaps the scale buffer the final multiply just read
+#pragma unroll
+        for (int ps = 0; ps < 2; ++ps) {
+            if (wm == ps) {
+#pragma unroll
+                for (int i = 0; i < MI; ++i)
+#pragma unroll
+                    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            tl[(i * 16 + (lane >> 4) * 4 + r) * RSH + wn * 64 + j * 16 + (lane & 15)] =
+                                (_Float16) gelu_lut_c(acc[i][j][r] + bias_j[j], lut);
+            }
+            __syncthreads();
+            // 16 lanes per row, four rows per wave-iteration, 16 rows per wave per pass
+            const int sub = lane & 15;
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+                const int rl = wave * 16 + it * 4 + (lane >> 4);
+                const int m = m0 + ps * 128 + rl;
+                typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+                const h8_t h0 = *(const h8_t *) (tl + rl * RSH + sub * 16);
+                const h8_t h1 = *(const h8_t *) (tl + rl * RSH + sub * 16 + 8);
+                float v[16];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) { v[e] = (float) h0[e]; v[8 + e] = (float) h1[e]; }
+                if (m < p.M)
+                    quant_q8k_row16(v, sub, p.outH + (int64_t) m * p.ldo + n0 + sub * 16, p.qdy + (int64_t) kb * p.dy_ld + m,
+                                    p.qaext + ((int64_t) kb * p.dy_ld + m) * 16);
+            }
+            __syncthreads();
+        }
+        return;
+    } else if constexpr (EPI == Q2A_EPI_GELU_Q8K) {
         // fc1 + GELU + Q8_K quantization of the produced activation (the conversion ggml applies before fc2,
         // quantize_row_q8_K_ref): the 256-column tile is exactly one Q8_K block per row. Stage 64 rows x 256 f32
         // through LDS per pass, then one wave quantizes one row (a float4 per lane) exactly like k_rownorm.
@@ -679,26 +730,36 @@ bool wide_tiles(int M, int N) {
     return big;
 }
 
+bool pipe8_enabled() {
+    static const bool on = [] { const char * v = getenv("Q2A_GEMM_PIPE"); return v ? atoi(v) != 0 : true; }();
+    return on;
+}
+
+// the 8-phase kernels: 256x256 tiles, 32-bit operand offsets, K-steps in pairs (fp16) or whole Q4_K blocks
+bool pipe8_ok(const q2a_gemm_args & a, int blk) {
+    if (!pipe8_enabled() || !wide_tiles(a.M, a.N)) return false;
+    const int64_t last = (int64_t) ((a.M - 1) / a.a_rpg) * a.a_gstride + (int64_t) ((a.M - 1) % a.a_rpg) * a.a_step;
+    if ((last + 1) * a.lda >= (1ll << 32) || (int64_t) a.N * a.ldw >= (1ll << 32)) return false;
+    if (blk == 0) return (a.K / BK) % 2 == 0;
+    if (blk == 256) return (a.K / BK) % 4 == 0;
+    return false;
+}
+
 template <int EPI>
 hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
     const bool big = wide_tiles(a.M, a.N);
-    static const bool pipe8 = [] { const char * v = getenv("Q2A_GEMM_PIPE"); return v ? atoi(v) != 0 : true; }();
+    const bool p8 = pipe8_ok(a, blk) && (blk != 256 || a.beta);
     if constexpr (EPI == Q2A_EPI_GELU_Q8K) {
         if (!big || blk != 256) return hipErrorInvalidValue;
+        if (p8) return launch_cfg<256, 256, 2, 4, EPI, 256, 1>(a, s);
         return launch_cfg<128, 256, 2, 4, EPI, 256>(a, s);
     } else {
         if (blk == 0) {
-            // 8-phase pipeline needs an even number (>= 2) of 64-deep K-steps
-            // (it addresses operands with 32-bit element offsets)
-            const int64_t last = (int64_t) ((a.M - 1) / a.a_rpg) * a.a_gstride + (int64_t) ((a.M - 1) % a.a_rpg) * a.a_step;
-            const bool fits = (last + 1) * a.lda < (1ll << 32) && (int64_t) a.N * a.ldw < (1ll << 32);
-            if (big && pipe8 && fits && (a.K / BK) % 2 == 0) return launch_cfg<256, 256, 2, 4, EPI, 0, 1>(a, s);
+            if (p8) return launch_cfg<256, 256, 2, 4, EPI, 0, 1>(a, s);
             return big ? launch_cfg<256, 256, 2, 4, EPI, 0>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 0>(a, s);
         }
         if (blk == 256) {
-            const int64_t last = (int64_t) ((a.M - 1) / a.a_rpg) * a.a_gstride + (int64_t) ((a.M - 1) % a.a_rpg) * a.a_step;
-            const bool fits = (last + 1) * a.lda < (1ll << 32) && (int64_t) a.N * a.ldw < (1ll << 32);
-            if (big && pipe8 && fits && a.beta && (a.K / BK) % 4 == 0) return launch_cfg<256, 256, 2, 4, EPI, 256, 1>(a, s);
+            if (p8) return launch_cfg<256, 256, 2, 4, EPI, 256, 1>(a, s);
             return big ? launch_cfg<128, 256, 2, 4, EPI, 256>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 256>(a, s);
         }
         if (blk == 32) return big ? launch_cfg<128, 256, 2, 4, EPI, 32>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 32>(a, s);
@@ -724,3 +785,5 @@ hipError_t q2a_launch_gemm(const q2a_gemm_args & a, int epi, int blk, hipStream_
 }
 
 bool q2a_gemm_wide_tiles(int M, int N, int blk) { (void) blk; return wide_tiles(M, N); }
+
+bool q2a_gemm_pipe8(const q2a_gemm_args & a, int blk) { return pipe8_ok(a, blk) && (blk != 256 || a.beta); }

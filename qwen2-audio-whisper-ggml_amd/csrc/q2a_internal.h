@@ -66,6 +66,9 @@ struct q2a_gemm_args {
 hipError_t q2a_launch_gemm(const q2a_gemm_args & a, int epi, int blk, hipStream_t s);
 // true when the launcher will use the 256-column tile configuration for this shape (Q2A_EPI_GELU_Q8K needs it)
 bool q2a_gemm_wide_tiles(int M, int N, int blk);
+// true when the launcher will use the 8-phase 256x256 kernel for these arguments (its Q4_K flavour fuses
+// Q2A_EPI_GELU_Q8K efficiently)
+bool q2a_gemm_pipe8(const q2a_gemm_args & a, int blk);
 
 struct q2a_attn_args {
     const q2a_half *qh, *ql, *kh, *kl, *vt;

@@ -47,6 +47,60 @@ __device__ __forceinline__ void quant_q8k_block(float4 y, int lane, q2a_half * c
     }
 }
 
+// quantize one 256-block held by 16 lanes (16 consecutive values per lane; lane group = lane >> 4 = one row):
+// same arithmetic as quant_q8k_block, four rows per wave at once. Cross-lane steps stay inside the 16-lane group
+// (ds_swizzle xor patterns). codes: this lane's 16 codes; aext: the row's 16-half bsum operand.
+__device__ __forceinline__ int swz_xor_i(int v, int o) {
+    switch (o) {
+        case 1: return __builtin_amdgcn_ds_swizzle(v, 0x041F);
+        case 2: return __builtin_amdgcn_ds_swizzle(v, 0x081F);
+        case 4: return __builtin_amdgcn_ds_swizzle(v, 0x101F);
+        default: return __builtin_amdgcn_ds_swizzle(v, 0x201F);
+    }
+}
+__device__ __forceinline__ float swz_xor_f(float v, int o) { return __int_as_float(swz_xor_i(__float_as_int(v), o)); }
+
+__device__ __forceinline__ void quant_q8k_row16(const float (&v)[16], int sub, q2a_half * codes, float * dy_out,
+                                                q2a_half * aext) {
+    float amax = fabsf(v[0]), mx = v[0];
+    int idx = sub * 16;
+#pragma unroll
+    for (int e = 1; e < 16; ++e)
+        if (fabsf(v[e]) > amax) { amax = fabsf(v[e]); mx = v[e]; idx = sub * 16 + e; }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+        const float a2 = swz_xor_f(amax, o), m2 = swz_xor_f(mx, o);
+        const int i2 = swz_xor_i(idx, o);
+        if (a2 > amax || (a2 == amax && i2 < idx)) { amax = a2; mx = m2; idx = i2; }
+    }
+    int q[16];
+    float d = 1.f;   // all-zero block: see quant_q8k_block
+    if (amax != 0.f) {
+        const float iscale = -127.f / mx;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) q[e] = min(127, (int) rintf(iscale * v[e]));
+        d = 1 / iscale;
+    } else {
+#pragma unroll
+        for (int e = 0; e < 16; ++e) q[e] = 0;
+    }
+    typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+    h8_t c0, c1;
+    int s = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { c0[e] = (_Float16) (float) q[e]; c1[e] = (_Float16) (float) q[8 + e]; s += q[e] + q[8 + e]; }
+    *(h8_t *) codes = c0;
+    *(h8_t *) (codes + 8) = c1;
+    if (sub == 0) *dy_out = d;
+    s += swz_xor_i(s, 1);                                     // bsum32 of sub-block j = sub / 2
+    if ((sub & 1) == 0) {
+        const int hi = (s >= 0) ? (s >> 6) : -((-s + 63) >> 6);   // floor(s / 64)
+        const int lo = s - 64 * hi;
+        typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+        *(h2_t *) (aext + sub) = h2_t{(_Float16) (float) hi, (_Float16) (float) lo};
+    }
+}
+
 // quantize one 32-block (8 lanes x float4) to Q8_0 codes with the x86 AVX2 semantics
 __device__ __forceinline__ void quant_q80_block(float4 y, int lane, q2a_half * codes, float * dy_out) {
     float amax = fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w)));

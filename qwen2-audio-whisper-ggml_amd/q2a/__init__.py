@@ -11,7 +11,7 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libq2a.so")
+LIB_PATH = os.environ.get("Q2A_LIB_PATH") or os.path.join(PKG_DIR, "lib", "libq2a.so")   # override: A/B builds
 HOST_LIB_PATH = os.path.join(PKG_DIR, "lib", "libq2a_host.so")
 TOOL_PATH = os.path.join(PKG_DIR, "bin", "q2a_tool")
 
