@@ -82,6 +82,15 @@ int q2a_encode_device(q2a_engine * e, const float * pcm_dev, int64_t pcm_stride,
 int q2a_encode_host(q2a_engine * e, const float * const * pcm, const int32_t * n_samples, int n_clips,
                     int offset_ms, float * out_host, int32_t * status);
 
+/* Per-clip window offsets (milliseconds, host array [n_clips]) instead of one offset_ms: e.g. the consecutive 30 s
+ * windows of a long recording passed as n_clips rows that all point at the same PCM (pcm_stride 0 on the device
+ * variant). Each window's log-mel is normalised over the whole recording, exactly as whisper_full(offset_ms = k *
+ * 30000) on that recording would (the reference itself only ever encodes the first window). */
+int q2a_encode_device_ex(q2a_engine * e, const float * pcm_dev, int64_t pcm_stride, const int32_t * n_samples,
+                         const int32_t * offsets_ms, int n_clips, float * out_dev, int32_t * status, void * stream);
+int q2a_encode_host_ex(q2a_engine * e, const float * const * pcm, const int32_t * n_samples, const int32_t * offsets_ms,
+                       int n_clips, int offset_ms, float * out_host, int32_t * status);
+
 /* log-mel of one clip (whisper_pcm_to_mel semantics): writes [n_mels][n_len] into mel_out (capacity
  * mel_cap floats) and *n_len. Runs the same kernels as the encoder on the engine's device. */
 int q2a_pcm_to_mel(q2a_engine * e, const float * pcm, int n_samples, float * mel_out, int64_t mel_cap, int * n_len);

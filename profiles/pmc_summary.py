@@ -1,0 +1,77 @@
+#!/usr/bin/env python3
+"""Summarise two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) of one bench.py run into per-kernel HBM bytes.
+
+    python profiles/pmc_summary.py FETCH_counter_collection.csv WRITE_counter_collection.csv OUT.json "source text"
+
+FETCH_SIZE / WRITE_SIZE are KiB per dispatch (TCC, summed over channels). gfx950 correction (MI355X_MICROARCH.md,
+HBM section): FETCH_SIZE x2, because 16-B-per-lane streaming reads are counted at half size. Kernel classes are
+mapped to the engine's launch sites by template signature (k_gemm<BM, BN, WM, WN, EPI, BLK, PIPE>).
+"""
+import csv
+import json
+import re
+import sys
+from collections import defaultdict
+
+EPI = {0: "qkv", 1: "resid", 2: "gelu_h", 3: "conv2", 4: "gelu_f", 5: "store_f", 6: "gelu_q8k"}
+
+
+def classify(name: str) -> str:
+    if "k_attn" in name:
+        return "attention"
+    m = re.search(r"k_gemm<(\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (\d+)>", name)
+    if not m:
+        return name.split("(")[0].strip()[:60]
+    epi, blk = int(m.group(5)), int(m.group(6))
+    if epi == 0:
+        return "gemm_qkv"
+    if epi == 1:
+        return "gemm_o+gemm_fc2"
+    if epi == 3:
+        return "conv2"
+    if epi == 2 and blk == 0:
+        return "gelu_h_fp16 (conv1, and fc1 on F16 models)"
+    if epi in (2, 4, 6):
+        return "gemm_fc1"
+    return EPI.get(epi, str(epi))
+
+
+def load(path, counter):
+    per = defaultdict(list)
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row.get("Counter_Name") != counter:
+                continue
+            per[row["Kernel_Name"]].append(float(row["Counter_Value"]))
+    return per
+
+
+def main():
+    fetch_csv, write_csv, out, source = sys.argv[1:5]
+    fetch, write = load(fetch_csv, "FETCH_SIZE"), load(write_csv, "WRITE_SIZE")
+    res = {}
+    for k in sorted(set(fetch) | set(write)):
+        cls = classify(k)
+        f = fetch.get(k, [])
+        w = write.get(k, [])
+        e = {"kernel": k, "dispatches": max(len(f), len(w))}
+        if f:
+            e["FETCH_SIZE_KiB_avg"] = sum(f) / len(f)
+        if w:
+            e["WRITE_SIZE_KiB_avg"] = sum(w) / len(w)
+        if f and w:
+            e["hbm_bytes_per_launch_corrected"] = (2 * e["FETCH_SIZE_KiB_avg"] + e["WRITE_SIZE_KiB_avg"]) * 1024
+        key = cls
+        while key in res:
+            key += "'"
+        res[key] = e
+    with open(out, "w") as fo:
+        json.dump({"source": source,
+                   "units": "FETCH_SIZE/WRITE_SIZE in KiB per dispatch; gfx950 correction: FETCH_SIZE x2 (16-B/lane "
+                            "streaming reads count half, MI355X_MICROARCH.md HBM section); Infinity-Cache hits are "
+                            "included in these counters",
+                   "kernels": res}, fo, indent=1)
+
+
+if __name__ == "__main__":
+    main()

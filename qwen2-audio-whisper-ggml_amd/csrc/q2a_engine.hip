@@ -666,13 +666,14 @@ int run_frontend(q2a_engine * e, const float * pcm, int64_t stride, int B, int m
 }
 
 // per-clip metadata (host): whisper_encoder_output_with_state's seek / too-short logic (:2356-2365)
-int prepare_meta(q2a_engine * e, const int32_t * n_samples, int B, int offset_ms, int32_t * status, int & max_frames,
+int prepare_meta(q2a_engine * e, const int32_t * n_samples, int B, int offset_ms, const int32_t * offs, int32_t * status, int & max_frames,
                  int64_t max_valid, hipStream_t s) {
     int32_t * mh = e->meta_host;
     HIP_TRY(hipEventSynchronize(e->meta_evt));   // the previous call's upload out of mh may still be queued
     max_frames = 0;
-    const int seek = offset_ms / 10;
     for (int c = 0; c < B; ++c) {
+        const int seek = (offs ? offs[c] : offset_ms) / 10;
+        if (seek < 0) { set_err("clip %d: negative offset", c); return Q2A_ERR_ARG; }
         const int n = n_samples[c];
         if (n < 0 || (max_valid >= 0 && n > max_valid)) { set_err("clip %d: bad n_samples %d", c, n); return Q2A_ERR_ARG; }
         const int n_len_org = 1 + (n + 200 - 400) / 160;   // mel.n_len_org (:2613), C truncation
@@ -689,14 +690,14 @@ int prepare_meta(q2a_engine * e, const int32_t * n_samples, int B, int offset_ms
 }
 
 int encode_impl(q2a_engine * e, const float * pcm, int64_t stride, const int32_t * n_samples, int B, int offset_ms,
-                float * out, int32_t * status, hipStream_t s) {
+                const int32_t * offs, float * out, int32_t * status, hipStream_t s) {
     if (B <= 0 || !pcm || !n_samples || !out) { set_err("invalid arguments"); return Q2A_ERR_ARG; }
     if (offset_ms < 0) { set_err("offset_ms must be >= 0"); return Q2A_ERR_ARG; }
     HIP_TRY(hipSetDevice(e->device));
     int rc = reserve(e, B);
     if (rc) return rc;
     int max_frames = 0;
-    rc = prepare_meta(e, n_samples, B, offset_ms, status, max_frames, stride, s);
+    rc = prepare_meta(e, n_samples, B, offset_ms, offs, status, max_frames, stride > 0 ? stride : -1, s);   // stride 0: shared PCM
     if (rc) return rc;
     rc = run_frontend(e, pcm, stride, B, max_frames, s);
     if (rc) return rc;
@@ -804,11 +805,23 @@ int q2a_encode_device(q2a_engine * e, const float * pcm_dev, int64_t pcm_stride,
                       int n_clips, int offset_ms, float * out_dev, int32_t * status, void * stream) {
     if (!e) return Q2A_ERR_ARG;
     hipStream_t s = stream ? (hipStream_t) stream : e->stream;
-    return encode_impl(e, pcm_dev, pcm_stride, n_samples, n_clips, offset_ms, out_dev, status, s);
+    return encode_impl(e, pcm_dev, pcm_stride, n_samples, n_clips, offset_ms, nullptr, out_dev, status, s);
+}
+
+int q2a_encode_device_ex(q2a_engine * e, const float * pcm_dev, int64_t pcm_stride, const int32_t * n_samples,
+                         const int32_t * offsets_ms, int n_clips, float * out_dev, int32_t * status, void * stream) {
+    if (!e || !offsets_ms) { set_err("invalid arguments"); return Q2A_ERR_ARG; }
+    hipStream_t s = stream ? (hipStream_t) stream : e->stream;
+    return encode_impl(e, pcm_dev, pcm_stride, n_samples, n_clips, 0, offsets_ms, out_dev, status, s);
 }
 
 int q2a_encode_host(q2a_engine * e, const float * const * pcm, const int32_t * n_samples, int n_clips, int offset_ms,
                     float * out_host, int32_t * status) {
+    return q2a_encode_host_ex(e, pcm, n_samples, nullptr, n_clips, offset_ms, out_host, status);
+}
+
+int q2a_encode_host_ex(q2a_engine * e, const float * const * pcm, const int32_t * n_samples, const int32_t * offsets_ms,
+                       int n_clips, int offset_ms, float * out_host, int32_t * status) {
     if (!e || !pcm || !n_samples || !out_host || n_clips <= 0) { set_err("invalid arguments"); return Q2A_ERR_ARG; }
     HIP_TRY(hipSetDevice(e->device));
     int64_t maxn = 1;
@@ -825,7 +838,7 @@ int q2a_encode_host(q2a_engine * e, const float * const * pcm, const int32_t * n
             rc = Q2A_ERR_HIP;
     // outputs of skipped clips are left untouched: seed the device buffer with the caller's current contents
     if (rc == Q2A_OK && hipMemcpyAsync(dout, out_host, out_bytes, hipMemcpyHostToDevice, e->stream) != hipSuccess) rc = Q2A_ERR_HIP;
-    if (rc == Q2A_OK) rc = encode_impl(e, dpcm, maxn, n_samples, n_clips, offset_ms, dout, status, e->stream);
+    if (rc == Q2A_OK) rc = encode_impl(e, dpcm, maxn, n_samples, n_clips, offset_ms, offsets_ms, dout, status, e->stream);
     if (rc == Q2A_OK && hipMemcpyAsync(out_host, dout, out_bytes, hipMemcpyDeviceToHost, e->stream) != hipSuccess) rc = Q2A_ERR_HIP;
     if (hipStreamSynchronize(e->stream) != hipSuccess && rc == Q2A_OK) { set_err("stream error"); rc = Q2A_ERR_HIP; }
     (void) hipFree(dpcm);
