@@ -61,6 +61,13 @@ int64_t q2a_pack_model(const char * model_path, void ** host_blob);   /* returns
 void q2a_free_host_blob(void * host_blob);
 q2a_engine * q2a_open_device_blob(const void * device_blob, int64_t size, int device);  /* blob not owned */
 
+/* A second engine on the same device sharing `base`'s weights (its own workspace and stream): the analogue of a
+ * second whisper_state on one whisper_context. `base` must outlive it. */
+q2a_engine * q2a_open_shared(const q2a_engine * base);
+/* Encode windows with under 1 s of audio after the offset too (default off: they are skipped, Q2A_CLIP_SKIPPED,
+ * like the reference). whisper_full uses it when duration_ms overrides the length check (qwen2-whisper.cpp:2357). */
+int q2a_set_force_encode(q2a_engine * e, int on);
+
 void q2a_close(q2a_engine * e);
 int q2a_get_info(const q2a_engine * e, q2a_info * info);
 

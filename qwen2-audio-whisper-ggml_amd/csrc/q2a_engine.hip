@@ -396,6 +396,7 @@ struct q2a_engine {
     float * hF = nullptr;
     int TP = 0;
     int dy_ld = 0;
+    bool force_encode = false;   // encode windows with under 1 s of audio too (whisper_full with duration_ms set)
     // fc1 epilogue quantization (Q2A_FUSE_Q8K=1): correct, but at present no faster than the fp16 GELU output
     // plus the bandwidth-bound quantizer, so off by default
     int fuse_q8k = [] { const char * v = getenv("Q2A_FUSE_Q8K"); return v ? atoi(v) : -1; }();
@@ -677,7 +678,7 @@ int prepare_meta(q2a_engine * e, const int32_t * n_samples, int B, int offset_ms
         const int n = n_samples[c];
         if (n < 0 || (max_valid >= 0 && n > max_valid)) { set_err("clip %d: bad n_samples %d", c, n); return Q2A_ERR_ARG; }
         const int n_len_org = 1 + (n + 200 - 400) / 160;   // mel.n_len_org (:2613), C truncation
-        const bool ok = n > 200 && !(n_len_org < seek + 100);
+        const bool ok = n > 200 && (e->force_encode || !(n_len_org < seek + 100));
         mh[c] = ok ? n : 0;
         mh[B + c] = seek;
         mh[2 * B + c] = ok ? 1 : 0;
@@ -772,6 +773,17 @@ q2a_engine * q2a_open_device_blob(const void * dev_blob, int64_t size, int devic
     e->own_blob = false;
     e->blob_size = size;
     return e;
+}
+
+q2a_engine * q2a_open_shared(const q2a_engine * base) {
+    if (!base) { set_err("invalid arguments"); return nullptr; }
+    return q2a_open_device_blob(base->blob, base->blob_size, base->device);
+}
+
+int q2a_set_force_encode(q2a_engine * e, int on) {
+    if (!e) return Q2A_ERR_ARG;
+    e->force_encode = on != 0;
+    return Q2A_OK;
 }
 
 void q2a_close(q2a_engine * e) {

@@ -162,7 +162,6 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     // otherwise guard each read of the scale buffer with a vmcnt(0) that drains the whole pipeline
     typedef const __attribute__((address_space(3))) float * lds_fp;
     typedef const __attribute__((address_space(3))) f4 * lds_f4p;
-    typedef const __attribute__((address_space(3))) half4 * lds_h4p;
     const uint32_t lds0 = (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) char *) lds_raw;
     const uint32_t sb0 = lds0 + SBUF_OFF;
     // start of block kb: acc <- acc * alpha[m] * beta[n] - gamma[n] * S2[m][n]. The scale-buffer reads are inline
