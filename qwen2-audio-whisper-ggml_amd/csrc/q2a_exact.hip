@@ -2,6 +2,7 @@
 // -ffp-contract=off): log-mel frontend, LayerNorm (+ activation quantizers), AvgPool + final LayerNorm.
 // All are HBM/latency-bound; they are fused so that each tensor is read once and written once.
 #include "q2a_internal.h"
+#include <cstdlib>
 #include "q2a_quant.h"
 
 #include <math.h>
@@ -167,7 +168,7 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 
-template <int MODE, bool LN, bool HIN = false>
+template <int MODE, bool LN, bool HIN = false, int NBQ = 0>
 __global__ __launch_bounds__(256) void k_rownorm(const float * __restrict__ X, int M, int D, const float * __restrict__ g,
                                                  const float * __restrict__ b, q2a_half * outH, float * dy, q2a_half * aext,
                                                  int nseg, int ld) {
@@ -222,6 +223,22 @@ __global__ __launch_bounds__(256) void k_rownorm(const float * __restrict__ X, i
             if (c < nch) v[u] = x4[c];
         }
     }
+    if constexpr (MODE == 1 && LN && NBQ > 0) {
+        // whole row resident: the NBQ Q8_K blocks of the row quantized with interleaved reductions
+        float4 y[NBQ];
+#pragma unroll
+        for (int u = 0; u < NBQ; ++u) {
+            const int c = lane + 64 * u;
+            const float4 gg = ((const float4 *) g)[c], bb = ((const float4 *) b)[c];
+            y[u].x = (v[u].x * scale) * gg.x + bb.x;
+            y[u].y = (v[u].y * scale) * gg.y + bb.y;
+            y[u].z = (v[u].z * scale) * gg.z + bb.z;
+            y[u].w = (v[u].w * scale) * gg.w + bb.w;
+        }
+        quant_q8k_blocks<NBQ>(y, lane, outH + (int64_t) row * D + 4 * lane, 256, dy + row, ld, aext + (int64_t) row * 16,
+                              (int64_t) ld * 16);
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < MAXC; ++u) {
         const int c = lane + 64 * u;
@@ -246,6 +263,24 @@ __global__ __launch_bounds__(256) void k_rownorm(const float * __restrict__ X, i
             quant_q80_block(y, lane, o, dy + (int64_t) bf * ld + m);
         }
     }
+}
+
+// Q8_K quantizer for fp16 rows (the fc1 GELU output), 16 lanes per 256-block: a wave quantizes four blocks at
+// once with 16-B loads and stores (quant_q8k_row16: the arithmetic of quant_q8k_block, shorter reduction chains)
+__global__ __launch_bounds__(256) void k_quant_q8k_h16(const q2a_half * __restrict__ X, int64_t nblocks, int bpr,
+                                                       q2a_half * outH, float * dy, q2a_half * aext, int ld) {
+    const int lane = threadIdx.x & 63, sub = lane & 15;
+    const int64_t blk = ((int64_t) blockIdx.x * 4 + (threadIdx.x >> 6)) * 4 + (lane >> 4);
+    if (blk >= nblocks) return;
+    const int64_t m = blk / bpr;
+    const int bf = (int) (blk - m * bpr);
+    typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+    const h8_t * src = (const h8_t *) (X + blk * 256 + sub * 16);
+    const h8_t h0 = __builtin_nontemporal_load(src), h1 = __builtin_nontemporal_load(src + 1);
+    float v[16];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { v[e] = (float) h0[e]; v[8 + e] = (float) h1[e]; }
+    quant_q8k_row16(v, sub, outH + blk * 256 + sub * 16, dy + (int64_t) bf * ld + m, aext + ((int64_t) bf * ld + m) * 16);
 }
 
 // AvgPool1d(k=2,s=2) over time (ggml.c:15077-15125: drow = 0; += a; += b; /= 2) + final LayerNorm -> f32
@@ -317,6 +352,8 @@ hipError_t q2a_launch_layernorm(const q2a_ln_args & a, hipStream_t s) {
     if (a.mode == 2 && a.D % 32) return hipErrorInvalidValue;
     const dim3 grid((a.M + 3) / 4), blk(256);
     if (a.mode == 0) hipLaunchKernelGGL((k_rownorm<0, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
+    else if (a.mode == 1 && a.D == 1280 && !getenv("Q2A_QUANT_V1"))
+        hipLaunchKernelGGL((k_rownorm<1, true, false, 5>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else if (a.mode == 1) hipLaunchKernelGGL((k_rownorm<1, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else hipLaunchKernelGGL((k_rownorm<2, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     return hipGetLastError();
@@ -330,7 +367,11 @@ hipError_t q2a_launch_quant_act(const q2a_quant_args & a, hipStream_t s) {
     const dim3 grid((a.M * nseg + 3) / 4), blk(256);
     // view X as [M*nseg][seg]: contiguous, and the block structure (256 / 32) never straddles a segment
     const float * X = a.XH ? (const float *) a.XH : a.X;
-    if (a.mode == 1 && a.XH) {
+    if (a.mode == 1 && a.XH && !getenv("Q2A_QUANT_V1")) {
+        const int64_t nb = (int64_t) a.M * (a.K / 256);
+        hipLaunchKernelGGL(k_quant_q8k_h16, dim3((unsigned) ((nb + 15) / 16)), dim3(256), 0, s, a.XH, nb, a.K / 256, a.outH,
+                           a.dy, a.aext, a.dy_ld);
+    } else if (a.mode == 1 && a.XH) {
         hipLaunchKernelGGL((k_rownorm<1, false, true>), grid, blk, 0, s, X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext, nseg, a.dy_ld);
     } else if (a.mode == 2 && a.XH) {
         hipLaunchKernelGGL((k_rownorm<2, false, true>), grid, blk, 0, s, X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext, nseg, a.dy_ld);

@@ -84,7 +84,8 @@ __device__ __forceinline__ half8 frag(const char * img, int row, int chunk) {
 // the following five phases raised by those 3 instructions. Zero scales never occur (quantizers store d = 1 for
 // an all-zero activation block, the pack stores dx = 1 and zero weights for a d = 0 weight block).
 constexpr int SBUF_OFF = 8 * 128 * ROWB;     // 128 KiB: scale staging after the 8 operand images
-constexpr int SBUF_BYTES = 24 * 1024;       // 21 pieces of 1 KiB (+3 pad slots for the uniform 3 glds per thread)
+constexpr int SBUF_BYTES = 25 * 1024;       // 21 pieces of 1 KiB (+3 pad slots for the uniform 3 glds per thread)
+constexpr int ALPHA_OFF = 24 * 1024;        //   + alpha = dy_{b-1}/dy_b per tile row (1 KiB), computed a block ahead
 
 template <int BLK, bool LUT>
 __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&acc)[8][4], char * lds_raw, int m0, int n0,
@@ -121,7 +122,9 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     auto stage_tail = [&](int b, int h) {
         if (LUT && b * 4 + h < 5) {
             char * dst = lds_raw + (b * 4 + h) * HT + wave * 8 * ROWB;
-            const char * src = (const char *) p.gelu_c + (b * 4 + h) * HT + wave * 8 * ROWB + lane * 16;
+            uint32_t l16 = lane * 16;
+            asm volatile("" : "+v"(l16));
+            const char * src = (const char *) p.gelu_c + (b * 4 + h) * HT + wave * 8 * ROWB + l16;
 #pragma unroll
             for (int i = 0; i < 2; ++i)
                 __builtin_amdgcn_global_load_lds((const void *) (src + i * 64 * ROWB), (lds_ptr_t) (dst + i * 64 * ROWB), 16, 0, 0);
@@ -167,40 +170,53 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     // start of block kb: acc <- acc * alpha[m] * beta[n] - gamma[n] * S2[m][n]. The scale-buffer reads are inline
     // asm with an explicit lgkmcnt wait tied to their results: a compiler-visible LDS read of this array gets a
     // vmcnt(0) guard against the in-flight glds that would drain the whole pipeline once per block.
+    // alpha for this wave's 32 rows of the tile into the alpha array (the block's scales must be resident)
+    auto alpha_compute = [&]() {
+        const uint32_t row = (uint32_t) (wave * 32 + (lane & 31));
+        float yp, yc;
+        asm volatile("ds_read_b32 %0, %1" : "=v"(yp) : "v"(sb0 + row * 4));
+        asm volatile("ds_read_b32 %0, %1 offset:1024" : "=v"(yc) : "v"(sb0 + row * 4));
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(yp), "+v"(yc));
+        const float al = yp * __builtin_amdgcn_rcpf(yc);
+        asm volatile("ds_write_b32 %0, %1" :: "v"(sb0 + ALPHA_OFF + row * 4), "v"(al) : "memory");
+    };
     auto block_start = [&]() {
 #ifdef Q2A_DIAG_NO_RESCALE
         return;   // timing diagnostic only (wrong results)
 #endif
-        const uint32_t s_dy = sb0 + (wm * 128 + (lane >> 4) * 4) * 4;                       // piece 0 | piece 1 at +1024
+        const uint32_t s_al = sb0 + ALPHA_OFF + (wm * 128 + (lane >> 4) * 4) * 4;
         const uint32_t s_ae = sb0 + 5 * 1024 + (wm * 128 + (lane & 15)) * 32 + (lane >> 4) * 8;
         const uint32_t s_cn = sb0 + 2048 + (wn * 64 + (lane & 15)) * 4;                      // beta | gamma at +1024
         const uint32_t s_we = sb0 + 13 * 1024 + (wn * 64 + (lane & 15)) * 32 + (lane >> 4) * 8;
         float bet[4], gam[4];
         half4 we[4];
+        f4 al[2];
+        half4 ae[2];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(bet[j]) : "v"(s_cn), "i"(j * 64));
             asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(gam[j]) : "v"(s_cn), "i"(1024 + j * 64));
             asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(we[j]) : "v"(s_we), "i"(j * 512));
         }
+        asm volatile("ds_read_b128 %0, %1" : "=v"(al[0]) : "v"(s_al));
+        asm volatile("ds_read_b64 %0, %1" : "=v"(ae[0]) : "v"(s_ae));
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bet[0]), "+v"(bet[1]), "+v"(bet[2]), "+v"(bet[3]), "+v"(gam[0]),
-                     "+v"(gam[1]), "+v"(gam[2]), "+v"(gam[3]), "+v"(we[0]), "+v"(we[1]), "+v"(we[2]), "+v"(we[3]));
+                     "+v"(gam[1]), "+v"(gam[2]), "+v"(gam[3]), "+v"(we[0]), "+v"(we[1]), "+v"(we[2]), "+v"(we[3]),
+                     "+v"(al[0]), "+v"(ae[0]));
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            f4 yp, yc;
-            half4 ae;
-            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(yp) : "v"(s_dy), "i"(i * 64));
-            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(yc) : "v"(s_dy), "i"(1024 + i * 64));
-            asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(ae) : "v"(s_ae), "i"(i * 512));
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(yp), "+v"(yc), "+v"(ae));
-            const float al[4] = {yp[0] * __builtin_amdgcn_rcpf(yc[0]), yp[1] * __builtin_amdgcn_rcpf(yc[1]),
-                                 yp[2] * __builtin_amdgcn_rcpf(yc[2]), yp[3] * __builtin_amdgcn_rcpf(yc[3])};
+            const int c = i & 1, n = c ^ 1;
+            if (i + 1 < 8) {   // next row block's data in flight while this one is processed
+                asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(al[n]) : "v"(s_al), "i"((i + 1) * 64));
+                asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(ae[n]) : "v"(s_ae), "i"((i + 1) * 512));
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const f4 s2 = __builtin_amdgcn_mfma_f32_16x16x16f16(ae, we[j], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                const f4 s2 = __builtin_amdgcn_mfma_f32_16x16x16f16(ae[c], we[j], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] * (al[r] * bet[j]) - gam[j] * s2[r];
+                for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] * (al[c][r] * bet[j]) - gam[j] * s2[r];
             }
+            if (i + 1 < 8) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(al[n]), "+v"(ae[n]));
             __builtin_amdgcn_sched_barrier(0);   // one row block at a time: bounds the live min-term results
         }
     };
@@ -281,6 +297,10 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
         Q2A_KSTEP(1, stage_tail(0, 1), stage_tail(1, 0), stage_tail(1, 2), stage_tail(1, 3), 10, 10, 10, 10);
     } else {
         static_assert(BLK == 256, "8-phase k-quant loop is Q4_K only");
+        alpha_compute();                                     // block 0 (alpha = 1: acc is 0 anyway)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // raw barrier: __syncthreads would drain the prologue glds
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
         int kt = 0;
         for (; kt < nk - 4; kt += 4) {
             block_start();
@@ -288,7 +308,9 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
                       stage(0, 3, kt + 2), 10, 13, 13, 13);
             Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 13, 13, 10, 10);
-            Q2A_KSTEP(0, stage(1, 1, kt + 3), stage(0, 0, kt + 4), stage(0, 2, kt + 4), stage(0, 3, kt + 4), 10, 10, 10, 10);
+            // phase 9: the next block's alpha (its scales, staged in phase 2, landed by phase 7)
+            Q2A_KSTEP(0, (alpha_compute(), stage(1, 1, kt + 3)), stage(0, 0, kt + 4), stage(0, 2, kt + 4), stage(0, 3, kt + 4),
+                      10, 10, 10, 10);
             Q2A_KSTEP(1, stage(0, 1, kt + 4), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5), 10, 10, 10, 10);
         }
         // last block: its scales stay in place for the final multiply (the scale re-stage keeps the vmcnt counts)

@@ -101,6 +101,64 @@ __device__ __forceinline__ void quant_q8k_row16(const float (&v)[16], int sub, q
     }
 }
 
+// NB independent 256-blocks, one float4 per lane each (block u = lanes 0..63 x 4 of y[u]): quant_q8k_block's
+// arithmetic with the NB reduction chains interleaved (the LayerNorm kernel's row is NB = D/256 blocks)
+template <int NB>
+__device__ __forceinline__ void quant_q8k_blocks(const float4 (&y)[NB], int lane, q2a_half * codes, int64_t code_stride,
+                                                 float * dy_out, int64_t dy_stride, q2a_half * aext, int64_t aext_stride) {
+    float amax[NB], mx[NB];
+    int idx[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+        const float vv[4] = {y[u].x, y[u].y, y[u].z, y[u].w};
+        amax[u] = fabsf(vv[0]); mx[u] = vv[0]; idx[u] = lane * 4;
+#pragma unroll
+        for (int e = 1; e < 4; ++e)
+            if (fabsf(vv[e]) > amax[u]) { amax[u] = fabsf(vv[e]); mx[u] = vv[e]; idx[u] = lane * 4 + e; }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        float a2[NB], m2[NB];
+        int i2[NB];
+#pragma unroll
+        for (int u = 0; u < NB; ++u) { a2[u] = __shfl_xor(amax[u], o); m2[u] = __shfl_xor(mx[u], o); i2[u] = __shfl_xor(idx[u], o); }
+#pragma unroll
+        for (int u = 0; u < NB; ++u)
+            if (a2[u] > amax[u] || (a2[u] == amax[u] && i2[u] < idx[u])) { amax[u] = a2[u]; mx[u] = m2[u]; idx[u] = i2[u]; }
+    }
+    int s[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+        const float vv[4] = {y[u].x, y[u].y, y[u].z, y[u].w};
+        int q[4] = {0, 0, 0, 0};
+        float d = 1.f;   // all-zero block: see quant_q8k_block
+        if (amax[u] != 0.f) {
+            const float iscale = -127.f / mx[u];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) q[e] = min(127, (int) rintf(iscale * vv[e]));
+            d = 1 / iscale;
+        }
+        typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
+        *(h4_t *) (codes + u * code_stride) = h4_t{(_Float16) (float) q[0], (_Float16) (float) q[1], (_Float16) (float) q[2], (_Float16) (float) q[3]};
+        if (lane == 0) dy_out[u * dy_stride] = d;
+        s[u] = q[0] + q[1] + q[2] + q[3];
+    }
+#pragma unroll
+    for (int o = 1; o < 8; o <<= 1)
+#pragma unroll
+        for (int u = 0; u < NB; ++u) s[u] += __shfl_xor(s[u], o);
+    if ((lane & 7) == 0) {
+        const int j = lane >> 3;
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+            const int hi = (s[u] >= 0) ? (s[u] >> 6) : -((-s[u] + 63) >> 6);   // floor(s / 64)
+            const int lo = s[u] - 64 * hi;
+            typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+            *(h2_t *) (aext + u * aext_stride + 2 * j) = h2_t{(_Float16) (float) hi, (_Float16) (float) lo};
+        }
+    }
+}
+
 // quantize one 32-block (8 lanes x float4) to Q8_0 codes with the x86 AVX2 semantics
 __device__ __forceinline__ void quant_q80_block(float4 y, int lane, q2a_half * codes, float * dy_out) {
     float amax = fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w)));
