@@ -27,6 +27,7 @@ namespace {
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef float f2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void * lds_ptr_t;
 
 constexpr int BK = 64;
@@ -210,11 +211,23 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
                 asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(al[n]) : "v"(s_al), "i"((i + 1) * 64));
                 asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(ae[n]) : "v"(s_ae), "i"((i + 1) * 512));
             }
+            f4 s2v[4];   // the four min-term MFMAs first, their latency under the first rescale products
+#pragma unroll
+            for (int j = 0; j < 4; ++j) s2v[j] = __builtin_amdgcn_mfma_f32_16x16x16f16(ae[c], we[j], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const f4 s2 = __builtin_amdgcn_mfma_f32_16x16x16f16(ae[c], we[j], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                const f4 s2 = s2v[j];
+                // packed fp32 (v_pk_mul/v_pk_fma): two rows per instruction
+                const f2 bj = {bet[j], bet[j]}, gj = {gam[j], gam[j]};
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc[i][j][r] = acc[i][j][r] * (al[c][r] * bet[j]) - gam[j] * s2[r];
+                for (int r = 0; r < 4; r += 2) {
+                    const f2 a2 = {acc[i][j][r], acc[i][j][r + 1]};
+                    const f2 al2 = {al[c][r], al[c][r + 1]};
+                    const f2 s22 = {s2[r], s2[r + 1]};
+                    const f2 res = a2 * (al2 * bj) - gj * s22;
+                    acc[i][j][r] = res[0];
+                    acc[i][j][r + 1] = res[1];
+                }
             }
             if (i + 1 < 8) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(al[n]), "+v"(ae[n]));
             __builtin_amdgcn_sched_barrier(0);   // one row block at a time: bounds the live min-term results
