@@ -1,0 +1,50 @@
+/*
+ * ggml-q2a.h — the MI355X (gfx950) ggml backend of this repository: lib/libggml-q2a.so.
+ *
+ * A ggml backend plugin in the shape of the reference's own GPU backends (ggml/include/ggml-cuda.h:22-44): the
+ * reference's whisper_full() builds its conv and encoder graphs unchanged (src/qwen2-whisper.cpp:1892-2203),
+ * ggml_backend_sched splits them by supports_op, and graph_compute runs every node of the hot path on the GPU with
+ * this repository's HIP kernels — including the nodes no shipped backend accepts, MUL_MAT(F32 im2col, F16 conv
+ * kernel) and POOL_1D, so F16 / Q4_K / Q8_0 / Q4_0 model files run without the CPU split.
+ *
+ * Vtables implemented (ggml/src/ggml-backend-impl.h): ggml_backend_buffer_type_i :15-27, ggml_backend_buffer_i
+ * :39-57, ggml_backend_i :86-133, ggml_backend_device_i :153-196, ggml_backend_reg_i :208-218.
+ *
+ * The plugin is compiled against ggml's headers (GGML_DIR in the package Makefile) and resolves ggml's own
+ * functions (ggml_nbytes, ggml_backend_buffer_init, ...) from the application's ggml at load time, like a backend
+ * built into libggml. Integration into whisper.cpp: INTEGRATION.md §"ggml backend".
+ */
+#pragma once
+
+#include "ggml.h"
+#include "ggml-backend.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GGML_Q2A_NAME "Q2A"
+#define GGML_Q2A_MAX_DEVICES 16
+
+/* backend (one HIP stream) on HIP device `device`; NULL if the device does not exist */
+GGML_API ggml_backend_t ggml_backend_q2a_init(int device);          /* replaces ggml_backend_cuda_init, ggml-cuda.h:23 */
+GGML_API bool ggml_backend_is_q2a(ggml_backend_t backend);          /* ggml_backend_is_cuda, ggml-cuda.h:25 */
+
+/* device memory buffer type (weights and compute buffers) */
+GGML_API ggml_backend_buffer_type_t ggml_backend_q2a_buffer_type(int device);   /* ggml-cuda.h:28 */
+
+GGML_API int  ggml_backend_q2a_get_device_count(void);                                           /* ggml-cuda.h:36 */
+GGML_API void ggml_backend_q2a_get_device_description(int device, char * description, size_t description_size);
+GGML_API void ggml_backend_q2a_get_device_memory(int device, size_t * free, size_t * total);      /* ggml-cuda.h:38 */
+
+GGML_API ggml_backend_reg_t ggml_backend_q2a_reg(void);             /* ggml-cuda.h:43 */
+
+/* statistics of the last graph_compute on this backend (test / profiling aid): nodes executed per kind */
+typedef struct {
+    int n_nodes, n_mul_mat_fast, n_mul_mat_f32, n_attn_fused, n_other;
+} ggml_backend_q2a_stats;
+GGML_API void ggml_backend_q2a_get_stats(ggml_backend_t backend, ggml_backend_q2a_stats * stats);
+
+#ifdef __cplusplus
+}
+#endif

@@ -1,0 +1,997 @@
+// ggml-q2a.hip — the MI355X ggml backend (include/ggml-q2a.h): buffer type, buffer, backend, device and registry
+// vtables of ggml/src/ggml-backend-impl.h:15-224 over HIP device memory, and a graph executor that runs every node
+// of the reference's conv and encoder graphs (src/qwen2-whisper.cpp:1892-2203) on gfx950.
+//
+// Node kinds and how they run here:
+//   MUL_MAT, weight × activation (F16 / Q4_K / Q8_0 / Q4_0 weights, F32 rows): ggml's activation conversion
+//       (fp16 RNE / Q8_K / Q8_0, the same quantizer kernels as the fused engine) + the engine's MFMA GEMM
+//       (q2a_launch_gemm) on the weight repacked once into the GEMM layout (cached per weight tensor, dropped when
+//       the tensor's bytes are written again).
+//   MUL_MAT, everything else (conv im2col × F16/F32 kernel, per-head K·Q and V·softmax, F32 weights): an exact-f32
+//       batched GEMM on v_mfma_f32_16x16x4_f32 (f32 in, f32 accumulate: ggml_vec_dot_f32 products, ggml.c:12348).
+//       With an F16 src0, src1 is rounded to fp16 first (ggml's vec_dot_type conversion, ggml.c:12462-12475).
+//   KQ -> SOFT_MAX -> KQV with K, Q, V views of the QKV projections: the fused flash kernel of the engine
+//       (k_attn: F32-class scores from hi/lo fp16 halves, online softmax), when the chain matches exactly.
+//   IM2COL (ggml.c:14717), NORM (:11941, double sums), SOFT_MAX (:13854, double sum), GELU (fp16 table,
+//       :2556-2570), ADD / MUL with broadcast, SCALE, CONT/CPY/DUP (strided), POOL_1D avg (:15077): elementwise /
+//       row kernels below, with the CPU kernels' float operation order.
+// Views, reshapes, permutes and transposes are free. Compiled with -ffp-contract=off (exact op order).
+#include "ggml-q2a.h"
+#include "ggml-backend-impl.h"
+
+#include "q2a_format.h"
+#include "q2a_internal.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#define Q2A_HIP(x)                                                                                   \
+    do {                                                                                             \
+        hipError_t e_ = (x);                                                                         \
+        if (e_ != hipSuccess) GGML_ABORT("ggml-q2a: %s failed: %s", #x, hipGetErrorString(e_));     \
+    } while (0)
+
+#define Q2A_LOG_ERROR(...) fprintf(stderr, __VA_ARGS__)
+
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// ------------------------------------------------------------------------------------------------
+// kernels
+// ------------------------------------------------------------------------------------------------
+struct tview {            // a strided 4-D view: element (i0,i1,i2,i3) at base + i0*nb0 + i1*nb1 + i2*nb2 + i3*nb3
+    char * base;
+    int64_t ne[4];
+    int64_t nb[4];
+};
+
+__device__ __forceinline__ int64_t voff(const tview & t, int64_t i0, int64_t i1, int64_t i2, int64_t i3) {
+    return i0 * t.nb[0] + i1 * t.nb[1] + i2 * t.nb[2] + i3 * t.nb[3];
+}
+
+__device__ __forceinline__ float ld_as_f32(const char * p, int type) {
+    if (type == GGML_TYPE_F16) return (float) *(const _Float16 *) p;
+    return *(const float *) p;
+}
+__device__ __forceinline__ void st_from_f32(char * p, int type, float v) {
+    if (type == GGML_TYPE_F16) *(_Float16 *) p = (_Float16) v;
+    else *(float *) p = v;
+}
+
+// dst = src (any strides, F32/F16 either side), one thread per element of dst's logical shape
+__global__ void k_copy(tview s, int st, tview d, int dt, int64_t n) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t i0 = i % d.ne[0], r = i / d.ne[0];
+    const int64_t i1 = r % d.ne[1], r2 = r / d.ne[1];
+    const int64_t i2 = r2 % d.ne[2], i3 = r2 / d.ne[2];
+    // ggml_dup walks both tensors in their own logical (row-major) element order; with equal element counts the
+    // flat index i maps to the source's own (i0, i1, i2, i3)
+    const int64_t j0 = i % s.ne[0], q = i / s.ne[0];
+    const int64_t j1 = q % s.ne[1], q2 = q / s.ne[1];
+    const int64_t j2 = q2 % s.ne[2], j3 = q2 / s.ne[2];
+    const char * sp = s.base + voff(s, j0, j1, j2, j3);
+    char * dp = d.base + voff(d, i0, i1, i2, i3);
+    if (st == dt && st == GGML_TYPE_F16) *(uint16_t *) dp = *(const uint16_t *) sp;
+    else st_from_f32(dp, dt, ld_as_f32(sp, st));
+}
+
+// dst = a (op) b with b broadcast (ggml_can_repeat), F32. op 0 add, 1 mul
+template <int OP>
+__global__ void k_binary(tview a, tview b, tview d, int64_t n) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t i0 = i % d.ne[0], r = i / d.ne[0];
+    const int64_t i1 = r % d.ne[1], r2 = r / d.ne[1];
+    const int64_t i2 = r2 % d.ne[2], i3 = r2 / d.ne[2];
+    const float x = *(const float *) (a.base + voff(a, i0, i1, i2, i3));
+    const float y = *(const float *) (b.base + voff(b, i0 % b.ne[0], i1 % b.ne[1], i2 % b.ne[2], i3 % b.ne[3]));
+    *(float *) (d.base + voff(d, i0, i1, i2, i3)) = OP == 0 ? x + y : x * y;
+}
+
+// unary F32: 0 scale (ggml_vec_scale_f32), 1 GELU (ggml_vec_gelu_f32 with GGML_GELU_FP16, ggml.c:2556-2570)
+template <int OP>
+__global__ void k_unary(tview a, tview d, int64_t n, float scale, const uint16_t * gelu_tab) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t i0 = i % d.ne[0], r = i / d.ne[0];
+    const int64_t i1 = r % d.ne[1], r2 = r / d.ne[1];
+    const int64_t i2 = r2 % d.ne[2], i3 = r2 / d.ne[2];
+    const float x = *(const float *) (a.base + voff(a, i0, i1, i2, i3));
+    float y;
+    if (OP == 0) {
+        y = x * scale;
+    } else {
+        if (x <= -10.0f) y = 0.0f;
+        else if (x >= 10.0f) y = x;
+        else {
+            const _Float16 h = (_Float16) x;
+            uint16_t u;
+            __builtin_memcpy(&u, &h, 2);
+            const uint16_t g = gelu_tab[u];
+            _Float16 gh;
+            __builtin_memcpy(&gh, &g, 2);
+            y = (float) gh;
+        }
+    }
+    *(float *) (d.base + voff(d, i0, i1, i2, i3)) = y;
+}
+
+__device__ __forceinline__ double block_sum_d(double v, double * red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    double t = 0.0;
+    for (int i = 0; i < (int) (blockDim.x >> 6); ++i) t += red[i];
+    return t;
+}
+__device__ __forceinline__ float block_max_f(float v, float * red) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    __syncthreads();
+    if (l == 0) red[w] = v;
+    __syncthreads();
+    float t = -INFINITY;
+    for (int i = 0; i < (int) (blockDim.x >> 6); ++i) t = fmaxf(t, red[i]);
+    return t;
+}
+
+// NORM over ne0 (ggml_compute_forward_norm_f32, ggml.c:11941-11990): mean and variance with double sums,
+// y = (x - mean) * (1/sqrtf(var + eps)). One block per row.
+__global__ __launch_bounds__(256) void k_norm(tview a, tview d, float eps) {
+    __shared__ double red[4];
+    const int64_t r = blockIdx.x;
+    const int64_t i1 = r % a.ne[1], i2 = (r / a.ne[1]) % a.ne[2], i3 = r / (a.ne[1] * a.ne[2]);
+    const float * x = (const float *) (a.base + voff(a, 0, i1, i2, i3));
+    float * y = (float *) (d.base + voff(d, 0, i1, i2, i3));
+    const int n = (int) a.ne[0];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) s += (double) x[i];
+    s = block_sum_d(s, red);
+    const float mean = (float) (s / n);
+    double s2 = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const float v = x[i] - mean;
+        s2 += (double) (v * v);
+    }
+    s2 = block_sum_d(s2, red);
+    const float variance = (float) (s2 / n);
+    const float scale = 1.0f / sqrtf(variance + eps);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) y[i] = (x[i] - mean) * scale;
+}
+
+// SOFT_MAX without mask (ggml.c:13854-13950): w = x*scale, max, e = exp(w - max) with a double sum,
+// y = e * (float)(1/sum). One block per row.
+__global__ __launch_bounds__(256) void k_softmax(tview a, tview d, float scale) {
+    __shared__ double red[4];
+    __shared__ float redf[4];
+    const int64_t r = blockIdx.x;
+    const int64_t i1 = r % a.ne[1], i2 = (r / a.ne[1]) % a.ne[2], i3 = r / (a.ne[1] * a.ne[2]);
+    const float * x = (const float *) (a.base + voff(a, 0, i1, i2, i3));
+    float * y = (float *) (d.base + voff(d, 0, i1, i2, i3));
+    const int n = (int) a.ne[0];
+    float mx = -INFINITY;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) mx = fmaxf(mx, x[i] * scale);
+    mx = block_max_f(mx, redf);
+    double s = 0.0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const float e = expf(x[i] * scale - mx);
+        y[i] = e;
+        s += (double) e;
+    }
+    s = block_sum_d(s, red);
+    const float inv = (float) (1.0 / s);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) y[i] = y[i] * inv;
+}
+
+// IM2COL, 1-D (ggml.c:14717-14786): dst[n][ow][ic*KW + kw] = src[n][ic][ow*s0 + kw*d0 - p0] (0 outside)
+__global__ void k_im2col1d(tview s, tview d, int dt, int IC, int IW, int KW, int OW, int s0, int p0, int d0, int64_t n) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int kw = (int) (i % KW);
+    int64_t r = i / KW;
+    const int ic = (int) (r % IC); r /= IC;
+    const int ow = (int) (r % OW);
+    const int64_t in = r / OW;
+    const int64_t iw = (int64_t) ow * s0 + (int64_t) kw * d0 - p0;
+    const float v = (iw < 0 || iw >= IW) ? 0.0f : *(const float *) (s.base + in * s.nb[2] + ic * s.nb[1] + iw * s.nb[0]);
+    st_from_f32(d.base + voff(d, (int64_t) ic * KW + kw, ow, in, 0), dt, v);
+}
+
+// POOL_1D avg, kernel == stride, no padding (ggml_compute_forward_pool_1d_sk_p0, ggml.c:15077-15125):
+// acc = 0; acc += x[j] for the k inputs; acc /= k
+__global__ void k_pool1d_avg(tview s, tview d, int k, int64_t n) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t i0 = i % d.ne[0], r = i / d.ne[0];
+    const int64_t i1 = r % d.ne[1], r2 = r / d.ne[1];
+    const int64_t i2 = r2 % d.ne[2], i3 = r2 / d.ne[2];
+    float acc = 0.0f;
+    for (int ki = 0; ki < k; ++ki) acc += *(const float *) (s.base + voff(s, i0 * k + ki, i1, i2, i3));
+    acc /= (float) k;
+    *(float *) (d.base + voff(d, i0, i1, i2, i3)) = acc;
+}
+
+// fp32 -> fp16 (RNE) of a contiguous F32 activation block (ggml_fp32_to_fp16_row, the F16 vec_dot_type)
+__global__ void k_f32_to_f16(const float * x, _Float16 * y, int64_t n) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = (_Float16) x[i];
+}
+
+// Batched exact-f32 GEMM: dst[i3][i2][i1][i0] = sum_k src0[i3/r3][i2/r2][i0][k] * src1[i3][i2][i1][k]
+// (ggml_compute_forward_mul_mat semantics for src0 F32/F16 x src1 F32/F16; R16 rounds src1 to fp16 first, the
+// conversion ggml applies for an F16 src0). 64x64 tile per workgroup, 4 waves of 32x32, K-step 16 staged in LDS,
+// v_mfma_f32_16x16x4_f32 (f32 operands, f32 accumulation).
+struct mm_args {
+    tview a, b, d;
+    int ta, tb;
+    int64_t K, r2, r3;
+};
+template <bool R16>
+__global__ __launch_bounds__(256) void k_mm_f32(mm_args p) {
+    __shared__ float As[64][17];
+    __shared__ float Bs[64][17];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int wr = w >> 1, wc = w & 1;
+    const int64_t i0b = (int64_t) blockIdx.x * 64, i1b = (int64_t) blockIdx.y * 64;
+    const int64_t z = blockIdx.z, i2 = z % p.d.ne[2], i3 = z / p.d.ne[2];
+    const char * abase = p.a.base + (i2 / p.r2) * p.a.nb[2] + (i3 / p.r3) * p.a.nb[3];
+    const char * bbase = p.b.base + i2 * p.b.nb[2] + i3 * p.b.nb[3];
+    const int64_t M0 = p.a.ne[1], M1 = p.b.ne[1];
+    f4 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int64_t k0 = 0; k0 < p.K; k0 += 16) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int idx = tid + 256 * u, row = idx >> 4, kk = idx & 15;
+            const int64_t k = k0 + kk;
+            float va = 0.f, vb = 0.f;
+            if (k < p.K && i0b + row < M0) va = ld_as_f32(abase + (i0b + row) * p.a.nb[1] + k * p.a.nb[0], p.ta);
+            if (k < p.K && i1b + row < M1) {
+                vb = ld_as_f32(bbase + (i1b + row) * p.b.nb[1] + k * p.b.nb[0], p.tb);
+                if (R16) vb = (float) (_Float16) vb;
+            }
+            As[row][kk] = va;
+            Bs[row][kk] = vb;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) {
+            const int k = k4 * 4 + (lane >> 4);
+            float av[2], bv[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) av[i] = As[wr * 32 + i * 16 + (lane & 15)][k];
+#pragma unroll
+            for (int j = 0; j < 2; ++j) bv[j] = Bs[wc * 32 + j * 16 + (lane & 15)][k];
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i], bv[j], acc[i][j], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    char * dbase = p.d.base + i2 * p.d.nb[2] + i3 * p.d.nb[3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int64_t c1 = i1b + wc * 32 + j * 16 + (lane & 15);
+            if (c1 >= M1) continue;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t c0 = i0b + wr * 32 + i * 16 + (lane >> 4) * 4 + r;
+                if (c0 < M0) *(float *) (dbase + c1 * p.d.nb[1] + c0 * p.d.nb[0]) = acc[i][j][r];
+            }
+        }
+}
+
+// attention operands for the fused path: per-head fp16 hi/lo halves of Q (already scaled) and K, V^T
+__global__ void k_attn_prep(tview q, tview k, tview v, _Float16 * qh, _Float16 * ql, _Float16 * kh, _Float16 * kl,
+                            _Float16 * vt, int T, int H, int TP, int64_t n) {
+    // element (d, t, h): q/k/v views have ne = [64, T, H]; q,k -> [t][h*64+d], v -> vt[h][d][t]
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int d = (int) (i & 63);
+    const int64_t r = i >> 6;
+    const int t = (int) (r % T), h = (int) (r / T);
+    const float qv = *(const float *) (q.base + voff(q, d, t, h, 0));
+    const float kv = *(const float *) (k.base + voff(k, d, t, h, 0));
+    const float vv = *(const float *) (v.base + voff(v, t, d, h, 0));
+    const int64_t o = (int64_t) t * H * 64 + h * 64 + d;
+    const _Float16 a = (_Float16) qv, b = (_Float16) kv;
+    qh[o] = a; ql[o] = (_Float16) (qv - (float) a);
+    kh[o] = b; kl[o] = (_Float16) (kv - (float) b);
+    vt[((int64_t) h * 64 + d) * TP + t] = (_Float16) vv;
+}
+
+// fused attention output [t][h*64+d] (f32) -> the KQV node's layout dst (ne = [64, T, H])
+__global__ void k_attn_out(const float * o, tview d, int T, int H, int64_t n) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int dd = (int) (i & 63);
+    const int64_t r = i >> 6;
+    const int t = (int) (r % T), h = (int) (r / T);
+    *(float *) (d.base + voff(d, dd, t, h, 0)) = o[(int64_t) t * H * 64 + h * 64 + dd];
+}
+
+// ------------------------------------------------------------------------------------------------
+// devices, buffers, weight cache
+// ------------------------------------------------------------------------------------------------
+struct packed_w {
+    const char * raw;        // the weight tensor's bytes in a Q2A buffer
+    size_t raw_bytes;
+    int type, N, K;
+    void * dev;              // repacked GEMM operand (q2a_pack_linear layout)
+    uint64_t off[6];
+};
+
+struct q2a_device_ctx {
+    int device = 0;
+    std::string name, desc;
+    ggml_backend_buffer_type buft;
+    ggml_backend_device dev;
+    std::mutex mu;
+    std::vector<packed_w> wcache;
+    uint16_t * gelu_tab = nullptr;     // device copy of the 64 Ki-entry fp16 GELU table (lazy)
+};
+
+struct q2a_reg_ctx {
+    std::vector<q2a_device_ctx *> devs;
+};
+
+struct q2a_buffer_ctx {
+    int device;
+    void * ptr;
+    size_t size;
+    std::string name;
+};
+
+struct q2a_backend_ctx {
+    int device;
+    std::string name;
+    hipStream_t stream = nullptr;
+    void * scratch = nullptr;
+    size_t scratch_bytes = 0;
+    ggml_backend_q2a_stats stats{};
+};
+
+q2a_reg_ctx * reg_ctx();
+ggml_backend_reg * the_reg();
+
+q2a_device_ctx * dev_ctx(int device) {
+    q2a_reg_ctx * r = reg_ctx();
+    if (device < 0 || device >= (int) r->devs.size()) return nullptr;
+    return r->devs[device];
+}
+
+// drop cached repacks whose source bytes overlap [p, p + n)
+void invalidate(int device, const void * p, size_t n) {
+    q2a_device_ctx * d = dev_ctx(device);
+    if (!d) return;
+    std::lock_guard<std::mutex> lk(d->mu);
+    const char * a = (const char *) p;
+    for (size_t i = 0; i < d->wcache.size();) {
+        packed_w & w = d->wcache[i];
+        if (w.raw < a + n && a < w.raw + w.raw_bytes) {
+            (void) hipSetDevice(device);
+            (void) hipFree(w.dev);
+            d->wcache[i] = d->wcache.back();
+            d->wcache.pop_back();
+        } else {
+            ++i;
+        }
+    }
+}
+
+const uint16_t * gelu_table(int device) {
+    q2a_device_ctx * d = dev_ctx(device);
+    std::lock_guard<std::mutex> lk(d->mu);
+    if (!d->gelu_tab) {
+        std::vector<uint16_t> t(65536);
+        q2a_make_gelu_table(t.data());
+        Q2A_HIP(hipMalloc((void **) &d->gelu_tab, 65536 * 2));
+        Q2A_HIP(hipMemcpy(d->gelu_tab, t.data(), 65536 * 2, hipMemcpyHostToDevice));
+    }
+    return d->gelu_tab;
+}
+
+// ---- buffer -----------------------------------------------------------------------------------
+const char * buf_get_name(ggml_backend_buffer_t b) { return ((q2a_buffer_ctx *) b->context)->name.c_str(); }
+void buf_free(ggml_backend_buffer_t b) {
+    q2a_buffer_ctx * c = (q2a_buffer_ctx *) b->context;
+    invalidate(c->device, c->ptr, c->size);
+    (void) hipSetDevice(c->device);
+    (void) hipFree(c->ptr);
+    delete c;
+}
+void * buf_get_base(ggml_backend_buffer_t b) { return ((q2a_buffer_ctx *) b->context)->ptr; }
+void buf_memset_tensor(ggml_backend_buffer_t b, ggml_tensor * t, uint8_t v, size_t off, size_t n) {
+    q2a_buffer_ctx * c = (q2a_buffer_ctx *) b->context;
+    Q2A_HIP(hipSetDevice(c->device));
+    invalidate(c->device, (char *) t->data + off, n);
+    Q2A_HIP(hipMemset((char *) t->data + off, v, n));
+}
+void buf_set_tensor(ggml_backend_buffer_t b, ggml_tensor * t, const void * data, size_t off, size_t n) {
+    q2a_buffer_ctx * c = (q2a_buffer_ctx *) b->context;
+    Q2A_HIP(hipSetDevice(c->device));
+    invalidate(c->device, (char *) t->data + off, n);
+    Q2A_HIP(hipMemcpy((char *) t->data + off, data, n, hipMemcpyHostToDevice));
+}
+void buf_get_tensor(ggml_backend_buffer_t b, const ggml_tensor * t, void * data, size_t off, size_t n) {
+    q2a_buffer_ctx * c = (q2a_buffer_ctx *) b->context;
+    Q2A_HIP(hipSetDevice(c->device));
+    Q2A_HIP(hipMemcpy(data, (const char *) t->data + off, n, hipMemcpyDeviceToHost));
+}
+bool is_q2a_buffer(ggml_backend_buffer_t b);
+bool buf_cpy_tensor(ggml_backend_buffer_t b, const ggml_tensor * src, ggml_tensor * dst) {
+    if (!src->buffer || !is_q2a_buffer(src->buffer)) return false;
+    q2a_buffer_ctx * c = (q2a_buffer_ctx *) b->context;
+    Q2A_HIP(hipSetDevice(c->device));
+    invalidate(c->device, dst->data, ggml_nbytes(dst));
+    Q2A_HIP(hipMemcpy(dst->data, src->data, ggml_nbytes(src), hipMemcpyDeviceToDevice));
+    return true;
+}
+void buf_clear(ggml_backend_buffer_t b, uint8_t v) {
+    q2a_buffer_ctx * c = (q2a_buffer_ctx *) b->context;
+    Q2A_HIP(hipSetDevice(c->device));
+    invalidate(c->device, c->ptr, c->size);
+    Q2A_HIP(hipMemset(c->ptr, v, c->size));
+}
+
+const ggml_backend_buffer_i k_buffer_iface = {
+    /* get_name      */ buf_get_name,
+    /* free_buffer   */ buf_free,
+    /* get_base      */ buf_get_base,
+    /* init_tensor   */ nullptr,
+    /* memset_tensor */ buf_memset_tensor,
+    /* set_tensor    */ buf_set_tensor,
+    /* get_tensor    */ buf_get_tensor,
+    /* cpy_tensor    */ buf_cpy_tensor,
+    /* clear         */ buf_clear,
+    /* reset         */ nullptr,
+};
+
+bool is_q2a_buffer(ggml_backend_buffer_t b) { return b->iface.get_name == buf_get_name; }
+
+// ---- buffer type --------------------------------------------------------------------------------
+const char * buft_get_name(ggml_backend_buffer_type_t t) { return ((q2a_device_ctx *) t->context)->name.c_str(); }
+ggml_backend_buffer_t buft_alloc(ggml_backend_buffer_type_t t, size_t size) {
+    q2a_device_ctx * d = (q2a_device_ctx *) t->context;
+    if (hipSetDevice(d->device) != hipSuccess) return nullptr;
+    void * p = nullptr;
+    if (hipMalloc(&p, std::max<size_t>(size, 1)) != hipSuccess) {
+        (void) hipGetLastError();
+        Q2A_LOG_ERROR("ggml-q2a: allocating %.2f MB on device %d failed\n", size / 1e6, d->device);
+        return nullptr;
+    }
+    q2a_buffer_ctx * c = new q2a_buffer_ctx{d->device, p, size, d->name};
+    return ggml_backend_buffer_init(t, k_buffer_iface, c, size);
+}
+size_t buft_get_alignment(ggml_backend_buffer_type_t) { return 256; }
+bool buft_is_host(ggml_backend_buffer_type_t) { return false; }
+
+const ggml_backend_buffer_type_i k_buft_iface = {
+    /* get_name       */ buft_get_name,
+    /* alloc_buffer   */ buft_alloc,
+    /* get_alignment  */ buft_get_alignment,
+    /* get_max_size   */ nullptr,
+    /* get_alloc_size */ nullptr,
+    /* is_host        */ buft_is_host,
+};
+
+// ------------------------------------------------------------------------------------------------
+// graph execution
+// ------------------------------------------------------------------------------------------------
+tview tv(const ggml_tensor * t) {
+    tview v;
+    v.base = (char *) t->data;
+    for (int i = 0; i < 4; ++i) { v.ne[i] = t->ne[i]; v.nb[i] = (int64_t) t->nb[i]; }
+    return v;
+}
+
+dim3 grid1(int64_t n) { return dim3((unsigned) ((n + 255) / 256)); }
+
+void * scratch(q2a_backend_ctx * b, size_t bytes) {
+    if (bytes > b->scratch_bytes) {
+        Q2A_HIP(hipStreamSynchronize(b->stream));
+        if (b->scratch) Q2A_HIP(hipFree(b->scratch));
+        b->scratch = nullptr;
+        Q2A_HIP(hipMalloc(&b->scratch, bytes));
+        b->scratch_bytes = bytes;
+    }
+    return b->scratch;
+}
+
+bool is_weight_type(int t) {
+    return t == GGML_TYPE_F16 || t == GGML_TYPE_Q4_K || t == GGML_TYPE_Q8_0 || t == GGML_TYPE_Q4_0;
+}
+
+// the fast MUL_MAT path: contiguous 2-D weight (ne00 = K, ne01 = N) x contiguous F32 rows
+bool mm_fast_ok(const ggml_tensor * op) {
+    const ggml_tensor * w = op->src[0];
+    const ggml_tensor * x = op->src[1];
+    if (!is_weight_type(w->type) || x->type != GGML_TYPE_F32 || op->type != GGML_TYPE_F32) return false;
+    if (!ggml_is_contiguous(w) || !ggml_is_contiguous(x) || !ggml_is_contiguous(op)) return false;
+    if (w->ne[2] != 1 || w->ne[3] != 1) return false;
+    const int64_t K = w->ne[0], N = w->ne[1];
+    return N % 128 == 0 && K % 256 == 0 && K <= 8192 && N <= (1 << 30);
+}
+
+const packed_w * get_packed(q2a_backend_ctx * b, const ggml_tensor * w) {
+    q2a_device_ctx * d = dev_ctx(b->device);
+    {
+        std::lock_guard<std::mutex> lk(d->mu);
+        for (const packed_w & p : d->wcache)
+            if (p.raw == (const char *) w->data && p.type == w->type && p.N == w->ne[1] && p.K == w->ne[0]) return &p;
+    }
+    // first use: repack on the host from the device bytes (one-time, per weight tensor)
+    const size_t nb = ggml_nbytes(w);
+    std::vector<uint8_t> raw(nb);
+    Q2A_HIP(hipStreamSynchronize(b->stream));
+    Q2A_HIP(hipMemcpy(raw.data(), w->data, nb, hipMemcpyDeviceToHost));
+    packed_w p;
+    p.raw = (const char *) w->data; p.raw_bytes = nb; p.type = w->type; p.N = (int) w->ne[1]; p.K = (int) w->ne[0];
+    std::vector<uint8_t> out;
+    if (q2a_pack_linear(raw.data(), w->type, p.N, p.K, out, p.off) != 0) GGML_ABORT("ggml-q2a: cannot pack %s", w->name);
+    Q2A_HIP(hipMalloc(&p.dev, out.size()));
+    Q2A_HIP(hipMemcpy(p.dev, out.data(), out.size(), hipMemcpyHostToDevice));
+    std::lock_guard<std::mutex> lk(d->mu);
+    d->wcache.push_back(p);
+    return &d->wcache.back();
+}
+
+void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op) {
+    const ggml_tensor * w = op->src[0];
+    const ggml_tensor * x = op->src[1];
+    const int K = (int) w->ne[0], N = (int) w->ne[1];
+    const int M = (int) (x->ne[1] * x->ne[2] * x->ne[3]);
+    const int blk = w->type == GGML_TYPE_Q4_K ? 256 : w->type == GGML_TYPE_F16 ? 0 : 32;
+    const int MP = (M + 255) / 256 * 256;
+    // scratch: A operand fp16 [M][K] | dy [K/blk][MP] | aext [K/256][MP][16]
+    const size_t a_bytes = ((size_t) M * K * 2 + 255) & ~size_t(255);
+    const size_t dy_bytes = blk ? ((size_t) (K / blk) * MP * 4 + 255) & ~size_t(255) : 0;
+    const size_t ae_bytes = blk == 256 ? (size_t) (K / 256) * MP * 32 : 0;
+    char * s = (char *) scratch(b, a_bytes + dy_bytes + ae_bytes);
+    q2a_half * A = (q2a_half *) s;
+    float * dy = (float *) (s + a_bytes);
+    q2a_half * aext = (q2a_half *) (s + a_bytes + dy_bytes);
+    if (blk == 0) {
+        const int64_t n = (int64_t) M * K;
+        hipLaunchKernelGGL(k_f32_to_f16, grid1(n), dim3(256), 0, b->stream, (const float *) x->data, A, n);
+    } else {
+        q2a_quant_args qa{(const float *) x->data, nullptr, M, K, blk == 256 ? 1 : 2, A, dy, aext, MP};
+        Q2A_HIP(q2a_launch_quant_act(qa, b->stream));
+    }
+    q2a_gemm_args a;
+    memset(&a, 0, sizeof(a));
+    a.A = A; a.lda = K; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
+    a.M = M; a.N = N; a.K = K; a.ldw = K;
+    a.outF = (float *) op->data; a.ldo = N;
+    a.gelu_tab = gelu_table(b->device);
+    if (blk == 0) {
+        a.W = (const q2a_half *) w->data;
+    } else {
+        const packed_w * p = get_packed(b, w);
+        const char * base = (const char *) p->dev;
+        a.W = (const q2a_half *) (base + p->off[0]);
+        a.nblk = K / blk;
+        a.dx = (const float *) (base + p->off[1]);
+        a.dy = dy; a.dy_ld = MP;
+        if (blk == 256) {
+            a.dmin = (const float *) (base + p->off[2]);
+            a.wext = (const q2a_half *) (base + p->off[3]);
+            a.beta = (const float *) (base + p->off[4]);
+            a.gamma = (const float *) (base + p->off[5]);
+            a.aext = aext;
+        }
+    }
+    Q2A_HIP(q2a_launch_gemm(a, Q2A_EPI_STORE_F, blk, b->stream));
+}
+
+void run_mm_f32(q2a_backend_ctx * b, ggml_tensor * op) {
+    const ggml_tensor * s0 = op->src[0];
+    const ggml_tensor * s1 = op->src[1];
+    mm_args p;
+    p.a = tv(s0); p.b = tv(s1); p.d = tv(op);
+    p.ta = s0->type; p.tb = s1->type;
+    p.K = s0->ne[0];
+    p.r2 = s1->ne[2] / s0->ne[2];
+    p.r3 = s1->ne[3] / s0->ne[3];
+    const dim3 g((unsigned) ((op->ne[0] + 63) / 64), (unsigned) ((op->ne[1] + 63) / 64), (unsigned) (op->ne[2] * op->ne[3]));
+    if (s0->type == GGML_TYPE_F16) hipLaunchKernelGGL(k_mm_f32<true>, g, dim3(256), 0, b->stream, p);
+    else hipLaunchKernelGGL(k_mm_f32<false>, g, dim3(256), 0, b->stream, p);
+}
+
+// KQ = MUL_MAT(K, Q) -> SOFT_MAX(KQ, no mask) -> KQV = MUL_MAT(V, KQ_soft_max), heads of 64 (qwen2-whisper.cpp:
+// 2052-2106): when nodes i..i+2 form exactly this chain and KQ / KQ_soft_max feed nothing else, run it as the
+// engine's flash kernel and skip the 20 x T x T score tensors. Returns the number of nodes consumed (0 = no match).
+int try_fused_attention(q2a_backend_ctx * b, ggml_cgraph * g, int i) {
+    static const bool off = [] { const char * v = getenv("GGML_Q2A_NO_FUSED_ATTN"); return v && atoi(v); }();
+    if (off || i + 2 >= ggml_graph_n_nodes(g)) return 0;
+    ggml_tensor * kq = ggml_graph_node(g, i);
+    ggml_tensor * sm = ggml_graph_node(g, i + 1);
+    ggml_tensor * kqv = ggml_graph_node(g, i + 2);
+    if (kq->op != GGML_OP_MUL_MAT || sm->op != GGML_OP_SOFT_MAX || kqv->op != GGML_OP_MUL_MAT) return 0;
+    if (sm->src[0] != kq || sm->src[1] != nullptr || kqv->src[1] != sm) return 0;
+    float scale, max_bias;
+    memcpy(&scale, (const float *) sm->op_params + 0, 4);
+    memcpy(&max_bias, (const float *) sm->op_params + 1, 4);
+    if (scale != 1.0f || max_bias != 0.0f) return 0;
+    // the score tensors must be used by this chain only
+    for (int j = 0; j < ggml_graph_n_nodes(g); ++j) {
+        ggml_tensor * n = ggml_graph_node(g, j);
+        if (n == sm || n == kqv) continue;
+        for (int s = 0; s < GGML_MAX_SRC; ++s)
+            if (n->src[s] == kq || n->src[s] == sm) return 0;
+    }
+    if ((kq->flags | sm->flags) & GGML_TENSOR_FLAG_OUTPUT) return 0;
+    const ggml_tensor * K = kq->src[0];
+    const ggml_tensor * Q = kq->src[1];
+    const ggml_tensor * V = kqv->src[0];
+    const int64_t T = Q->ne[1], H = Q->ne[2];
+    auto f32 = [](const ggml_tensor * t) { return t->type == GGML_TYPE_F32 && t->nb[0] == 4 && t->ne[3] == 1; };
+    if (!f32(K) || !f32(Q) || !f32(V) || kqv->type != GGML_TYPE_F32 || kqv->ne[3] != 1) return 0;
+    if (Q->ne[0] != 64 || K->ne[0] != 64 || K->ne[1] != T || K->ne[2] != H) return 0;
+    if (V->ne[0] != T || V->ne[1] != 64 || V->ne[2] != H) return 0;
+    if (kqv->ne[0] != 64 || kqv->ne[1] != T || kqv->ne[2] != H) return 0;
+    const int TP = (int) ((T + 63) / 64 * 64);
+    const int64_t D = H * 64, n = T * D;
+    const size_t hb = ((size_t) n * 2 + 255) & ~size_t(255);
+    const size_t vb = ((size_t) H * 64 * TP * 2 + 255) & ~size_t(255);
+    char * s = (char *) scratch(b, 4 * hb + vb + (size_t) n * 4);
+    _Float16 *qh = (_Float16 *) s, *ql = (_Float16 *) (s + hb), *kh = (_Float16 *) (s + 2 * hb), *kl = (_Float16 *) (s + 3 * hb);
+    _Float16 * vt = (_Float16 *) (s + 4 * hb);
+    float * o = (float *) (s + 4 * hb + vb);
+    Q2A_HIP(hipMemsetAsync(vt, 0, vb, b->stream));   // V^T tail columns past T are read as zero weights
+    hipLaunchKernelGGL(k_attn_prep, grid1(n), dim3(256), 0, b->stream, tv(Q), tv(K), tv(V), qh, ql, kh, kl, vt, (int) T, (int) H, TP, n);
+    q2a_attn_args at{(const q2a_half *) qh, (const q2a_half *) ql, (const q2a_half *) kh, (const q2a_half *) kl,
+                     (const q2a_half *) vt, 1, (int) T, (int) D, (int) H, TP, nullptr, o};
+    Q2A_HIP(q2a_launch_attention(at, b->stream));
+    hipLaunchKernelGGL(k_attn_out, grid1(n), dim3(256), 0, b->stream, (const float *) o, tv(kqv), (int) T, (int) H, n);
+    b->stats.n_attn_fused++;
+    return 3;
+}
+
+bool op_supported(const ggml_tensor * op) {
+    auto f32 = [](const ggml_tensor * t) { return t && t->type == GGML_TYPE_F32; };
+    auto f = [](const ggml_tensor * t) { return t && (t->type == GGML_TYPE_F32 || t->type == GGML_TYPE_F16); };
+    switch (op->op) {
+        case GGML_OP_NONE: case GGML_OP_RESHAPE: case GGML_OP_VIEW: case GGML_OP_PERMUTE: case GGML_OP_TRANSPOSE:
+            return true;
+        case GGML_OP_MUL_MAT: {
+            const ggml_tensor * a = op->src[0];
+            const ggml_tensor * x = op->src[1];
+            if (op->type != GGML_TYPE_F32 || a->ne[2] == 0 || a->ne[3] == 0) return false;
+            if (x->ne[2] % a->ne[2] || x->ne[3] % a->ne[3]) return false;
+            if (mm_fast_ok(op)) return true;
+            return f(a) && f(x) && a->nb[0] == ggml_type_size(a->type) && x->nb[0] == ggml_type_size(x->type);
+        }
+        case GGML_OP_ADD: case GGML_OP_MUL:
+            return f32(op) && f32(op->src[0]) && f32(op->src[1]) && ggml_can_repeat(op->src[1], op->src[0]);
+        case GGML_OP_SCALE:
+            return f32(op) && f32(op->src[0]);
+        case GGML_OP_NORM: case GGML_OP_SOFT_MAX:
+            if (op->op == GGML_OP_SOFT_MAX && op->src[1]) return false;   // masks / ALiBi are not on this path
+            return f32(op) && f32(op->src[0]) && op->src[0]->nb[0] == 4 && op->nb[0] == 4;
+        case GGML_OP_UNARY:
+            return ggml_get_unary_op(op) == GGML_UNARY_OP_GELU && f32(op) && f32(op->src[0]);
+        case GGML_OP_CONT: case GGML_OP_DUP: case GGML_OP_CPY:
+            return f(op) && f(op->src[0]) && ggml_nelements(op) == ggml_nelements(op->src[0]);
+        case GGML_OP_IM2COL:
+            return ((const int32_t *) op->op_params)[6] == 0 && f32(op->src[1]) && op->src[1]->nb[0] == 4 && f(op) &&
+                   ggml_is_contiguous(op);
+        case GGML_OP_POOL_1D: {
+            const int32_t * pp = (const int32_t *) op->op_params;
+            return pp[0] == GGML_OP_POOL_AVG && pp[1] == pp[2] && pp[3] == 0 && f32(op) && f32(op->src[0]);
+        }
+        default:
+            return false;
+    }
+}
+
+ggml_status graph_compute(ggml_backend_t backend, ggml_cgraph * g) {
+    q2a_backend_ctx * b = (q2a_backend_ctx *) backend->context;
+    Q2A_HIP(hipSetDevice(b->device));
+    b->stats = ggml_backend_q2a_stats{};
+    const int nn = ggml_graph_n_nodes(g);
+    for (int i = 0; i < nn; ++i) {
+        ggml_tensor * op = ggml_graph_node(g, i);
+        if (ggml_is_empty(op) || op->op == GGML_OP_NONE || op->op == GGML_OP_RESHAPE || op->op == GGML_OP_VIEW ||
+            op->op == GGML_OP_PERMUTE || op->op == GGML_OP_TRANSPOSE)
+            continue;
+        b->stats.n_nodes++;
+        const ggml_tensor * s0 = op->src[0];
+        const ggml_tensor * s1 = op->src[1];
+        const int64_t n = ggml_nelements(op);
+        hipStream_t st = b->stream;
+        switch (op->op) {
+            case GGML_OP_MUL_MAT: {
+                const int used = try_fused_attention(b, g, i);
+                if (used) { i += used - 1; break; }
+                if (mm_fast_ok(op)) { run_mm_fast(b, op); b->stats.n_mul_mat_fast++; }
+                else { run_mm_f32(b, op); b->stats.n_mul_mat_f32++; }
+                break;
+            }
+            case GGML_OP_ADD:
+                hipLaunchKernelGGL(k_binary<0>, grid1(n), dim3(256), 0, st, tv(s0), tv(s1), tv(op), n);
+                b->stats.n_other++;
+                break;
+            case GGML_OP_MUL:
+                hipLaunchKernelGGL(k_binary<1>, grid1(n), dim3(256), 0, st, tv(s0), tv(s1), tv(op), n);
+                b->stats.n_other++;
+                break;
+            case GGML_OP_SCALE: {
+                float sc;
+                memcpy(&sc, op->op_params, 4);
+                hipLaunchKernelGGL(k_unary<0>, grid1(n), dim3(256), 0, st, tv(s0), tv(op), n, sc, (const uint16_t *) nullptr);
+                b->stats.n_other++;
+                break;
+            }
+            case GGML_OP_UNARY:
+                hipLaunchKernelGGL(k_unary<1>, grid1(n), dim3(256), 0, st, tv(s0), tv(op), n, 1.0f, gelu_table(b->device));
+                b->stats.n_other++;
+                break;
+            case GGML_OP_NORM: {
+                float eps;
+                memcpy(&eps, op->op_params, 4);
+                hipLaunchKernelGGL(k_norm, dim3((unsigned) ggml_nrows(op)), dim3(256), 0, st, tv(s0), tv(op), eps);
+                b->stats.n_other++;
+                break;
+            }
+            case GGML_OP_SOFT_MAX: {
+                float sc;
+                memcpy(&sc, op->op_params, 4);
+                hipLaunchKernelGGL(k_softmax, dim3((unsigned) ggml_nrows(op)), dim3(256), 0, st, tv(s0), tv(op), sc);
+                b->stats.n_other++;
+                break;
+            }
+            case GGML_OP_CONT: case GGML_OP_DUP: case GGML_OP_CPY: {
+                ggml_tensor * dst = op->op == GGML_OP_CPY ? op->src[1] : op;
+                hipLaunchKernelGGL(k_copy, grid1(n), dim3(256), 0, st, tv(s0), (int) s0->type, tv(dst), (int) dst->type, n);
+                b->stats.n_other++;
+                break;
+            }
+            case GGML_OP_IM2COL: {
+                const int32_t * pp = (const int32_t *) op->op_params;
+                const int IC = (int) s1->ne[1], IW = (int) s1->ne[0], KW = (int) s0->ne[0], OW = (int) op->ne[1];
+                hipLaunchKernelGGL(k_im2col1d, grid1(n), dim3(256), 0, st, tv(s1), tv(op), (int) op->type, IC, IW, KW, OW,
+                                   pp[0], pp[2], pp[4], n);
+                b->stats.n_other++;
+                break;
+            }
+            case GGML_OP_POOL_1D: {
+                const int32_t * pp = (const int32_t *) op->op_params;
+                hipLaunchKernelGGL(k_pool1d_avg, grid1(n), dim3(256), 0, st, tv(s0), tv(op), (int) pp[1], n);
+                b->stats.n_other++;
+                break;
+            }
+            default:
+                Q2A_LOG_ERROR("ggml-q2a: unsupported op %s (%s)\n", ggml_op_desc(op), op->name);
+                return GGML_STATUS_FAILED;
+        }
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) {
+            Q2A_LOG_ERROR("ggml-q2a: %s (%s) launch failed: %s\n", ggml_op_desc(op), op->name, hipGetErrorString(e));
+            return GGML_STATUS_FAILED;
+        }
+    }
+    return GGML_STATUS_SUCCESS;
+}
+
+// ---- backend ------------------------------------------------------------------------------------
+ggml_guid_t q2a_guid() {
+    static ggml_guid guid = {0x51, 0x32, 0x41, 0x2d, 0x67, 0x66, 0x78, 0x39, 0x35, 0x30, 0x4d, 0x49, 0x33, 0x35, 0x35, 0x58};
+    return &guid;
+}
+
+const char * be_get_name(ggml_backend_t be) { return ((q2a_backend_ctx *) be->context)->name.c_str(); }
+void be_free(ggml_backend_t be) {
+    q2a_backend_ctx * b = (q2a_backend_ctx *) be->context;
+    (void) hipSetDevice(b->device);
+    (void) hipStreamSynchronize(b->stream);
+    if (b->scratch) (void) hipFree(b->scratch);
+    (void) hipStreamDestroy(b->stream);
+    delete b;
+    delete be;
+}
+ggml_backend_buffer_type_t be_get_default_buft(ggml_backend_t be) {
+    return ggml_backend_q2a_buffer_type(((q2a_backend_ctx *) be->context)->device);
+}
+void be_set_tensor_async(ggml_backend_t be, ggml_tensor * t, const void * data, size_t off, size_t n) {
+    q2a_backend_ctx * b = (q2a_backend_ctx *) be->context;
+    ggml_backend_buffer_t buf = t->view_src ? t->view_src->buffer : t->buffer;
+    GGML_ASSERT(buf && is_q2a_buffer(buf) && "unsupported buffer type");
+    invalidate(b->device, (char *) t->data + off, n);
+    Q2A_HIP(hipMemcpyAsync((char *) t->data + off, data, n, hipMemcpyHostToDevice, b->stream));
+}
+void be_get_tensor_async(ggml_backend_t be, const ggml_tensor * t, void * data, size_t off, size_t n) {
+    q2a_backend_ctx * b = (q2a_backend_ctx *) be->context;
+    ggml_backend_buffer_t buf = t->view_src ? t->view_src->buffer : t->buffer;
+    GGML_ASSERT(buf && is_q2a_buffer(buf) && "unsupported buffer type");
+    Q2A_HIP(hipMemcpyAsync(data, (const char *) t->data + off, n, hipMemcpyDeviceToHost, b->stream));
+}
+void be_synchronize(ggml_backend_t be) {
+    q2a_backend_ctx * b = (q2a_backend_ctx *) be->context;
+    Q2A_HIP(hipSetDevice(b->device));
+    Q2A_HIP(hipStreamSynchronize(b->stream));
+}
+bool dev_supports_op(ggml_backend_dev_t, const ggml_tensor * op) { return op_supported(op); }
+bool dev_supports_buft(ggml_backend_dev_t dev, ggml_backend_buffer_type_t t) {
+    return t->iface.get_name == buft_get_name && t->context == dev->context;
+}
+bool be_supports_op(ggml_backend_t, const ggml_tensor * op) { return op_supported(op); }
+bool be_supports_buft(ggml_backend_t be, ggml_backend_buffer_type_t t) {
+    return t->iface.get_name == buft_get_name && ((q2a_device_ctx *) t->context)->device == ((q2a_backend_ctx *) be->context)->device;
+}
+bool be_offload_op(ggml_backend_t, const ggml_tensor *) { return false; }
+
+const ggml_backend_i k_backend_iface = {
+    /* get_name                */ be_get_name,
+    /* free                    */ be_free,
+    /* get_default_buffer_type */ be_get_default_buft,
+    /* set_tensor_async        */ be_set_tensor_async,
+    /* get_tensor_async        */ be_get_tensor_async,
+    /* cpy_tensor_async        */ nullptr,
+    /* synchronize             */ be_synchronize,
+    /* graph_plan_create       */ nullptr,
+    /* graph_plan_free         */ nullptr,
+    /* graph_plan_update       */ nullptr,
+    /* graph_plan_compute      */ nullptr,
+    /* graph_compute           */ graph_compute,
+    /* supports_op             */ be_supports_op,
+    /* supports_buft           */ be_supports_buft,
+    /* offload_op              */ be_offload_op,
+    /* event_record            */ nullptr,
+    /* event_wait              */ nullptr,
+};
+
+// ---- device / registry --------------------------------------------------------------------------
+const char * dev_get_name(ggml_backend_dev_t d) { return ((q2a_device_ctx *) d->context)->name.c_str(); }
+const char * dev_get_desc(ggml_backend_dev_t d) { return ((q2a_device_ctx *) d->context)->desc.c_str(); }
+void dev_get_memory(ggml_backend_dev_t d, size_t * free, size_t * total) {
+    ggml_backend_q2a_get_device_memory(((q2a_device_ctx *) d->context)->device, free, total);
+}
+enum ggml_backend_dev_type dev_get_type(ggml_backend_dev_t) { return GGML_BACKEND_DEVICE_TYPE_GPU_FULL; }
+void dev_get_props(ggml_backend_dev_t d, ggml_backend_dev_props * p) {
+    p->name = dev_get_name(d);
+    p->description = dev_get_desc(d);
+    p->type = dev_get_type(d);
+    dev_get_memory(d, &p->memory_free, &p->memory_total);
+    p->caps = {/* async */ true, /* host_buffer */ false, /* events */ false};
+}
+ggml_backend_t dev_init_backend(ggml_backend_dev_t d, const char *) {
+    return ggml_backend_q2a_init(((q2a_device_ctx *) d->context)->device);
+}
+ggml_backend_buffer_type_t dev_get_buft(ggml_backend_dev_t d) { return &((q2a_device_ctx *) d->context)->buft; }
+bool dev_offload_op(ggml_backend_dev_t, const ggml_tensor *) { return false; }
+
+const ggml_backend_device_i k_device_iface = {
+    /* get_name             */ dev_get_name,
+    /* get_description      */ dev_get_desc,
+    /* get_memory           */ dev_get_memory,
+    /* get_type             */ dev_get_type,
+    /* get_props            */ dev_get_props,
+    /* init_backend         */ dev_init_backend,
+    /* get_buffer_type      */ dev_get_buft,
+    /* get_host_buffer_type */ nullptr,
+    /* buffer_from_host_ptr */ nullptr,
+    /* supports_op          */ dev_supports_op,
+    /* supports_buft        */ dev_supports_buft,
+    /* offload_op           */ dev_offload_op,
+    /* event_new            */ nullptr,
+    /* event_free           */ nullptr,
+    /* event_synchronize    */ nullptr,
+};
+
+const char * reg_get_name(ggml_backend_reg_t) { return GGML_Q2A_NAME; }
+size_t reg_get_device_count(ggml_backend_reg_t) { return reg_ctx()->devs.size(); }
+ggml_backend_dev_t reg_get_device(ggml_backend_reg_t, size_t i) {
+    q2a_reg_ctx * r = reg_ctx();
+    return i < r->devs.size() ? &r->devs[i]->dev : nullptr;
+}
+
+const ggml_backend_reg_i k_reg_iface = {
+    /* get_name         */ reg_get_name,
+    /* get_device_count */ reg_get_device_count,
+    /* get_device       */ reg_get_device,
+    /* get_proc_address */ nullptr,
+};
+
+ggml_backend_reg * the_reg() {
+    static ggml_backend_reg reg = {k_reg_iface, nullptr};
+    return &reg;
+}
+
+q2a_reg_ctx * reg_ctx() {
+    static q2a_reg_ctx * r = [] {
+        q2a_reg_ctx * c = new q2a_reg_ctx();
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) { (void) hipGetLastError(); n = 0; }
+        for (int i = 0; i < std::min(n, GGML_Q2A_MAX_DEVICES); ++i) {
+            q2a_device_ctx * d = new q2a_device_ctx();
+            d->device = i;
+            d->name = std::string(GGML_Q2A_NAME) + std::to_string(i);
+            hipDeviceProp_t prop;
+            d->desc = hipGetDeviceProperties(&prop, i) == hipSuccess ? std::string(prop.name) + " (" + prop.gcnArchName + ")" : "HIP device";
+            d->buft = {k_buft_iface, &d->dev, d};
+            d->dev = {k_device_iface, the_reg(), d};
+            c->devs.push_back(d);
+        }
+        return c;
+    }();
+    return r;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// public API (include/ggml-q2a.h)
+// ------------------------------------------------------------------------------------------------
+extern "C" {
+
+ggml_backend_t ggml_backend_q2a_init(int device) {
+    q2a_device_ctx * d = dev_ctx(device);
+    if (!d) {
+        Q2A_LOG_ERROR("ggml-q2a: invalid device %d\n", device);
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) return nullptr;
+    q2a_backend_ctx * b = new q2a_backend_ctx();
+    b->device = device;
+    b->name = d->name;
+    // a blocking stream: the buffers' synchronous copies on the null stream stay ordered with graph work
+    if (hipStreamCreate(&b->stream) != hipSuccess) {
+        delete b;
+        return nullptr;
+    }
+    return new ggml_backend{q2a_guid(), k_backend_iface, &d->dev, b};
+}
+
+bool ggml_backend_is_q2a(ggml_backend_t backend) {
+    return backend != nullptr && ggml_guid_matches(backend->guid, q2a_guid());
+}
+
+ggml_backend_buffer_type_t ggml_backend_q2a_buffer_type(int device) {
+    q2a_device_ctx * d = dev_ctx(device);
+    return d ? &d->buft : nullptr;
+}
+
+int ggml_backend_q2a_get_device_count(void) { return (int) reg_ctx()->devs.size(); }
+
+void ggml_backend_q2a_get_device_description(int device, char * description, size_t n) {
+    q2a_device_ctx * d = dev_ctx(device);
+    snprintf(description, n, "%s", d ? d->desc.c_str() : "");
+}
+
+void ggml_backend_q2a_get_device_memory(int device, size_t * free, size_t * total) {
+    *free = 0;
+    *total = 0;
+    if (hipSetDevice(device) != hipSuccess) return;
+    (void) hipMemGetInfo(free, total);
+}
+
+ggml_backend_reg_t ggml_backend_q2a_reg(void) {
+    (void) reg_ctx();
+    return the_reg();
+}
+
+void ggml_backend_q2a_get_stats(ggml_backend_t backend, ggml_backend_q2a_stats * stats) {
+    if (ggml_backend_is_q2a(backend) && stats) *stats = ((q2a_backend_ctx *) backend->context)->stats;
+}
+
+}  // extern "C"

@@ -332,6 +332,35 @@ int pack(const char * path, std::vector<uint8_t> & out) {
     return Q2A_OK;
 }
 
+}  // namespace
+
+// One weight matrix on its own (the ggml-backend plugin's MUL_MAT weights): same arrays as a blob matrix,
+// laid out in one allocation whose offsets go to off[A_W..A_GAMMA] (0 = absent).
+int q2a_pack_linear(const uint8_t * raw, int wtype, int N, int K, std::vector<uint8_t> & out, uint64_t off[6]) {
+    const int blk = blk_of(wtype);
+    if ((wtype != Q2A_TYPE_F16 && !blk) || (blk && K % blk) || N <= 0 || K <= 0) return Q2A_ERR_UNSUPPORTED;
+    uint64_t o = 0;
+    auto take = [&](uint64_t bytes) { const uint64_t r = o; o += (bytes + 255) & ~uint64_t(255); return r; };
+    for (int i = 0; i < A_COUNT; ++i) off[i] = 0;
+    off[A_W] = take((uint64_t) N * K * 2);
+    if (blk) off[A_DX] = take((uint64_t) N * (K / blk) * 4);
+    if (blk == 256) {
+        off[A_DMIN] = take((uint64_t) N * (K / 256) * 4);
+        off[A_WEXT] = take((uint64_t) N * (K / 256) * 16 * 2);
+        off[A_BETA] = take((uint64_t) N * (K / 256) * 4);
+        off[A_GAMMA] = take((uint64_t) N * (K / 256) * 4);
+    }
+    out.assign(o, 0);
+    const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t]() { expand_rows(raw, wtype, K, N, (int) ((int64_t) N * t / nt), (int) ((int64_t) N * (t + 1) / nt), out.data(), off, 0); });
+    for (auto & x : th) x.join();
+    return Q2A_OK;
+}
+
+namespace {
+
 __global__ void k_split_hilo(const float * x, q2a_half * hi, q2a_half * lo, int64_t n) {
     const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;

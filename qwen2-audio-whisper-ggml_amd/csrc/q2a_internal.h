@@ -126,6 +126,14 @@ struct q2a_quant_args {
 };
 hipError_t q2a_launch_quant_act(const q2a_quant_args & a, hipStream_t s);
 
+// One ggml weight matrix [N][K] (raw ggml rows, host memory; F16 / Q4_K / Q8_0 / Q4_0) packed into the GEMM's
+// operand layout: fp16 W' [N][K] plus the block-major scale arrays, at byte offsets off[0..5] = W, DX, DMIN, WEXT,
+// BETA, GAMMA of `out` (0 = absent). Used by the ggml-backend plugin for weights living in its buffers.
+#ifdef __cplusplus
+#include <vector>
+int q2a_pack_linear(const uint8_t * raw, int wtype, int N, int K, std::vector<uint8_t> & out, uint64_t off[6]);
+#endif
+
 // AvgPool1d(2,2) over time + final LayerNorm -> out [clips][T/2][D] f32
 struct q2a_pool_args {
     const float * X;     // [clips*T][D]

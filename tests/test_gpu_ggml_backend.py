@@ -1,0 +1,83 @@
+"""The reference's own whisper_full() on the Q2A ggml backend (lib/libggml-q2a.so, include/ggml-q2a.h).
+
+oracle/_ref/ggml_harness is src/qwen2-whisper.cpp + ggml compiled unmodified from the reference sources, with the
+GPU-backend branch of whisper_backend_init_gpu / whisper_default_buffer_type (qwen2-whisper.cpp:1217-1337) pointed
+at our backend (oracle/ggml_harness.cpp). The reference's loader puts the weights in our buffers, its graph builders
+and ggml_backend_sched hand the conv and encoder graphs to our graph_compute, and embd_enc is read back from our
+buffer. Outputs are compared with the reference's CPU outputs (tests/golden). No conv shim here: the graph's
+MUL_MAT(F32 im2col, F16 kernel), which no shipped ggml backend accepts, runs on the backend.
+"""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, rel_errors
+
+pytestmark = pytest.mark.gpu
+
+HARNESS = os.path.join(ROOT, "oracle", "_ref", "ggml_harness")
+
+
+@pytest.fixture(scope="module")
+def harness():
+    if not os.path.exists(HARNESS):
+        pytest.fail("oracle/_ref/ggml_harness missing: build it where /root/reference exists (make -C oracle)")
+    return HARNESS
+
+
+def run(harness, model, pcm, tmp_path, env_extra=None, reps=1):
+    pcm_path = tmp_path / "pcm.f32"
+    pcm.astype(np.float32).tofile(pcm_path)
+    out = tmp_path / "embd.f32"
+    env = dict(os.environ)
+    env.update(env_extra or {})
+    r = subprocess.run([harness, "encode", model, str(pcm_path), str(out), str(reps)], capture_output=True,
+                       text=True, timeout=600, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    emb = np.fromfile(out, dtype=np.float32).reshape(info["ne1"], info["ne0"])
+    return emb, info
+
+
+@pytest.mark.parametrize("wt", ["f16", "q4_k", "q8_0", "q4_0"])
+def test_reference_whisper_full_on_backend_tiny(harness, make_model, make_clip, golden, wt, tmp_path):
+    _, g = golden
+    emb, info = run(harness, make_model("tiny", wt), make_clip(0), tmp_path)
+    assert info["backend"] == "Q2A0" and info["embd_buffer"] == "Q2A0", info
+    # every weight GEMM on the fast path, attention fused, nothing left for the CPU
+    L = 2
+    assert info["mul_mat_fast"] == 6 * L and info["attn_fused"] == L and info["mul_mat_f32"] == 0, info
+    assert info["n_splits_encode"] == 1, info
+    if wt == "f16":
+        mx, l2 = rel_errors(emb, g["tiny_f16_c0"])
+        assert mx < 1e-3 and l2 < 1e-4, (mx, l2)
+    else:
+        mx, l2 = rel_errors(emb[g["rows_stride5"]], g[f"tiny_{wt}_c0_rows"])
+        assert l2 < 1e-3 and mx < 5e-3, (mx, l2)
+
+
+def test_backend_unfused_attention_path(harness, make_model, make_clip, golden, tmp_path):
+    """The generic per-node path (K.Q on the exact-f32 MFMA GEMM, SOFT_MAX with a double sum, V.P) also matches."""
+    _, g = golden
+    emb, info = run(harness, make_model("tiny", "f16"), make_clip(1), tmp_path, {"GGML_Q2A_NO_FUSED_ATTN": "1"})
+    assert info["attn_fused"] == 0 and info["mul_mat_f32"] == 2 * 2, info
+    mx, l2 = rel_errors(emb[g["rows_stride5"]], g["tiny_f16_c1_rows"])
+    assert mx < 1e-3 and l2 < 1e-4, (mx, l2)
+
+
+@pytest.mark.parametrize("wt", ["f16", "q4_k"])
+def test_reference_whisper_full_on_backend_full_size(harness, make_model, make_clip, golden, wt, tmp_path):
+    _, g = golden
+    emb, info = run(harness, make_model("full", wt), make_clip(0), tmp_path)
+    assert info["mul_mat_fast"] == 6 * 32 and info["attn_fused"] == 32, info
+    o = emb.reshape(-1)
+    mxs, l2s = rel_errors(o[g[f"full_{wt}_c0_idx"]], g[f"full_{wt}_c0_val"])
+    rn = np.linalg.norm(emb.astype(np.float64), axis=1)
+    rnerr = np.abs(rn - g[f"full_{wt}_c0_rownorm"]).max() / g[f"full_{wt}_c0_rownorm"].max()
+    if wt == "f16":
+        assert mxs < 1e-3 and l2s < 1e-3 and rnerr < 1e-4, (mxs, l2s, rnerr)
+    else:   # inherent activation re-quantization flips, as for the engine
+        assert l2s < 2e-2 and rnerr < 2e-3, (mxs, l2s, rnerr)

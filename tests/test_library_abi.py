@@ -50,3 +50,19 @@ def test_python_mirror_exports_match(libq2a):
     import q2a
     for n in q2a.EXPORTS:
         assert hasattr(libq2a, n), n
+
+
+def test_ggml_backend_plugin_exports(libq2a):
+    """lib/libggml-q2a.so (the ggml backend, include/ggml-q2a.h) defines every entry point its header declares and
+    leaves ggml's own functions to the application's ggml (undefined here, resolved at load time)."""
+    so = os.path.join(PKG, "lib", "libggml-q2a.so")
+    if not os.path.exists(so):
+        pytest.skip("built only where ggml's headers are present (GGML_DIR)")
+    src = open(os.path.join(ROOT, "include", "ggml-q2a.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = sorted(set(re.findall(r"\b(ggml_backend_q2a_\w+|ggml_backend_is_q2a)\s*\(", src)))
+    assert len(names) >= 7
+    defined = subprocess.check_output(["nm", "-D", "--defined-only", so], text=True).split()
+    assert not [n for n in names if n not in defined]
+    undefined = subprocess.check_output(["nm", "-D", "--undefined-only", so], text=True)
+    assert "ggml_backend_buffer_init" in undefined and "ggml_nbytes" in undefined
