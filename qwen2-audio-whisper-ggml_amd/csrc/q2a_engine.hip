@@ -90,11 +90,15 @@ bool plan(blob_header & h, const q2a_hparams & hp, int wtype) {
     h.magic = BLOB_MAGIC; h.version = BLOB_VERSION; h.hp = hp; h.wtype = wtype; h.blk = blk_of(wtype); h.n_bins = 201;
     const dims d = dims_of(hp);
     if (d.L > MAX_LAYERS) return false;
+    // all-F32 files: every fp16 operand is a [hi | .. ] split (SPLIT = 3 parts of K for the linears, conv1 taps of
+    // 3 mel parts, conv2 taps of 2 parts), see expand_rows / pack
+    const bool f32 = wtype == Q2A_TYPE_F32;
+    const uint64_t kx = f32 ? 3 : 1;
     uint64_t off = HEADER_BYTES;
     auto take = [&](uint64_t bytes) { const uint64_t o = off; off += (bytes + 255) & ~uint64_t(255); return o; };
-    h.goff[G_CONV1_W] = take((uint64_t) d.D * 6 * d.M * 2);
+    h.goff[G_CONV1_W] = take((uint64_t) d.D * 3 * (f32 ? 3 : 2) * d.M * 2);
     h.goff[G_CONV1_B] = take((uint64_t) d.D * 4);
-    h.goff[G_CONV2_W] = take((uint64_t) d.D * 3 * d.D * 2);
+    h.goff[G_CONV2_W] = take((uint64_t) d.D * 3 * (f32 ? 2 : 1) * d.D * 2);
     h.goff[G_CONV2_B] = take((uint64_t) d.D * 4);
     h.goff[G_PE] = take((uint64_t) d.T * d.D * 4);
     h.goff[G_LNP_W] = take((uint64_t) d.D * 4);
@@ -117,7 +121,7 @@ bool plan(blob_header & h, const q2a_hparams & hp, int wtype) {
             int N, K;
             mat_dims(d, w, N, K);
             uint64_t * a = lo + L_MAT0 + w * A_COUNT;
-            a[A_W] = take((uint64_t) N * K * 2);
+            a[A_W] = take((uint64_t) N * K * 2 * kx);
             if (h.blk) a[A_DX] = take((uint64_t) N * (K / h.blk) * 4);
             if (h.blk == 256) {
                 a[A_DMIN] = take((uint64_t) N * (K / 256) * 4);
@@ -151,6 +155,16 @@ void expand_rows(const uint8_t * src, int wtype, int K, int Ntot, int r0, int r1
         uint16_t * wr = W + (size_t) n * K;
         if (wtype == Q2A_TYPE_F16) {
             memcpy(wr, row, (size_t) K * 2);
+        } else if (wtype == Q2A_TYPE_F32) {
+            // [Wh | Wh | Wl] against activations [Ah | Al | Ah]: Ah.Wh + Al.Wh + Ah.Wl, F32-class products
+            const float * x = (const float *) row;
+            uint16_t * w3 = W + (size_t) n * 3 * K;
+            for (int k = 0; k < K; ++k) {
+                const uint16_t hi = q2a_fp32_to_fp16(x[k]);
+                w3[k] = hi;
+                w3[K + k] = hi;
+                w3[2 * K + k] = q2a_fp32_to_fp16(x[k] - q2a_fp16_to_fp32(hi));
+            }
         } else if (wtype == Q2A_TYPE_Q4_K) {
             // block-major scale arrays: [nb][Ntot] / [nb][Ntot][16] so a tile's block scales are contiguous
             const int nb = K / 256;
@@ -213,7 +227,6 @@ int pack(const char * path, std::vector<uint8_t> & out) {
     struct guard { q2a_model_file * m; ~guard() { q2a_model_file_free(m); } } gd{mf};
     const q2a_hparams & hp = mf->hp;
     const int wtype = mf->wtype;
-    if (wtype == Q2A_TYPE_F32) { set_err("all-F32 model files (ftype 0) are not supported on this path yet"); return Q2A_ERR_UNSUPPORTED; }
     const dims d = dims_of(hp);
     if (d.D % 128 || d.D != d.H * 64 || d.T % 2 || d.M % 4 || (blk_of(wtype) == 256 && d.D % 256)) {
         set_err("unsupported shapes: D=%d H=%d T=%d M=%d", d.D, d.H, d.T, d.M);
@@ -239,30 +252,51 @@ int pack(const char * path, std::vector<uint8_t> & out) {
     };
     auto cpy = [&](uint64_t off, const uint8_t * src, size_t n) { memcpy(blob + off, src, n); };
 
-    // conv1: [oc][ic][k] F16 -> [oc][k*2M + (0|M) + ic] (k-major, duplicated for the hi|lo operand halves)
-    const uint8_t * c1 = T("conv1.weight", Q2A_TYPE_F16, {3, d.M, d.D});
+    // conv kernels are F16 in every file but the all-F32 one (vtype, qwen2-whisper.cpp:1542-1543)
+    const bool f32 = wtype == Q2A_TYPE_F32;
+    const int ctype = f32 ? Q2A_TYPE_F32 : Q2A_TYPE_F16;
+    const uint8_t * c1 = T("conv1.weight", ctype, {3, d.M, d.D});
     const uint8_t * c1b = T("conv1.bias", Q2A_TYPE_F32, {1, d.D});
-    const uint8_t * c2 = T("conv2.weight", Q2A_TYPE_F16, {3, d.D, d.D});
+    const uint8_t * c2 = T("conv2.weight", ctype, {3, d.D, d.D});
     const uint8_t * c2b = T("conv2.bias", Q2A_TYPE_F32, {1, d.D});
     const uint8_t * pe = T("embed_positions.weight", Q2A_TYPE_F32, {d.D, d.T});
     const uint8_t * lnw = T("layer_norm.weight", Q2A_TYPE_F32, {d.D});
     const uint8_t * lnb = T("layer_norm.bias", Q2A_TYPE_F32, {d.D});
     if (!c1 || !c1b || !c2 || !c2b || !pe || !lnw || !lnb) return Q2A_ERR_FORMAT;
     {
-        const uint16_t * s = (const uint16_t *) c1;
+        // hi / lo fp16 halves of a conv kernel element (F16 kernels: the value itself, lo = 0)
+        auto hl = [&](const uint8_t * src, size_t i, uint16_t & hi, uint16_t & lo) {
+            if (!f32) { hi = ((const uint16_t *) src)[i]; lo = 0; return; }
+            const float x = ((const float *) src)[i];
+            hi = q2a_fp32_to_fp16(x);
+            lo = q2a_fp32_to_fp16(x - q2a_fp16_to_fp32(hi));
+        };
+        // conv1: [oc][ic][k] -> k-major taps against the mel operand rows: F16 [w | w] x [mel_h | mel_l];
+        // F32 [wh | wh | wl] x [mel_h | mel_l | mel_h]
+        const int P1 = f32 ? 3 : 2;
         uint16_t * w = (uint16_t *) (blob + h.goff[G_CONV1_W]);
         for (int oc = 0; oc < d.D; ++oc)
             for (int ic = 0; ic < d.M; ++ic)
                 for (int k = 0; k < 3; ++k) {
-                    const uint16_t v = s[((size_t) oc * d.M + ic) * 3 + k];
-                    w[(size_t) oc * 6 * d.M + k * 2 * d.M + ic] = v;
-                    w[(size_t) oc * 6 * d.M + k * 2 * d.M + d.M + ic] = v;
+                    uint16_t hi, lo;
+                    hl(c1, ((size_t) oc * d.M + ic) * 3 + k, hi, lo);
+                    uint16_t * t = w + (size_t) oc * 3 * P1 * d.M + (size_t) k * P1 * d.M + ic;
+                    t[0] = hi;
+                    t[d.M] = hi;
+                    if (f32) t[2 * d.M] = lo;
                 }
-        const uint16_t * s2 = (const uint16_t *) c2;
+        // conv2: k-major taps over three consecutive conv1 output rows: F16 [w]; F32 [wh | wl] x rows [y | y]
+        const int P2 = f32 ? 2 : 1;
         uint16_t * w2 = (uint16_t *) (blob + h.goff[G_CONV2_W]);
         for (int oc = 0; oc < d.D; ++oc)
             for (int ic = 0; ic < d.D; ++ic)
-                for (int k = 0; k < 3; ++k) w2[(size_t) oc * 3 * d.D + k * d.D + ic] = s2[((size_t) oc * d.D + ic) * 3 + k];
+                for (int k = 0; k < 3; ++k) {
+                    uint16_t hi, lo;
+                    hl(c2, ((size_t) oc * d.D + ic) * 3 + k, hi, lo);
+                    uint16_t * t = w2 + (size_t) oc * 3 * P2 * d.D + (size_t) k * P2 * d.D + ic;
+                    t[0] = hi;
+                    if (f32) t[d.D] = lo;
+                }
     }
     cpy(h.goff[G_CONV1_B], c1b, (size_t) d.D * 4);
     cpy(h.goff[G_CONV2_B], c2b, (size_t) d.D * 4);
@@ -385,6 +419,25 @@ __global__ void k_to_half(const float * x, q2a_half * y, int64_t n) {
     if (i < n) y[i] = (_Float16) x[i];
 }
 
+// F32-weight activation operand: x [M][K] f32 -> [hi | lo | hi] rows of 3K fp16
+__global__ void k_split3(const float * x, q2a_half * y, int K, int64_t n) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t m = i / K;
+    const int k = (int) (i - m * K);
+    const float v = x[i];
+    const _Float16 h = (_Float16) v;
+    q2a_half * o = y + m * 3 * K + k;
+    o[0] = h;
+    o[K] = (_Float16) (v - (float) h);
+    o[2 * K] = h;
+}
+
+hipError_t launch_split3(const float * x, q2a_half * y, int K, int64_t n, hipStream_t s) {
+    hipLaunchKernelGGL(k_split3, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, y, K, n);
+    return hipGetLastError();
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------------------------------------
@@ -396,6 +449,8 @@ struct q2a_engine {
     blob_header h;
     dims d;
     int wtype = 0, blk = 0;
+    bool f32 = false;        // all-F32 model file: fp16 hi/lo split operands, GEMM K tripled (kx = 3)
+    int kx = 1;
     uint8_t * blob = nullptr;
     bool own_blob = false;
     int64_t blob_size = 0;
@@ -461,6 +516,8 @@ int engine_adopt_header(q2a_engine * e) {
     e->d = dims_of(e->h.hp);
     e->wtype = e->h.wtype;
     e->blk = e->h.blk;
+    e->f32 = e->wtype == Q2A_TYPE_F32;
+    e->kx = e->f32 ? 3 : 1;
     e->TP = ((e->d.T + 63) / 64) * 64;
     return Q2A_OK;
 }
@@ -486,11 +543,11 @@ int reserve(q2a_engine * e, int B) {
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
     const size_t o_meta = take((size_t) B * 4 * 4);
     const size_t o_mel = take((size_t) B * d.M * d.TM * 4);
-    const size_t o_xc1 = take((size_t) B * (d.TM + 2) * 2 * d.M * 2);
-    const size_t o_y1 = take((size_t) B * (d.TM + 1) * d.D * 2);
+    const size_t o_xc1 = take((size_t) B * (d.TM + 2) * (e->f32 ? 3 : 2) * d.M * 2);
+    const size_t o_y1 = take((size_t) B * (d.TM + 1) * d.D * 2 * (e->f32 ? 2 : 1));
     const size_t o_X = take((size_t) BT * d.D * 4);
-    const size_t o_actD = take((size_t) BT * d.D * 2);
-    const size_t o_actF = take((size_t) BT * d.F * 2);
+    const size_t o_actD = take((size_t) BT * d.D * 2 * e->kx);
+    const size_t o_actF = take((size_t) BT * d.F * 2 * e->kx);
     const size_t o_qh = take((size_t) BT * d.D * 2);
     const size_t o_ql = take((size_t) BT * d.D * 2);
     const size_t o_kh = take((size_t) BT * d.D * 2);
@@ -506,6 +563,8 @@ int reserve(q2a_engine * e, int B) {
         o_aF = take((size_t) MP * (d.F / 256 + 1) * 16 * 2);
         o_att = take((size_t) BT * d.D * 4);
         o_hF = take((size_t) BT * d.F * 4);
+    } else if (e->f32) {
+        o_att = take((size_t) BT * d.D * 4);
     }
     void * ws = nullptr;
     if (hipMalloc(&ws, off) != hipSuccess) {
@@ -531,6 +590,8 @@ int reserve(q2a_engine * e, int B) {
         e->dyD = (float *) (b + o_dyD); e->dyF = (float *) (b + o_dyF);
         e->aextD = (q2a_half *) (b + o_aD); e->aextF = (q2a_half *) (b + o_aF);
         e->attF = (float *) (b + o_att); e->hF = (float *) (b + o_hF);
+    } else if (e->f32) {
+        e->attF = (float *) (b + o_att);
     }
     HIP_TRY(hipStreamSynchronize(e->stream));
     return Q2A_OK;
@@ -542,9 +603,9 @@ q2a_gemm_args gemm_base(const q2a_engine * e, int l, int which, const q2a_half *
     int N, K;
     mat_dims(e->d, which, N, K);
     const uint64_t * m = e->mat(l, which);
-    a.A = A; a.lda = K; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
-    a.W = (const q2a_half *) (e->blob + m[A_W]); a.ldw = K;
-    a.M = M; a.N = N; a.K = K;
+    a.A = A; a.lda = (int64_t) K * e->kx; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
+    a.W = (const q2a_half *) (e->blob + m[A_W]); a.ldw = (int64_t) K * e->kx;
+    a.M = M; a.N = N; a.K = K * e->kx;
     a.gelu_tab = e->g<const uint16_t *>(G_GELU);
     a.gelu_c = e->g<const uint16_t *>(G_GELU_C);
     a.T = e->d.T; a.D = e->d.D; a.H = e->d.H; a.TP = e->TP;
@@ -584,7 +645,7 @@ hipEvent_t prof_event(q2a_engine * e) {
         if ((e)->prof) { (void) hipEventRecord(r_.b, s); (e)->pending.push_back(r_); } \
     } while (0)
 
-int ln_mode(const q2a_engine * e) { return e->blk == 0 ? 0 : e->blk == 256 ? 1 : 2; }
+int ln_mode(const q2a_engine * e) { return e->f32 ? 3 : e->blk == 0 ? 0 : e->blk == 256 ? 1 : 2; }
 
 #define LAUNCH(x)                                                                     \
     do {                                                                              \
@@ -613,7 +674,10 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         q2a_attn_args at{e->qh, e->ql, e->kh, e->kl, e->vt, B, d.T, d.D, d.H, e->TP, nullptr, nullptr};
         if (mode == 0) at.outH = e->actD; else at.outF = e->attF;
         PLAUNCH(e, s, Q2A_PROF_ATTN, q2a_launch_attention(at, s));
-        if (mode) {
+        if (mode == 3) {
+            const int64_t n = (int64_t) M * d.D;
+            PLAUNCH(e, s, Q2A_PROF_QUANT, launch_split3(e->attF, e->actD, d.D, n, s));
+        } else if (mode) {
             q2a_quant_args qa{e->attF, nullptr, M, d.D, mode, e->actD, e->dyD, e->aextD, e->dy_ld};
             PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_quant_act(qa, s));
         }
@@ -629,8 +693,11 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
     {
         q2a_gemm_args a = gemm_base(e, l, 2, e->actD, M);
         a.bias = e->lv<const float *>(l, L_B1);
-        if (mode == 0) {
-            a.outH = e->actF; a.ldo = d.F; a.o_rpg = M; a.o_gstride = 0; a.o_off = 0;
+        if (mode == 0 || mode == 3) {
+            // F32 weights: the GELU output is exactly fp16 (LUT), so the fc2 operand is [h | 0 | h] (middle third
+            // stays zero from the workspace memset) against [W2h | W2h | W2l]
+            a.outH = e->actF; a.ldo = (int64_t) d.F * e->kx; a.o_rpg = M; a.o_gstride = 0; a.o_off = 0;
+            a.o_dup = mode == 3 ? 2 * d.F : 0;
             PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_H, 0, s));
         } else if (mode == 1 && q2a_gemm_wide_tiles(M, d.F, e->blk) &&
                    e->fuse_q8k == 1 && q2a_gemm_pipe8(a, e->blk)) {
@@ -666,16 +733,18 @@ int run_frontend(q2a_engine * e, const float * pcm, int64_t stride, int B, int m
     ma.pcm = pcm; ma.pcm_stride = stride; ma.n_samples = nsamp; ma.seek = seek; ma.n_clips = B;
     ma.n_mel = d.M; ma.n_bins = 201; ma.n_frames_win = d.TM; ma.max_frames = max_frames;
     ma.filters = e->g<const float *>(G_FILT); ma.tab = e->g<const float *>(G_TAB);
-    ma.mel = e->mel; ma.clip_max = cmax; ma.xc1 = e->xc1;
+    ma.mel = e->mel; ma.clip_max = cmax; ma.xc1 = e->xc1; ma.xc_parts = e->f32 ? 3 : 2;
     PLAUNCH(e, s, Q2A_PROF_MEL, q2a_launch_mel(ma, s));
-    {   // conv1: implicit GEMM, A row t = xc1 rows t..t+2 of its clip (768 halves), K = 6M
+    const int P1 = e->f32 ? 3 : 2, P2 = e->f32 ? 2 : 1;   // operand parts per mel row / per conv1 output row
+    {   // conv1: implicit GEMM, A row t = xc1 rows t..t+2 of its clip (3 x P1 x M halves), K = 3 P1 M
         q2a_gemm_args a;
         memset(&a, 0, sizeof(a));
-        a.A = e->xc1; a.lda = 2 * d.M; a.a_rpg = d.TM; a.a_gstride = d.TM + 2; a.a_step = 1;
-        a.W = e->g<const q2a_half *>(G_CONV1_W); a.ldw = 6 * d.M;
-        a.M = B * d.TM; a.N = d.D; a.K = 6 * d.M;
+        a.A = e->xc1; a.lda = P1 * d.M; a.a_rpg = d.TM; a.a_gstride = d.TM + 2; a.a_step = 1;
+        a.W = e->g<const q2a_half *>(G_CONV1_W); a.ldw = 3 * P1 * d.M;
+        a.M = B * d.TM; a.N = d.D; a.K = 3 * P1 * d.M;
         a.bias = e->g<const float *>(G_CONV1_B);
-        a.outH = e->y1; a.ldo = d.D; a.o_rpg = d.TM; a.o_gstride = d.TM + 1; a.o_off = 1;
+        a.outH = e->y1; a.ldo = (int64_t) P2 * d.D; a.o_rpg = d.TM; a.o_gstride = d.TM + 1; a.o_off = 1;
+        a.o_dup = e->f32 ? d.D : 0;
         a.gelu_tab = e->g<const uint16_t *>(G_GELU);
         a.gelu_c = e->g<const uint16_t *>(G_GELU_C);
         PLAUNCH(e, s, Q2A_PROF_CONV1, q2a_launch_gemm(a, Q2A_EPI_GELU_H, 0, s));
@@ -683,9 +752,9 @@ int run_frontend(q2a_engine * e, const float * pcm, int64_t stride, int B, int m
     {   // conv2 (stride 2): A row t = y1 rows 2t..2t+2 (inputs 2t-1..2t+1), K = 3D; + pe
         q2a_gemm_args a;
         memset(&a, 0, sizeof(a));
-        a.A = e->y1; a.lda = d.D; a.a_rpg = d.T; a.a_gstride = d.TM + 1; a.a_step = 2;
-        a.W = e->g<const q2a_half *>(G_CONV2_W); a.ldw = 3 * d.D;
-        a.M = B * d.T; a.N = d.D; a.K = 3 * d.D;
+        a.A = e->y1; a.lda = (int64_t) P2 * d.D; a.a_rpg = d.T; a.a_gstride = d.TM + 1; a.a_step = 2;
+        a.W = e->g<const q2a_half *>(G_CONV2_W); a.ldw = 3 * P2 * d.D;
+        a.M = B * d.T; a.N = d.D; a.K = 3 * P2 * d.D;
         a.bias = e->g<const float *>(G_CONV2_B);
         a.outF = e->X; a.ldo = d.D; a.pe = e->g<const float *>(G_PE); a.T = d.T;
         a.gelu_tab = e->g<const uint16_t *>(G_GELU);
@@ -914,7 +983,7 @@ int q2a_pcm_to_mel(q2a_engine * e, const float * pcm, int n_samples, float * mel
         ma.pcm = dpcm; ma.pcm_stride = n_samples; ma.n_samples = e->meta; ma.seek = e->meta + 1; ma.n_clips = 1;
         ma.n_mel = d.M; ma.n_bins = 201; ma.n_frames_win = d.TM; ma.max_frames = n_len;
         ma.filters = e->g<const float *>(G_FILT); ma.tab = e->g<const float *>(G_TAB);
-        ma.mel = e->mel; ma.clip_max = e->meta + 3; ma.xc1 = e->xc1;
+        ma.mel = e->mel; ma.clip_max = e->meta + 3; ma.xc1 = e->xc1; ma.xc_parts = e->f32 ? 3 : 2;
         if (q2a_launch_mel(ma, s) != hipSuccess) { rc = Q2A_ERR_HIP; break; }
         if (hipMemcpyAsync(chunk.data(), e->mel, chunk.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipMemcpyAsync(&cmax, e->meta + 3, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -978,6 +1047,10 @@ int q2a_test_linear(q2a_engine * e, int layer, int which, const float * x, int M
     if (mode == 0) {
         const int64_t n = (int64_t) M * K;
         hipLaunchKernelGGL(k_to_half, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, A, n);
+        LAUNCH(hipGetLastError());
+    } else if (mode == 3) {
+        const int64_t n = (int64_t) M * K;
+        hipLaunchKernelGGL(k_split3, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, A, K, n);
         LAUNCH(hipGetLastError());
     } else {
         q2a_quant_args qa{x, nullptr, M, K, mode, A, K == d.D ? e->dyD : e->dyF, K == d.D ? e->aextD : e->aextF, e->dy_ld};

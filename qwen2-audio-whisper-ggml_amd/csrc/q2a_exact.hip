@@ -142,17 +142,18 @@ __global__ __launch_bounds__(256) void k_mel_norm(const q2a_mel_args p) {
         tile[j][tt] = v;
     }
     __syncthreads();
-    const int nm = p.n_mel;
-    q2a_half * xc = p.xc1 + (int64_t) c * (p.n_frames_win + 2) * 2 * nm;
+    const int nm = p.n_mel, P = p.xc_parts;
+    q2a_half * xc = p.xc1 + (int64_t) c * (p.n_frames_win + 2) * P * nm;
     for (int e = threadIdx.x; e < nm * 64; e += 256) {
         const int tt = e / nm, j = e % nm;
         if (t0 + tt >= p.n_frames_win) continue;
         const float v = tile[j][tt];
         const _Float16 h = (_Float16) v;
         const _Float16 l = (_Float16) (v - (float) h);
-        q2a_half * row = xc + (int64_t) (t0 + tt + 1) * 2 * nm;
+        q2a_half * row = xc + (int64_t) (t0 + tt + 1) * P * nm;
         row[j] = h;
         row[nm + j] = l;
+        if (P == 3) row[2 * nm + j] = h;   // F32 kernel: [h | l | h] x [wh | wh | wl]
     }
 }
 
@@ -251,10 +252,19 @@ __global__ __launch_bounds__(256) void k_rownorm(const float * __restrict__ X, i
             y.z = (y.z * scale) * gg.z + bb.z;
             y.w = (y.w * scale) * gg.w + bb.w;
         }
-        q2a_half * o = outH + (int64_t) row * D + 4 * c;
+        q2a_half * o = outH + (int64_t) row * (MODE == 3 ? 3 * D : D) + 4 * c;
         const int m = row / nseg, seg = row - m * nseg;
         if (MODE == 0) {
             o[0] = (_Float16) y.x; o[1] = (_Float16) y.y; o[2] = (_Float16) y.z; o[3] = (_Float16) y.w;
+        } else if (MODE == 3) {
+            const float yy[4] = {y.x, y.y, y.z, y.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const _Float16 h = (_Float16) yy[e];
+                o[e] = h;
+                o[D + e] = (_Float16) (yy[e] - (float) h);
+                o[2 * D + e] = h;
+            }
         } else if (MODE == 1) {
             const int bf = seg * (D / 256) + u;
             quant_q8k_block(y, lane, o, dy + (int64_t) bf * ld + m, aext + ((int64_t) bf * ld + m) * 16);
@@ -352,6 +362,7 @@ hipError_t q2a_launch_layernorm(const q2a_ln_args & a, hipStream_t s) {
     if (a.mode == 2 && a.D % 32) return hipErrorInvalidValue;
     const dim3 grid((a.M + 3) / 4), blk(256);
     if (a.mode == 0) hipLaunchKernelGGL((k_rownorm<0, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
+    else if (a.mode == 3) hipLaunchKernelGGL((k_rownorm<3, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else if (a.mode == 1 && a.D == 1280 && !getenv("Q2A_QUANT_V1"))
         hipLaunchKernelGGL((k_rownorm<1, true, false, 5>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else if (a.mode == 1) hipLaunchKernelGGL((k_rownorm<1, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);

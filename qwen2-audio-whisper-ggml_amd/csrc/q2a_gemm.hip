@@ -715,6 +715,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                     if (EPI == Q2A_EPI_GELU_H) {
                         const int64_t row = (int64_t) (m / p.o_rpg) * p.o_gstride + (m % p.o_rpg) + p.o_off;
                         *(uint4 *) (p.outH + row * p.ldo + cbase + c8) = v;
+                        if (p.o_dup) *(uint4 *) (p.outH + row * p.ldo + cbase + c8 + p.o_dup) = v;
                     } else {
                         const int c = cbase - part * p.D + c8;
                         const uint4 lo = *(const uint4 *) ((const _Float16 *) wl + PR * (WC + 8) + rl * (WC + 8) + c8);

@@ -40,6 +40,7 @@ struct q2a_gemm_args {
     int64_t ldo;
     q2a_half * outH;
     int o_rpg, o_gstride, o_off;      // output row remap for outH: (m / o_rpg) * o_gstride + (m % o_rpg) + o_off
+    int o_dup;                        // Q2A_EPI_GELU_H: also store the row at column offset o_dup (0 = no copy)
     const float * pe;
     int T;                            // positions per clip
     q2a_half *qh, *ql, *kh, *kl, *vt;
@@ -92,7 +93,9 @@ struct q2a_mel_args {
     const float * tab;          // hann[400] | cos[400] | sin[400]
     float * mel;                // [clips][n_mel][n_frames_win] raw log10 values
     int32_t * clip_max;         // [clips] ordered-int encoding of the max over ALL frames
-    q2a_half * xc1;             // [clips][n_frames_win+2][2*n_mel] conv1 operand (hi|lo per row), rows 0/last = 0
+    q2a_half * xc1;             // [clips][n_frames_win+2][parts*n_mel] conv1 operand (hi|lo or hi|lo|hi per row),
+                                //   rows 0/last = 0
+    int xc_parts;               // 2 (F16 conv kernel) or 3 (F32 conv kernel, all-F32 model files)
 };
 hipError_t q2a_launch_mel(const q2a_mel_args & a, hipStream_t s);
 
@@ -100,6 +103,7 @@ hipError_t q2a_launch_mel(const q2a_mel_args & a, hipStream_t s);
 //   0: fp16 [M][D]                     (F16 weights)
 //   1: Q8_K as fp16 codes + dy[M][D/256] + aext (Q4_K weights)
 //   2: Q8_0 as fp16 codes + dy[M][D/32]  (Q8_0 / Q4_0 weights)
+//   3: fp16 split [hi | lo | hi] rows of 3D (F32 weights: exact-f32-class products against [Wh | Wh | Wl])
 struct q2a_ln_args {
     const float * X;
     int M, D;

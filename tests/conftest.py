@@ -45,6 +45,15 @@ def golden():
 
 
 @pytest.fixture(scope="session")
+def golden_f32():
+    """Reference outputs for all-F32 model files (tests/golden/make_golden_f32.py)."""
+    with open(os.path.join(GOLDEN_DIR, "golden_f32.json")) as f:
+        meta = json.load(f)
+    arrays = dict(np.load(os.path.join(GOLDEN_DIR, "golden_f32.npz"), allow_pickle=False))
+    return meta, arrays
+
+
+@pytest.fixture(scope="session")
 def workdir(tmp_path_factory):
     return str(tmp_path_factory.mktemp("q2a"))
 
@@ -59,6 +68,16 @@ def make_model(host_build, workdir, golden):
         key = (cfg, wt)
         if key in cache:
             return cache[key]
+        if wt == "f32":   # all-F32 file straight from the generator (ftype 0)
+            path = os.path.join(workdir, f"{cfg}-f32.bin")
+            if not os.path.exists(path):
+                subprocess.check_call([TOOL, "gen-model", path, cfg, "f32", "0x51A2", str(min(16, os.cpu_count() or 8))])
+            with open(os.path.join(GOLDEN_DIR, "golden_f32.json")) as f:
+                want = json.load(f)["models"].get(f"{cfg}-f32", {}).get("sha256")
+            if want is not None:
+                assert _sha(path) == want, f"generator drift for {cfg}-f32"
+            cache[key] = path
+            return path
         base = os.path.join(workdir, f"{cfg}-f16.bin")
         if not os.path.exists(base):
             subprocess.check_call([TOOL, "gen-model", base, cfg, "f16", "0x51A2", str(min(16, os.cpu_count() or 8))])
