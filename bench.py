@@ -181,7 +181,8 @@ def main():
     elapsed = time.perf_counter() - ts
     lib.q2a_profile_read(C.c_void_p(eng.h), prof_ms, prof_n, 11, 0)
     lib.q2a_profile_enable(C.c_void_p(eng.h), 0)
-    assert torch.isfinite(out).all().item(), "non-finite encoder output"
+    if not os.environ.get("Q2A_DIAG_BUILD"):   # diagnostic A/B libraries (diag/) compute garbage on purpose
+        assert torch.isfinite(out).all().item(), "non-finite encoder output"
 
     elapsed = qd.max_over_ranks(dist, elapsed, "cuda")
 

@@ -47,7 +47,17 @@ __device__ __forceinline__ float gelu_lut(float x, const uint16_t * tab) {
     return (float) gh;
 }
 
-// same lookup against the compact |x| <= 10 table staged in LDS
+// same lookup against the compact |x| <= 10 table staged in LDS, result as fp16 (it is fp16 by construction)
+__device__ __forceinline__ _Float16 gelu_lut_c16(float x, const uint16_t * lut) {
+    const _Float16 h = (_Float16) x;
+    uint16_t u;
+    __builtin_memcpy(&u, &h, 2);
+    const uint16_t g = lut[(u & 0x7FFF) + ((u & 0x8000) ? Q2A_GELU_C_HALF : 0)];
+    _Float16 gh;
+    __builtin_memcpy(&gh, &g, 2);
+    return x <= -10.0f ? (_Float16) 0.0f : x >= 10.0f ? h : gh;
+}
+
 __device__ __forceinline__ float gelu_lut_c(float x, const uint16_t * lut) {
     if (x <= -10.0f) return 0.0f;
     if (x >= 10.0f) return x;
@@ -108,6 +118,9 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     const int nk = p.K / BK;
     // image h of buffer b: h = 0 A_q0, 1 A_q1, 2 B_q0, 3 B_q1
     auto stage = [&](int b, int h, int kt) {
+#ifdef Q2A_DIAG_NO_GLDS
+        if (kt >= 2) return;   // timing diagnostic only (wrong results): main-loop operand loads skipped
+#endif
         const int k0 = kt * BK;
         char * dst = lds_raw + (b * 4 + h) * HT + wave * 8 * ROWB;
 #pragma unroll
@@ -185,21 +198,23 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #ifdef Q2A_DIAG_NO_RESCALE
         return;   // timing diagnostic only (wrong results)
 #endif
-        const uint32_t s_al = sb0 + ALPHA_OFF + (wm * 128 + (lane >> 4) * 4) * 4;
+        // C^T accumulators: lane holds columns n = 16j + 4(lane>>4) + r of row m = 16i + (lane&15), so alpha (per
+        // row) is one scalar per row block and beta / gamma (per column) one float4 per column block
+        const uint32_t s_al = sb0 + ALPHA_OFF + (wm * 128 + (lane & 15)) * 4;
         const uint32_t s_ae = sb0 + 5 * 1024 + (wm * 128 + (lane & 15)) * 32 + (lane >> 4) * 8;
-        const uint32_t s_cn = sb0 + 2048 + (wn * 64 + (lane & 15)) * 4;                      // beta | gamma at +1024
+        const uint32_t s_cn = sb0 + 2048 + (wn * 64 + (lane >> 4) * 4) * 4;                  // beta | gamma at +1024
         const uint32_t s_we = sb0 + 13 * 1024 + (wn * 64 + (lane & 15)) * 32 + (lane >> 4) * 8;
-        float bet[4], gam[4];
+        f4 bet[4], gam[4];
         half4 we[4];
-        f4 al[2];
+        float al[2];
         half4 ae[2];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(bet[j]) : "v"(s_cn), "i"(j * 64));
-            asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(gam[j]) : "v"(s_cn), "i"(1024 + j * 64));
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bet[j]) : "v"(s_cn), "i"(j * 64));
+            asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(gam[j]) : "v"(s_cn), "i"(1024 + j * 64));
             asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(we[j]) : "v"(s_we), "i"(j * 512));
         }
-        asm volatile("ds_read_b128 %0, %1" : "=v"(al[0]) : "v"(s_al));
+        asm volatile("ds_read_b32 %0, %1" : "=v"(al[0]) : "v"(s_al));
         asm volatile("ds_read_b64 %0, %1" : "=v"(ae[0]) : "v"(s_ae));
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bet[0]), "+v"(bet[1]), "+v"(bet[2]), "+v"(bet[3]), "+v"(gam[0]),
                      "+v"(gam[1]), "+v"(gam[2]), "+v"(gam[3]), "+v"(we[0]), "+v"(we[1]), "+v"(we[2]), "+v"(we[3]),
@@ -208,21 +223,21 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
         for (int i = 0; i < 8; ++i) {
             const int c = i & 1, n = c ^ 1;
             if (i + 1 < 8) {   // next row block's data in flight while this one is processed
-                asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(al[n]) : "v"(s_al), "i"((i + 1) * 64));
+                asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(al[n]) : "v"(s_al), "i"((i + 1) * 64));
                 asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(ae[n]) : "v"(s_ae), "i"((i + 1) * 512));
             }
             f4 s2v[4];   // the four min-term MFMAs first, their latency under the first rescale products
 #pragma unroll
-            for (int j = 0; j < 4; ++j) s2v[j] = __builtin_amdgcn_mfma_f32_16x16x16f16(ae[c], we[j], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            for (int j = 0; j < 4; ++j) s2v[j] = __builtin_amdgcn_mfma_f32_16x16x16f16(we[j], ae[c], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const f4 s2 = s2v[j];
-                // packed fp32 (v_pk_mul/v_pk_fma): two rows per instruction
-                const f2 bj = {bet[j], bet[j]}, gj = {gam[j], gam[j]};
+                // packed fp32 (v_pk_mul/v_pk_fma): two columns per instruction
+                const f2 al2 = {al[c], al[c]};
 #pragma unroll
                 for (int r = 0; r < 4; r += 2) {
                     const f2 a2 = {acc[i][j][r], acc[i][j][r + 1]};
-                    const f2 al2 = {al[c][r], al[c][r + 1]};
+                    const f2 bj = {bet[j][r], bet[j][r + 1]}, gj = {gam[j][r], gam[j][r + 1]};
                     const f2 s22 = {s2[r], s2[r + 1]};
                     const f2 res = a2 * (al2 * bj) - gj * s22;
                     acc[i][j][r] = res[0];
@@ -273,7 +288,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
                     acc[qm * 4 + i][qn * 2 + j] =
-                        __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i][s2], bf[qn][j][s2], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+                        __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[qn][j][s2], af[i][s2], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
     };
 #define Q2A_PB(N)                                               \
     asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory");       \
@@ -344,12 +359,12 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
         // acc is in units of the last block's scale: multiply by dy_last[m] * dx_last[n]
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const float dxn = *(lds_fp) (uintptr_t) (sb0 + 4096 + (wn * 64 + j * 16 + (lane & 15)) * 4);
+            const f4 dx4 = *(lds_f4p) (uintptr_t) (sb0 + 4096 + (wn * 64 + j * 16 + (lane >> 4) * 4) * 4);
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                const f4 yc = *(lds_f4p) (uintptr_t) (sb0 + 1024 + (wm * 128 + i * 16 + (lane >> 4) * 4) * 4);
+                const float yc = *(lds_fp) (uintptr_t) (sb0 + 1024 + (wm * 128 + i * 16 + (lane & 15)) * 4);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc[i][j][r] *= yc[r] * dxn;
+                for (int r = 0; r < 4; ++r) acc[i][j][r] *= yc * dx4[r];
             }
         }
     }
@@ -493,8 +508,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                     const half8 a = frag(ia, wm * (BM / WM) + i * 16 + (lane & 15), chunk);
     #pragma unroll
                     for (int j = 0; j < NJ; ++j) {
-                        if (BLK == 0) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[j], acc[i][j], 0, 0, 0);
-                        else blk[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[j], blk[i][j], 0, 0, 0);
+                        // W as the A operand: C^T tiles (lane = 4 consecutive columns of one row, see the epilogue)
+                        if (BLK == 0) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], a, acc[i][j], 0, 0, 0);
+                        else blk[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], a, blk[i][j], 0, 0, 0);
                     }
                 }
                 if (BLK) {
@@ -507,21 +523,21 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                         const float * s_dx = (const float *) (sb + (BLK == 256 ? BM * 36 : 2 * BM * 4)) + (BLK == 256 ? 0 : sub * BN);
                         const float * s_dm = (const float *) (sb + BM * 36 + BN * 4);
                         const q2a_half * s_we = (const q2a_half *) (sb + BM * 36 + BN * 8);
-                        float dx[NJ], dm[NJ];
+                        // C^T tiles: per-column scales as float4 (columns 16j + 4(lane>>4) + r), per-row as a scalar
+                        f4 dx[NJ], dm[NJ];
                         half4 we[NJ];
     #pragma unroll
                         for (int j = 0; j < NJ; ++j) {
-                            const int n = wn * (BN / WN) + j * 16 + (lane & 15);
-                            dx[j] = s_dx[n];
+                            const int n4 = wn * (BN / WN) + j * 16 + (lane >> 4) * 4;
+                            dx[j] = *(const f4 *) (s_dx + n4);
                             if (BLK == 256) {
-                                dm[j] = s_dm[n];
-                                we[j] = *(const half4 *) (s_we + n * 16 + (lane >> 4) * 4);
+                                dm[j] = *(const f4 *) (s_dm + n4);
+                                we[j] = *(const half4 *) (s_we + (wn * (BN / WN) + j * 16 + (lane & 15)) * 16 + (lane >> 4) * 4);
                             }
                         }
     #pragma unroll
                         for (int i = 0; i < MI; ++i) {
-                            const float4 dyv = *(const float4 *) (s_dy + wm * (BM / WM) + i * 16 + (lane >> 4) * 4);
-                            const float dy[4] = {dyv.x, dyv.y, dyv.z, dyv.w};
+                            const float dyi = s_dy[wm * (BM / WM) + i * 16 + (lane & 15)];
                             half4 ae;
                             if (BLK == 256) {
                                 // min term S2 = sum_j m_j * bsum32_j: one 16x16x16 MFMA per tile on (hi,lo)-split bsums
@@ -530,15 +546,15 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
     #pragma unroll
                             for (int j = 0; j < NJ; ++j) {
                                 if (BLK == 256) {
-                                    const f4 s2 = __builtin_amdgcn_mfma_f32_16x16x16f16(ae, we[j], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                                    const f4 s2 = __builtin_amdgcn_mfma_f32_16x16x16f16(we[j], ae, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     #pragma unroll
                                     for (int r = 0; r < 4; ++r) {
-                                        acc[i][j][r] += (dy[r] * dx[j]) * blk[i][j][r];
-                                        acc[i][j][r] -= (dy[r] * dm[j]) * s2[r];
+                                        acc[i][j][r] += (dyi * dx[j][r]) * blk[i][j][r];
+                                        acc[i][j][r] -= (dyi * dm[j][r]) * s2[r];
                                     }
                                 } else {
     #pragma unroll
-                                    for (int r = 0; r < 4; ++r) acc[i][j][r] += (dx[j] * dy[r]) * blk[i][j][r];
+                                    for (int r = 0; r < 4; ++r) acc[i][j][r] += (dx[j][r] * dyi) * blk[i][j][r];
                                 }
                                 blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
                             }
@@ -563,21 +579,23 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
         _Float16 * tl = (_Float16 *) (lds_raw + Q2A_GELU_C_BYTES);
         const uint16_t * lut = (const uint16_t *) lds_raw;
         const int kb = n0 / 256;
-        float bias_j[NJ];
+        f4 bias4[NJ];   // C^T tiles: columns 16j + 4(lane>>4) + r of row 16i + (lane&15)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) bias_j[j] = p.bias[n0 + wn * 64 + j * 16 + (lane & 15)];
+        for (int j = 0; j < NJ; ++j) bias4[j] = *(const f4 *) (p.bias + n0 + wn * 64 + j * 16 + (lane >> 4) * 4);
         __syncthreads();   // the staging overlaps the scale buffer the final multiply just read
 #pragma unroll
         for (int ps = 0; ps < 2; ++ps) {
             if (wm == ps) {
+                typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
 #pragma unroll
                 for (int i = 0; i < MI; ++i)
 #pragma unroll
-                    for (int j = 0; j < NJ; ++j)
+                    for (int j = 0; j < NJ; ++j) {
+                        h4_t hv;
 #pragma unroll
-                        for (int r = 0; r < 4; ++r)
-                            tl[(i * 16 + (lane >> 4) * 4 + r) * RSH + wn * 64 + j * 16 + (lane & 15)] =
-                                (_Float16) gelu_lut_c(acc[i][j][r] + bias_j[j], lut);
+                        for (int r = 0; r < 4; ++r) hv[r] = gelu_lut_c16(acc[i][j][r] + bias4[j][r], lut);
+                        *(h4_t *) (tl + (i * 16 + (lane & 15)) * RSH + wn * 64 + j * 16 + (lane >> 4) * 4) = hv;
+                    }
             }
             __syncthreads();
             // 16 lanes per row, four rows per wave-iteration, 16 rows per wave per pass
@@ -609,9 +627,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
         static_assert(PRQ * RS * 4 <= 2 * OPB, "Q8_K staging exceeds LDS");
         float * tl = (float *) lds_raw;
         const int kb = n0 / 256;
-        float bias_j[NJ];
+        f4 bias4[NJ];   // C^T tiles: columns 16j + 4(lane>>4) + r of row 16i + (lane&15)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) bias_j[j] = p.bias[n0 + wn * 64 + j * 16 + (lane & 15)];
+        for (int j = 0; j < NJ; ++j) bias4[j] = *(const f4 *) (p.bias + n0 + wn * 64 + j * 16 + (lane >> 4) * 4);
         __syncthreads();
 #pragma unroll
         for (int ps = 0; ps < BM / PRQ; ++ps) {
@@ -621,11 +639,12 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                     const int rw = wm * (BM / WM) + i * 16;          // tile row of this 16-row block
                     if (rw < ps * PRQ || rw >= (ps + 1) * PRQ) continue;
 #pragma unroll
-                    for (int j = 0; j < NJ; ++j)
+                    for (int j = 0; j < NJ; ++j) {
+                        f4 gv;
 #pragma unroll
-                        for (int r = 0; r < 4; ++r)
-                            tl[(rw - ps * PRQ + (lane >> 4) * 4 + r) * RS + wn * 64 + j * 16 + (lane & 15)] =
-                                gelu_lut(acc[i][j][r] + bias_j[j], p.gelu_tab);
+                        for (int r = 0; r < 4; ++r) gv[r] = gelu_lut(acc[i][j][r] + bias4[j][r], p.gelu_tab);
+                        *(f4 *) (tl + (rw - ps * PRQ + (lane & 15)) * RS + wn * 64 + j * 16 + (lane >> 4) * 4) = gv;
+                    }
                 }
             }
             __syncthreads();
@@ -644,106 +663,161 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
         return;
     }
 
-    // ---- epilogue. Per-element math (bias, scale, GELU) in registers, then an LDS transpose per wave so every
-    // global access is 16 B per lane along a row (8 B along t for V^T) instead of 2-4 B scattered stores
-    // (the 16x16 C layout gives each lane 4 rows of ONE column). The operand images are dead: reuse the LDS.
+#ifdef Q2A_DIAG_NO_EPI
+    {   // timing diagnostic only (wrong results): keep the accumulators live, skip the epilogue
+        float t = 0.f;
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+        if (t == 1234.5f && p.outF) p.outF[0] = t;
+        return;
+    }
+#endif
+    // ---- epilogue. The accumulators are C^T tiles (the MFMAs take W as A and the activations as B): lane holds the
+    // 4 CONSECUTIVE output columns n = 16j + 4q + r (q = lane>>4) of ONE row m = 16i + (lane&15), so results go to
+    // memory straight from registers: f32 outputs as one float4 per (i, j); fp16 outputs as 16 B after one lane
+    // exchange (xor 16) that pairs column chunks of tiles j and j+1. Only V^T (t-major) is transposed through LDS.
     constexpr int WR = BM / WM, WC = BN / WN;        // rows x cols owned by a wave (WC == 64)
-    static_assert(WC == 64, "epilogue assumes 64 columns per wave");
-    constexpr int PR = 32;                           // rows per pass (two 16-row tiles)
+    static_assert(WC == 64 && NJ == 4, "epilogue assumes 64 columns per wave");
     const int rbase = m0 + wm * WR, cbase = n0 + wn * WC;
-    float bias_j[NJ];
+    const int q = lane >> 4, l16 = lane & 15;
     int part = 0;
     if (EPI == Q2A_EPI_QKV) part = cbase / p.D;     // q | k | v: uniform per wave (D % 64 == 0)
+    f4 bias4[NJ];
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) bias_j[j] = (EPI == Q2A_EPI_STORE_F) ? 0.f : p.bias[cbase + j * 16 + (lane & 15)];
+    for (int j = 0; j < NJ; ++j)
+        bias4[j] = (EPI == Q2A_EPI_STORE_F) ? f4{0.f, 0.f, 0.f, 0.f} : *(const f4 *) (p.bias + cbase + j * 16 + 4 * q);
     const float vscale = (EPI == Q2A_EPI_QKV && part == 0) ? p.qscale : 1.0f;
-    constexpr int WREG = 2 * PR * (WC + 8) * 2;                  // per-wave staging bytes (max of the layouts)
-    static_assert(PR * (WC + 4) * 4 <= WREG && WREG == EPI_WREG, "epilogue staging layout");
-    char * wl = lds_raw + EPI_OFF + wave * WREG;
     const uint16_t * lut = (const uint16_t *) lds_raw;
-    __syncthreads();
-#pragma unroll
-    for (int ps = 0; ps < WR / PR; ++ps) {
-        // 1) registers -> LDS
-#pragma unroll
-        for (int ii = 0; ii < PR / 16; ++ii) {
-            const int i = ps * (PR / 16) + ii;
-#pragma unroll
-            for (int j = 0; j < NJ; ++j)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int rl = ii * 16 + (lane >> 4) * 4 + r, cl = j * 16 + (lane & 15);
-                    float v = acc[i][j][r];
-                    if (EPI != Q2A_EPI_STORE_F) v = v + bias_j[j];
-                    if (LUT_EPI) v = gelu_lut_c(v, lut);
-                    else if (EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_GELU_F || EPI == Q2A_EPI_CONV2) v = gelu_lut(v, p.gelu_tab);
-                    if (EPI == Q2A_EPI_QKV) v = v * vscale;   // ggml_scale after the bias add (:2054), exact 2^-3
-                    if (EPI == Q2A_EPI_QKV && part == 2) {
-                        ((_Float16 *) wl)[cl * (PR + 4) + rl] = (_Float16) v;           // V^T image [col][row]
-                    } else if (EPI == Q2A_EPI_QKV) {
-                        const _Float16 hi = (_Float16) v;
-                        ((_Float16 *) wl)[rl * (WC + 8) + cl] = hi;
-                        ((_Float16 *) wl)[PR * (WC + 8) + rl * (WC + 8) + cl] = (_Float16) (v - (float) hi);
-                    } else if (EPI == Q2A_EPI_GELU_H) {
-                        ((_Float16 *) wl)[rl * (WC + 8) + cl] = (_Float16) v;
-                    } else {
-                        ((float *) wl)[rl * (WC + 4) + cl] = v;
-                    }
-                }
-        }
+    // per-element value before the store: bias, GELU (LDS table when staged), Q scale
+    auto val = [&](int i, int j, int r) -> float {
+        float v = acc[i][j][r];
+        if (EPI != Q2A_EPI_STORE_F) v = v + bias4[j][r];
+        if (LUT_EPI && EPI != Q2A_EPI_GELU_H) v = gelu_lut_c(v, lut);
+        else if (!LUT_EPI && (EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_GELU_F || EPI == Q2A_EPI_CONV2)) v = gelu_lut(v, p.gelu_tab);
+        if (EPI == Q2A_EPI_QKV) v = v * vscale;   // ggml_scale after the bias add (:2054), exact 2^-3
+        return v;
+    };
+    typedef _Float16 h4v __attribute__((ext_vector_type(4)));
+    // 8 fp16 = this lane's 16-B piece of columns [32 jp + 16 (q&1) + 8 (q>>1), +8) from chunks (a: tile 2jp, b: 2jp+1)
+    auto pair16 = [&](h4v a, h4v b) -> uint4 {
+        uint2 ua, ub;
+        __builtin_memcpy(&ua, &a, 8);
+        __builtin_memcpy(&ub, &b, 8);
+        const bool odd = q & 1;
+        const uint2 send = odd ? ua : ub;
+        uint2 recv;
+        recv.x = __shfl_xor(send.x, 16, 64);
+        recv.y = __shfl_xor(send.y, 16, 64);
+        return odd ? make_uint4(recv.x, recv.y, ub.x, ub.y) : make_uint4(ua.x, ua.y, recv.x, recv.y);
+    };
+    const int pcol = 16 * (q & 1) + 8 * (q >> 1);    // column of this lane's 16-B piece within a 32-column pair
+    if (EPI == Q2A_EPI_QKV && part == 2) {
+        // V^T [clip][head][d][TP]: per 32-row pass, stage [col][row] fp16 in LDS, then 8 B (4 t) per lane
+        constexpr int PR = 32;
+        constexpr int WREG = 2 * PR * (WC + 8) * 2;
+        static_assert(WREG == EPI_WREG, "epilogue staging layout");
+        char * wl = lds_raw + EPI_OFF + wave * WREG;
         __syncthreads();
-        // 2) LDS -> global, 16 B per lane
-        const int prow = rbase + ps * PR;
-        if (EPI == Q2A_EPI_QKV && part == 2) {
-            // lane: column cl = lane, 4 consecutive rows per 8-B store; 8 row groups
+#pragma unroll
+        for (int ps = 0; ps < WR / PR; ++ps) {
+#pragma unroll
+            for (int ii = 0; ii < PR / 16; ++ii)
+#pragma unroll
+                for (int j = 0; j < NJ; ++j)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        ((_Float16 *) wl)[(j * 16 + 4 * q + r) * (PR + 4) + ii * 16 + l16] = (_Float16) val(ps * (PR / 16) + ii, j, r);
+            __syncthreads();
+            const int prow = rbase + ps * PR;
             const int c = cbase - 2 * p.D + lane, h = c >> 6, d = c & 63;
+            const int clip0 = prow / p.T, t0 = prow - clip0 * p.T;   // one division per pass (T >= PR)
 #pragma unroll
             for (int a = 0; a < PR / 4; ++a) {
                 const int m = prow + 4 * a;
                 if (m >= p.M) break;
-                const int clip = m / p.T, t = m - clip * p.T;
+                const bool wrap = t0 + 4 * a >= p.T;
+                const int clip = clip0 + (wrap ? 1 : 0), t = t0 + 4 * a - (wrap ? p.T : 0);
                 const uint2 v = *(const uint2 *) ((const _Float16 *) wl + lane * (PR + 4) + 4 * a);
                 *(uint2 *) (p.vt + (((int64_t) clip * p.H + h) * 64 + d) * p.TP + t) = v;
             }
-        } else if (EPI == Q2A_EPI_QKV || EPI == Q2A_EPI_GELU_H) {
+            __syncthreads();
+        }
+    } else if (EPI == Q2A_EPI_QKV || EPI == Q2A_EPI_GELU_H) {
+        // output row remap (conv1's padded per-clip rows): one division per wave, its rows span < o_rpg
+        const int oq = (EPI == Q2A_EPI_GELU_H && p.o_rpg < p.M) ? rbase / p.o_rpg : 0;
+        const int orr = EPI == Q2A_EPI_GELU_H ? rbase - oq * p.o_rpg : 0;
 #pragma unroll
-            for (int it = 0; it < PR / 8; ++it) {
-                const int rl = it * 8 + (lane >> 3), c8 = (lane & 7) * 8;
-                const int m = prow + rl;
-                if (m < p.M) {
-                    const uint4 v = *(const uint4 *) ((const _Float16 *) wl + rl * (WC + 8) + c8);
-                    if (EPI == Q2A_EPI_GELU_H) {
-                        const int64_t row = (int64_t) (m / p.o_rpg) * p.o_gstride + (m % p.o_rpg) + p.o_off;
-                        *(uint4 *) (p.outH + row * p.ldo + cbase + c8) = v;
-                        if (p.o_dup) *(uint4 *) (p.outH + row * p.ldo + cbase + c8 + p.o_dup) = v;
+        for (int i = 0; i < MI; ++i) {
+            const int ml = i * 16 + l16, m = rbase + ml;
+#pragma unroll
+            for (int jp = 0; jp < NJ / 2; ++jp) {
+                h4v ha, hb, la, lb;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if (EPI == Q2A_EPI_GELU_H && LUT_EPI) {
+                        ha[r] = gelu_lut_c16(acc[i][2 * jp][r] + bias4[2 * jp][r], lut);
+                        hb[r] = gelu_lut_c16(acc[i][2 * jp + 1][r] + bias4[2 * jp + 1][r], lut);
                     } else {
-                        const int c = cbase - part * p.D + c8;
-                        const uint4 lo = *(const uint4 *) ((const _Float16 *) wl + PR * (WC + 8) + rl * (WC + 8) + c8);
-                        *(uint4 *) ((part == 0 ? p.qh : p.kh) + (int64_t) m * p.D + c) = v;
-                        *(uint4 *) ((part == 0 ? p.ql : p.kl) + (int64_t) m * p.D + c) = lo;
+                        const float va = val(i, 2 * jp, r), vb = val(i, 2 * jp + 1, r);
+                        ha[r] = (_Float16) va;
+                        hb[r] = (_Float16) vb;
+                        if (EPI == Q2A_EPI_QKV) {
+                            la[r] = (_Float16) (va - (float) ha[r]);
+                            lb[r] = (_Float16) (vb - (float) hb[r]);
+                        }
                     }
                 }
-            }
-        } else {
-#pragma unroll
-            for (int it = 0; it < PR / 4; ++it) {
-                const int rl = it * 4 + (lane >> 4), c4 = (lane & 15) * 4;
-                const int m = prow + rl;
+                const uint4 hv = pair16(ha, hb);
+                uint4 lv;
+                if (EPI == Q2A_EPI_QKV) lv = pair16(la, lb);
                 if (m < p.M) {
-                    float4 v = *(const float4 *) ((const float *) wl + rl * (WC + 4) + c4);
-                    float * o = p.outF + (int64_t) m * p.ldo + cbase + c4;
-                    if (EPI == Q2A_EPI_RESID) {
-                        const float4 x = *(const float4 *) o;
-                        v.x = v.x + x.x; v.y = v.y + x.y; v.z = v.z + x.z; v.w = v.w + x.w;
-                    } else if (EPI == Q2A_EPI_CONV2) {
-                        const float4 pe = *(const float4 *) (p.pe + (int64_t) (m % p.T) * p.ldo + cbase + c4);
-                        v.x = pe.x + v.x; v.y = pe.y + v.y; v.z = pe.z + v.z; v.w = pe.w + v.w;
+                    const int col = 32 * jp + pcol;
+                    if (EPI == Q2A_EPI_GELU_H) {
+                        const bool wrap = orr + ml >= p.o_rpg;
+                        const int64_t row = (int64_t) (oq + (wrap ? 1 : 0)) * p.o_gstride + (orr + ml - (wrap ? p.o_rpg : 0)) + p.o_off;
+                        *(uint4 *) (p.outH + row * p.ldo + cbase + col) = hv;
+                        if (p.o_dup) *(uint4 *) (p.outH + row * p.ldo + cbase + col + p.o_dup) = hv;
+                    } else {
+                        const int64_t o = (int64_t) m * p.D + cbase - part * p.D + col;
+                        *(uint4 *) ((part == 0 ? p.qh : p.kh) + o) = hv;
+                        *(uint4 *) ((part == 0 ? p.ql : p.kl) + o) = lv;
                     }
-                    *(float4 *) o = v;
                 }
             }
         }
-        __syncthreads();
+    } else {
+        // f32 outputs: residual add (O-proj, fc2), GELU (+ positional rows for conv2), plain store
+        const int pq = EPI == Q2A_EPI_CONV2 ? rbase / p.T : 0;
+        const int pt0 = EPI == Q2A_EPI_CONV2 ? rbase - pq * p.T : 0;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int ml = i * 16 + l16, m = rbase + ml;
+            if (m >= p.M) continue;
+            float * orow = p.outF + (int64_t) m * p.ldo + cbase + 4 * q;
+            f4 add[NJ];
+            if (EPI == Q2A_EPI_RESID) {
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) add[j] = *(const f4 *) (orow + 16 * j);
+            } else if (EPI == Q2A_EPI_CONV2) {
+                const int tpos = pt0 + ml >= p.T ? pt0 + ml - p.T : pt0 + ml;
+                const float * perow = p.pe + (int64_t) tpos * p.ldo + cbase + 4 * q;
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) add[j] = *(const f4 *) (perow + 16 * j);
+            }
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                f4 v;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    v[r] = val(i, j, r);
+                    if (EPI == Q2A_EPI_RESID) v[r] = v[r] + add[j][r];        // (acc + bias) + x
+                    else if (EPI == Q2A_EPI_CONV2) v[r] = add[j][r] + v[r];   // pe + gelu(...)
+                }
+                *(f4 *) (orow + 16 * j) = v;
+            }
+        }
     }
 #undef LDS_STAGE
 }
