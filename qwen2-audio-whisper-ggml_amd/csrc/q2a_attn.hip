@@ -93,6 +93,10 @@ __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
     const int ntiles = (T + KT - 1) / KT;
     Q2A_LOAD_TILE(0);
     Q2A_STORE_TILE(0);
+    // the Q fragments must be complete before the loop (an asm "use" makes the waitcnt pass wait for them here):
+    // otherwise their loads stay pending at the loop header, merge with the next-tile prefetch and every
+    // iteration's QK^T MFMAs wait on that prefetch
+    asm volatile("" :: "v"(qh[0]), "v"(qh[1]), "v"(qh[2]), "v"(qh[3]), "v"(ql[0]), "v"(ql[1]), "v"(ql[2]), "v"(ql[3]));
     __syncthreads();
 
     for (int t = 0; t < ntiles; ++t) {
