@@ -33,9 +33,15 @@ constexpr float L2E = 1.4426950408889634f;   // exp(x) = exp2(x * log2 e)
 __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
     __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int h = blockIdx.y, clip = blockIdx.z;
     const int T = p.T, D = p.D;
-    const int q0 = blockIdx.x * 128 + wave * 32;
+    // XCD-contiguous work order: workgroup L is dispatched to XCD L % 8, so work item w = (L % 8)·(total/8) + L/8
+    // puts the q-tiles of one (clip, head) on ONE XCD at about the same time and its K/V are fetched into that
+    // L2 once instead of into up to eight of them (bijective when total % 8 == 0, identity otherwise)
+    const int nq = (T + 127) / 128, total = (int) gridDim.x;
+    const int L = (int) blockIdx.x;
+    const int w = (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);
+    const int qt = w % nq, h = (w / nq) % p.H, clip = w / (nq * p.H);
+    const int q0 = qt * 128 + wave * 32;
     const int64_t rowbase = (int64_t) clip * T;
     const int hi = lane >> 5, col = lane & 31;
 
@@ -202,7 +208,7 @@ __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
 
 hipError_t q2a_launch_attention(const q2a_attn_args & a, hipStream_t s) {
     if (a.D != a.H * 64 || a.TP < ((a.T + KT - 1) / KT) * KT) return hipErrorInvalidValue;
-    dim3 grid((a.T + 127) / 128, a.H, a.n_clips);
+    dim3 grid(((a.T + 127) / 128) * a.H * a.n_clips);
     hipLaunchKernelGGL(k_attn, grid, dim3(256), 0, s, a);
     return hipGetLastError();
 }
