@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Benchmark of the MI355X encoder hot path (BASELINE.json metric: encoder audio-frames/s on 30 s clips).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config {q4k64,f16x1,f16x64,q80x64}]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config {q4k64,f16x1,f16x64,q80x64,q80bf16x64}]
 
 A "step" = one pass of the hot path (PCM -> log-mel -> conv -> 32 blocks -> pool+LN) over one batch of
 synthetic 30 s / 16 kHz clips per GPU, PCM already resident in HBM when the timed region starts.
@@ -35,6 +35,9 @@ CONFIGS = {
     "f16x1": ("f16", 1, "configs[1]: single 30 s synthetic 16 kHz clip, fp16 weights, 1xMI355X per rank"),
     "f16x64": ("f16", 64, "batch=64 30 s clips, fp16 weights (F16 path at the configs[2] batch)"),
     "q80x64": ("q8_0", 64, "batch=64 30 s clips, Q8_0 weights (exact Q8_0 x Q8_0 contract)"),
+    # configs[4] per rank: Q8_0 file, weights dequantized to bf16, bf16 inter-op activations (Q2A_ACT_BF16)
+    "q80bf16x64": ("q8_0", 64, "configs[4] per rank: batch=64 30 s clips (512 over 8 GPUs), Q8_0 weights + bf16 "
+                               "activations (Q2A_ACT_BF16: bf16-dequantized weights, bf16 MFMA, fp32 accumulation)"),
 }
 T_MEL = 3000              # mel frames per 30 s clip (10 ms hop) -> the metric's "audio frame"
 N_SAMPLES = 480000
@@ -136,7 +139,7 @@ def main():
     blob_host = None
     if rank == 0:
         model_path = make_model(wt, args.workdir, threads)
-        blob_host = q2a.pack_model(model_path)
+        blob_host = q2a.pack_model(model_path, q2a.ACT_BF16 if "bf16" in args.config else q2a.ACT_REFERENCE)
     t_bcast = 0.0
     if dist is not None:
         dist.barrier()
@@ -243,7 +246,8 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": {"q4_k": "q4_k x q8_k integer dots on fp16 MFMA (fp32 acc)", "f16": "fp16 MFMA (fp32 acc)",
+        "dtype": "bf16 MFMA (fp32 acc), q8_0 weights dequantized to bf16, bf16 activations" if "bf16" in args.config else
+                 {"q4_k": "q4_k x q8_k integer dots on fp16 MFMA (fp32 acc)", "f16": "fp16 MFMA (fp32 acc)",
                   "q8_0": "q8_0 x q8_0 integer dots on fp16 MFMA (fp32 acc)"}[wt],
         "data": "synthetic (deterministic 30 s / 16 kHz clips; random-init weights at Qwen2-Audio encoder shapes)",
         "config": {"workload": workload, "model": "qwen2-audio-encoder L32 D1280 H20 F5120 (synthetic weights)",

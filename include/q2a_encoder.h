@@ -48,12 +48,27 @@ typedef struct {
     int32_t device;
     int64_t weight_bytes;   /* device bytes of the packed weight blob */
     int64_t workspace_bytes;
+    int32_t act;            /* Q2A_ACT_REFERENCE or Q2A_ACT_BF16 (from the blob) */
+    int32_t reserved;
 } q2a_info;
 
 const char * q2a_last_error(void);
 
 /* Load a reference-format ggml model file (models/convert-pt-to-ggml.py layout) onto HIP device `device`. */
 q2a_engine * q2a_open(const char * model_path, int device);
+
+/* Activation contract of an engine (q2a_open_ex / q2a_pack_model_ex):
+ *   Q2A_ACT_REFERENCE  the reference's own: activations converted per ggml's vec_dot_type before every weight
+ *                      GEMM (fp16 / Q8_K / Q8_0, or the exact fp16 hi/lo split for F32 files), F32-class attention
+ *   Q2A_ACT_BF16       mixed precision (BASELINE configs[4]): linear weights dequantized (ggml dequantize_row_*) to
+ *                      bf16, inter-op activations (LN outputs, Q/K/V, attention probabilities and output, GELU
+ *                      output) in bf16, bf16 MFMA with f32 accumulation; the residual stream, LN statistics,
+ *                      softmax and the conv front end stay as in the reference contract. A different numerical
+ *                      contract from the reference CPU path: its error is reported separately. */
+#define Q2A_ACT_REFERENCE 0
+#define Q2A_ACT_BF16 1
+q2a_engine * q2a_open_ex(const char * model_path, int device, int act);
+int64_t q2a_pack_model_ex(const char * model_path, int act, void ** host_blob);
 
 /* Multi-GPU: pack the model into its device layout on the host (rank 0), move the bytes to every rank's device
  * (e.g. one RCCL broadcast over xGMI), then open an engine on the device copy. The blob is self-describing. */

@@ -21,6 +21,19 @@ namespace {
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef float f16v __attribute__((ext_vector_type(16)));
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+
+// 32x32x16 MFMA on fp16 operands, or on the same bits read as bf16 (bf16-activation mode)
+template <bool BF>
+__device__ __forceinline__ f16v mma32(half8 a, half8 b, f16v c) {
+    if constexpr (BF) return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf8, a), __builtin_bit_cast(bf8, b), c, 0, 0, 0);
+    else return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+template <bool BF>
+__device__ __forceinline__ _Float16 to16(float v) {
+    if constexpr (BF) return __builtin_bit_cast(_Float16, (__bf16) v);
+    else return (_Float16) v;
+}
 
 constexpr int KT = 64;            // keys per LDS tile
 constexpr int KROW = 144;         // bytes per K image row (64 halves + 16 B pad)
@@ -30,6 +43,8 @@ constexpr int VIMG = 64 * VROW;   // 8704
 constexpr int STAGE = 2 * KIMG + VIMG;
 constexpr float L2E = 1.4426950408889634f;   // exp(x) = exp2(x * log2 e)
 
+// BF: bf16-activation mode (Q, K, V^T, P and the output in bf16; S = K.Q^T is one MFMA per 16-deep step)
+template <bool BF>
 __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
     __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -54,7 +69,7 @@ __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
             qh[s] = *(const half8 *) (sh + 16 * s);
-            ql[s] = *(const half8 *) (sl + 16 * s);
+            ql[s] = BF ? qh[s] : *(const half8 *) (sl + 16 * s);
         }
     }
 
@@ -68,8 +83,10 @@ __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
         const int k0_ = min(kb0_ + (c0_ >> 3), T - 1), k1_ = min(kb0_ + (c1_ >> 3), T - 1);       \
         rk_h0 = *(const uint4 *) (p.kh + (rowbase + k0_) * D + h * 64 + (c0_ & 7) * 8);              \
         rk_h1 = *(const uint4 *) (p.kh + (rowbase + k1_) * D + h * 64 + (c1_ & 7) * 8);              \
-        rk_l0 = *(const uint4 *) (p.kl + (rowbase + k0_) * D + h * 64 + (c0_ & 7) * 8);              \
-        rk_l1 = *(const uint4 *) (p.kl + (rowbase + k1_) * D + h * 64 + (c1_ & 7) * 8);              \
+        if (!BF) {                                                                                  \
+            rk_l0 = *(const uint4 *) (p.kl + (rowbase + k0_) * D + h * 64 + (c0_ & 7) * 8);          \
+            rk_l1 = *(const uint4 *) (p.kl + (rowbase + k1_) * D + h * 64 + (c1_ & 7) * 8);          \
+        }                                                                                           \
         rv0 = *(const uint4 *) (vt_base + (int64_t) (c0_ >> 3) * p.TP + kb0_ + (c0_ & 7) * 8);      \
         rv1 = *(const uint4 *) (vt_base + (int64_t) (c1_ >> 3) * p.TP + kb0_ + (c1_ & 7) * 8);      \
     } while (0)
@@ -77,7 +94,7 @@ __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
     do {                                                                                            \
         const int r_ = (c_) >> 3, ch_ = (c_) & 7;                                                   \
         *(uint4 *) ((st_) + r_ * KROW + ch_ * 16) = (kh_);                                          \
-        *(uint4 *) ((st_) + KIMG + r_ * KROW + ch_ * 16) = (kl_);                                   \
+        if (!BF) *(uint4 *) ((st_) + KIMG + r_ * KROW + ch_ * 16) = (kl_);                          \
         uint2 * vv_ = (uint2 *) ((st_) + 2 * KIMG + r_ * VROW + ch_ * 16);                          \
         vv_[0] = make_uint2((v_).x, (v_).y);                                                        \
         vv_[1] = make_uint2((v_).z, (v_).w);                                                        \
@@ -122,10 +139,12 @@ __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
             for (int st = 0; st < 4; ++st) {
                 const int off = krow * KROW + (2 * st + hi) * 16;
                 const half8 ah = *(const half8 *) (kh_img + off);
-                const half8 al = *(const half8 *) (kl_img + off);
-                sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, qh[st], sc[kb], 0, 0, 0);
-                sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, qh[st], sc[kb], 0, 0, 0);
-                sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, ql[st], sc[kb], 0, 0, 0);
+                sc[kb] = mma32<BF>(ah, qh[st], sc[kb]);
+                if (!BF) {
+                    const half8 al = *(const half8 *) (kl_img + off);
+                    sc[kb] = mma32<BF>(al, qh[st], sc[kb]);
+                    sc[kb] = mma32<BF>(ah, ql[st], sc[kb]);
+                }
             }
         }
         if (t == ntiles - 1) {   // keys >= T exist only in the last tile (row of reg r = (r&3) + 8(r>>2) + 4hi)
@@ -152,7 +171,7 @@ __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
             for (int r = 0; r < 16; ++r) {
                 const float pv = __builtin_amdgcn_exp2f(fmaf(sc[kb][r], L2E, nm));
                 ls += pv;
-                pf[kb][r >> 3][r & 7] = (_Float16) pv;
+                pf[kb][r >> 3][r & 7] = to16<BF>(pv);
             }
         l_run = l_run * alpha + ls;
         m_run = m_new;
@@ -174,7 +193,7 @@ __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
                     const half4 v0 = *(const half4 *) (vrow + kbyte);
                     const half4 v1 = *(const half4 *) (vrow + kbyte + 16);
                     const half8 va = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-                    o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(va, pf[kb][sp], o[dt], 0, 0, 0);
+                    o[dt] = mma32<BF>(va, pf[kb][sp], o[dt]);
                 }
             }
         // buffer cur^1 was last read in iteration t-1, before the barrier that ended it
@@ -195,7 +214,7 @@ __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
                 const float v0 = o[dt][4 * g + 0] * inv, v1 = o[dt][4 * g + 1] * inv;
                 const float v2 = o[dt][4 * g + 2] * inv, v3 = o[dt][4 * g + 3] * inv;
                 if (p.outH) {
-                    const half4 hv = {(_Float16) v0, (_Float16) v1, (_Float16) v2, (_Float16) v3};
+                    const half4 hv = {to16<BF>(v0), to16<BF>(v1), to16<BF>(v2), to16<BF>(v3)};
                     *(half4 *) (p.outH + orow + d) = hv;
                 } else {
                     *(float4 *) (p.outF + orow + d) = make_float4(v0, v1, v2, v3);
@@ -209,6 +228,11 @@ __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
 hipError_t q2a_launch_attention(const q2a_attn_args & a, hipStream_t s) {
     if (a.D != a.H * 64 || a.TP < ((a.T + KT - 1) / KT) * KT) return hipErrorInvalidValue;
     dim3 grid(((a.T + 127) / 128) * a.H * a.n_clips);
-    hipLaunchKernelGGL(k_attn, grid, dim3(256), 0, s, a);
+    if (a.bf16) {
+        if (!a.outH) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_attn<true>, grid, dim3(256), 0, s, a);
+    } else {
+        hipLaunchKernelGGL(k_attn<false>, grid, dim3(256), 0, s, a);
+    }
     return hipGetLastError();
 }

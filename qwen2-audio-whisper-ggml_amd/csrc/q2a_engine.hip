@@ -59,7 +59,7 @@ enum { L_BQKV, L_BO, L_B1, L_B2, L_LN1W, L_LN1B, L_LN2W, L_LN2B, L_MAT0, L_COUNT
 struct blob_header {
     uint32_t magic, version;
     q2a_hparams hp;
-    int32_t wtype, blk, n_bins, reserved;
+    int32_t wtype, blk, n_bins, act;   // act: Q2A_ACT_REFERENCE (0) or Q2A_ACT_BF16 (1)
     uint64_t total;
     uint64_t goff[G_COUNT];
     uint64_t loff[MAX_LAYERS][L_COUNT];
@@ -85,15 +85,17 @@ void mat_dims(const dims & d, int which, int & N, int & K) {
 }
 int blk_of(int wtype) { return wtype == Q2A_TYPE_Q4_K ? 256 : (wtype == Q2A_TYPE_Q8_0 || wtype == Q2A_TYPE_Q4_0) ? 32 : 0; }
 
-bool plan(blob_header & h, const q2a_hparams & hp, int wtype) {
+bool plan(blob_header & h, const q2a_hparams & hp, int wtype, int act) {
     memset(&h, 0, sizeof(h));
-    h.magic = BLOB_MAGIC; h.version = BLOB_VERSION; h.hp = hp; h.wtype = wtype; h.blk = blk_of(wtype); h.n_bins = 201;
+    // bf16-activation mode: every linear weight dequantized to bf16 [N][K] (no block scales, no splits)
+    h.magic = BLOB_MAGIC; h.version = BLOB_VERSION; h.hp = hp; h.wtype = wtype; h.blk = act ? 0 : blk_of(wtype); h.n_bins = 201;
+    h.act = act;
     const dims d = dims_of(hp);
     if (d.L > MAX_LAYERS) return false;
     // all-F32 files: every fp16 operand is a [hi | .. ] split (SPLIT = 3 parts of K for the linears, conv1 taps of
     // 3 mel parts, conv2 taps of 2 parts), see expand_rows / pack
     const bool f32 = wtype == Q2A_TYPE_F32;
-    const uint64_t kx = f32 ? 3 : 1;
+    const uint64_t kx = f32 && !act ? 3 : 1;
     uint64_t off = HEADER_BYTES;
     auto take = [&](uint64_t bytes) { const uint64_t o = off; off += (bytes + 255) & ~uint64_t(255); return o; };
     h.goff[G_CONV1_W] = take((uint64_t) d.D * 3 * (f32 ? 3 : 2) * d.M * 2);
@@ -146,14 +148,60 @@ inline void scale_min_k4(int j, const uint8_t * q, uint8_t * dd, uint8_t * mm) {
 // Expand rows [r0, r1) of a ggml weight matrix into the blob arrays (rows offset by dst_row0).
 // F16: copied. Q4_K: W' = sc_j * q (exact small integers), DX = d, DMIN = dmin, WEXT = (64 m_j, m_j).
 // Q8_0: W' = q, DX = d. Q4_0: W' = q - 8, DX = d.
-void expand_rows(const uint8_t * src, int wtype, int K, int Ntot, int r0, int r1, uint8_t * blob, const uint64_t * a, int dst_row0) {
+// one ggml row -> f32 values, as ggml's dequantize_row_* computes them (ggml-quants.c: q8_0 :1734, q4_0 :1694,
+// q4_K :2555-2577 with d1 = d*sc, m1 = dmin*m, y = d1*q - m1)
+void dequant_row(const uint8_t * row, int wtype, int K, float * y) {
+    if (wtype == Q2A_TYPE_F32) { memcpy(y, row, (size_t) K * 4); return; }
+    if (wtype == Q2A_TYPE_F16) { for (int k = 0; k < K; ++k) y[k] = q2a_fp16_to_fp32(((const uint16_t *) row)[k]); return; }
+    if (wtype == Q2A_TYPE_Q8_0) {
+        for (int b = 0; b < K / 32; ++b) {
+            const q2a_block_q8_0 * x = (const q2a_block_q8_0 *) row + b;
+            const float d = q2a_fp16_to_fp32(x->d);
+            for (int l = 0; l < 32; ++l) y[b * 32 + l] = x->qs[l] * d;
+        }
+    } else if (wtype == Q2A_TYPE_Q4_0) {
+        for (int b = 0; b < K / 32; ++b) {
+            const q2a_block_q4_0 * x = (const q2a_block_q4_0 *) row + b;
+            const float d = q2a_fp16_to_fp32(x->d);
+            for (int l = 0; l < 16; ++l) {
+                y[b * 32 + l] = ((x->qs[l] & 0xF) - 8) * d;
+                y[b * 32 + 16 + l] = ((x->qs[l] >> 4) - 8) * d;
+            }
+        }
+    } else if (wtype == Q2A_TYPE_Q4_K) {
+        for (int b = 0; b < K / 256; ++b) {
+            const q2a_block_q4_K * x = (const q2a_block_q4_K *) row + b;
+            const float d = q2a_fp16_to_fp32(x->d), dmin = q2a_fp16_to_fp32(x->dmin);
+            for (int j = 0; j < 8; ++j) {
+                uint8_t sc, m;
+                scale_min_k4(j, x->scales, &sc, &m);
+                const float d1 = d * sc, m1 = dmin * m;
+                const uint8_t * q = x->qs + 32 * (j / 2);
+                for (int l = 0; l < 32; ++l) y[b * 256 + 32 * j + l] = d1 * ((j & 1) ? (q[l] >> 4) : (q[l] & 0xF)) - m1;
+            }
+        }
+    }
+}
+
+uint16_t f32_to_bf16(float f) {   // round to nearest even (finite inputs)
+    uint32_t u;
+    memcpy(&u, &f, 4);
+    return (uint16_t) ((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+
+void expand_rows(const uint8_t * src, int wtype, int K, int Ntot, int r0, int r1, uint8_t * blob, const uint64_t * a, int dst_row0,
+                 int act = 0) {
     uint16_t * W = (uint16_t *) (blob + a[A_W]);
     const size_t rs = q2a_row_size(wtype, K);
+    std::vector<float> tmp(act ? K : 0);
     for (int r = r0; r < r1; ++r) {
         const uint8_t * row = src + (size_t) r * rs;
         const int n = dst_row0 + r;
         uint16_t * wr = W + (size_t) n * K;
-        if (wtype == Q2A_TYPE_F16) {
+        if (act) {   // bf16-activation mode: dequantized weight, RNE to bf16
+            dequant_row(row, wtype, K, tmp.data());
+            for (int k = 0; k < K; ++k) wr[k] = f32_to_bf16(tmp[k]);
+        } else if (wtype == Q2A_TYPE_F16) {
             memcpy(wr, row, (size_t) K * 2);
         } else if (wtype == Q2A_TYPE_F32) {
             // [Wh | Wh | Wl] against activations [Ah | Al | Ah]: Ah.Wh + Al.Wh + Ah.Wl, F32-class products
@@ -220,7 +268,7 @@ void expand_rows(const uint8_t * src, int wtype, int K, int Ntot, int r0, int r1
     }
 }
 
-int pack(const char * path, std::vector<uint8_t> & out) {
+int pack(const char * path, std::vector<uint8_t> & out, int act = 0) {
     char err[256];
     q2a_model_file * mf = q2a_model_file_read(path, err, sizeof(err));
     if (!mf) { set_err("%s", err); return errno == ENOENT ? Q2A_ERR_IO : Q2A_ERR_FORMAT; }
@@ -234,7 +282,7 @@ int pack(const char * path, std::vector<uint8_t> & out) {
     }
     if (mf->n_mel_filt != d.M || mf->n_fft_filt != 201) { set_err("bad mel filter shape"); return Q2A_ERR_FORMAT; }
     blob_header h;
-    if (!plan(h, hp, wtype)) { set_err("too many layers"); return Q2A_ERR_UNSUPPORTED; }
+    if (!plan(h, hp, wtype, act)) { set_err("too many layers"); return Q2A_ERR_UNSUPPORTED; }
     out.assign(h.total, 0);
     uint8_t * blob = out.data();
     memcpy(blob, &h, sizeof(h));
@@ -359,7 +407,7 @@ int pack(const char * path, std::vector<uint8_t> & out) {
         th.emplace_back([&, t]() {
             for (const job & j : jobs) {
                 const int n = j.r1 - j.r0;
-                expand_rows(j.src, wtype, j.K, j.Ntot, j.r0 + n * t / nt, j.r0 + n * (t + 1) / nt, blob, j.a, j.dst0);
+                expand_rows(j.src, wtype, j.K, j.Ntot, j.r0 + n * t / nt, j.r0 + n * (t + 1) / nt, blob, j.a, j.dst0, act);
             }
         });
     for (auto & x : th) x.join();
@@ -419,6 +467,11 @@ __global__ void k_to_half(const float * x, q2a_half * y, int64_t n) {
     if (i < n) y[i] = (_Float16) x[i];
 }
 
+__global__ void k_to_bf16(const float * x, q2a_half * y, int64_t n) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) y[i] = __builtin_bit_cast(_Float16, (__bf16) x[i]);
+}
+
 // F32-weight activation operand: x [M][K] f32 -> [hi | lo | hi] rows of 3K fp16
 __global__ void k_split3(const float * x, q2a_half * y, int K, int64_t n) {
     const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
@@ -451,6 +504,8 @@ struct q2a_engine {
     int wtype = 0, blk = 0;
     bool f32 = false;        // all-F32 model file: fp16 hi/lo split operands, GEMM K tripled (kx = 3)
     int kx = 1;
+    bool bf16 = false;       // bf16-activation mode (Q2A_ACT_BF16): bf16 weights and inter-op activations
+    int gblk = 0;            // the GEMM launcher's blk: blk, or Q2A_BLK_BF16
     uint8_t * blob = nullptr;
     bool own_blob = false;
     int64_t blob_size = 0;
@@ -517,7 +572,9 @@ int engine_adopt_header(q2a_engine * e) {
     e->wtype = e->h.wtype;
     e->blk = e->h.blk;
     e->f32 = e->wtype == Q2A_TYPE_F32;
-    e->kx = e->f32 ? 3 : 1;
+    e->bf16 = e->h.act == Q2A_ACT_BF16;
+    e->kx = e->f32 && !e->bf16 ? 3 : 1;
+    e->gblk = e->bf16 ? Q2A_BLK_BF16 : e->blk;
     e->TP = ((e->d.T + 63) / 64) * 64;
     return Q2A_OK;
 }
@@ -645,7 +702,7 @@ hipEvent_t prof_event(q2a_engine * e) {
         if ((e)->prof) { (void) hipEventRecord(r_.b, s); (e)->pending.push_back(r_); } \
     } while (0)
 
-int ln_mode(const q2a_engine * e) { return e->f32 ? 3 : e->blk == 0 ? 0 : e->blk == 256 ? 1 : 2; }
+int ln_mode(const q2a_engine * e) { return e->bf16 ? 4 : e->f32 ? 3 : e->blk == 0 ? 0 : e->blk == 256 ? 1 : 2; }
 
 #define LAUNCH(x)                                                                     \
     do {                                                                              \
@@ -668,16 +725,16 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         a.bias = e->lv<const float *>(l, L_BQKV);
         a.qh = e->qh; a.ql = e->ql; a.kh = e->kh; a.kl = e->kl; a.vt = e->vt;
         a.qscale = 1.0f / sqrtf((float) (d.D / d.H));
-        PLAUNCH(e, s, Q2A_PROF_GEMM_QKV, q2a_launch_gemm(a, Q2A_EPI_QKV, e->blk, s));
+        PLAUNCH(e, s, Q2A_PROF_GEMM_QKV, q2a_launch_gemm(a, Q2A_EPI_QKV, e->gblk, s));
     }
     {
-        q2a_attn_args at{e->qh, e->ql, e->kh, e->kl, e->vt, B, d.T, d.D, d.H, e->TP, nullptr, nullptr};
-        if (mode == 0) at.outH = e->actD; else at.outF = e->attF;
+        q2a_attn_args at{e->qh, e->ql, e->kh, e->kl, e->vt, B, d.T, d.D, d.H, e->TP, nullptr, nullptr, e->bf16 ? 1 : 0};
+        if (mode == 0 || mode == 4) at.outH = e->actD; else at.outF = e->attF;
         PLAUNCH(e, s, Q2A_PROF_ATTN, q2a_launch_attention(at, s));
         if (mode == 3) {
             const int64_t n = (int64_t) M * d.D;
             PLAUNCH(e, s, Q2A_PROF_QUANT, launch_split3(e->attF, e->actD, d.D, n, s));
-        } else if (mode) {
+        } else if (mode == 1 || mode == 2) {
             q2a_quant_args qa{e->attF, nullptr, M, d.D, mode, e->actD, e->dyD, e->aextD, e->dy_ld};
             PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_quant_act(qa, s));
         }
@@ -686,19 +743,19 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         q2a_gemm_args a = gemm_base(e, l, 1, e->actD, M);
         a.bias = e->lv<const float *>(l, L_BO);
         a.outF = e->X; a.ldo = d.D;
-        PLAUNCH(e, s, Q2A_PROF_GEMM_O, q2a_launch_gemm(a, Q2A_EPI_RESID, e->blk, s));
+        PLAUNCH(e, s, Q2A_PROF_GEMM_O, q2a_launch_gemm(a, Q2A_EPI_RESID, e->gblk, s));
     }
     q2a_ln_args ln2{e->X, M, d.D, e->lv<const float *>(l, L_LN2W), e->lv<const float *>(l, L_LN2B), mode, e->actD, e->dyD, e->aextD, e->dy_ld};
     PLAUNCH(e, s, Q2A_PROF_LN, q2a_launch_layernorm(ln2, s));
     {
         q2a_gemm_args a = gemm_base(e, l, 2, e->actD, M);
         a.bias = e->lv<const float *>(l, L_B1);
-        if (mode == 0 || mode == 3) {
+        if (mode == 0 || mode == 3 || mode == 4) {
             // F32 weights: the GELU output is exactly fp16 (LUT), so the fc2 operand is [h | 0 | h] (middle third
             // stays zero from the workspace memset) against [W2h | W2h | W2l]
             a.outH = e->actF; a.ldo = (int64_t) d.F * e->kx; a.o_rpg = M; a.o_gstride = 0; a.o_off = 0;
             a.o_dup = mode == 3 ? 2 * d.F : 0;
-            PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_H, 0, s));
+            PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_H, e->gblk, s));
         } else if (mode == 1 && q2a_gemm_wide_tiles(M, d.F, e->blk) &&
                    e->fuse_q8k == 1 && q2a_gemm_pipe8(a, e->blk)) {
             // fused fc1 + GELU + Q8_K quantization of the fc2 input (one Q8_K block per 256-column tile)
@@ -717,7 +774,7 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         q2a_gemm_args a = gemm_base(e, l, 3, e->actF, M);
         a.bias = e->lv<const float *>(l, L_B2);
         a.outF = e->X; a.ldo = d.D;
-        PLAUNCH(e, s, Q2A_PROF_GEMM_FC2, q2a_launch_gemm(a, Q2A_EPI_RESID, e->blk, s));
+        PLAUNCH(e, s, Q2A_PROF_GEMM_FC2, q2a_launch_gemm(a, Q2A_EPI_RESID, e->gblk, s));
     }
     return Q2A_OK;
 }
@@ -818,9 +875,12 @@ extern "C" {
 
 const char * q2a_last_error(void) { return g_err.c_str(); }
 
-int64_t q2a_pack_model(const char * path, void ** host_blob) {
+int64_t q2a_pack_model(const char * path, void ** host_blob) { return q2a_pack_model_ex(path, Q2A_ACT_REFERENCE, host_blob); }
+
+int64_t q2a_pack_model_ex(const char * path, int act, void ** host_blob) {
+    if (act != Q2A_ACT_REFERENCE && act != Q2A_ACT_BF16) { set_err("unknown activation mode %d", act); return Q2A_ERR_ARG; }
     std::vector<uint8_t> v;
-    const int rc = pack(path, v);
+    const int rc = pack(path, v, act);
     if (rc) return rc;
     void * p = malloc(v.size());
     if (!p) { set_err("host allocation failed"); return Q2A_ERR_OOM; }
@@ -831,10 +891,13 @@ int64_t q2a_pack_model(const char * path, void ** host_blob) {
 
 void q2a_free_host_blob(void * p) { free(p); }
 
-q2a_engine * q2a_open(const char * model_path, int device) {
+q2a_engine * q2a_open(const char * model_path, int device) { return q2a_open_ex(model_path, device, Q2A_ACT_REFERENCE); }
+
+q2a_engine * q2a_open_ex(const char * model_path, int device, int act) {
+    if (act != Q2A_ACT_REFERENCE && act != Q2A_ACT_BF16) { set_err("unknown activation mode %d", act); return nullptr; }
     q2a_engine * e = new q2a_engine();
     std::vector<uint8_t> v;
-    if (engine_init(e, device) || pack(model_path, v)) { q2a_close(e); return nullptr; }
+    if (engine_init(e, device) || pack(model_path, v, act)) { q2a_close(e); return nullptr; }
     memcpy(&e->h, v.data(), sizeof(blob_header));
     if (engine_adopt_header(e)) { q2a_close(e); return nullptr; }
     if (hipMalloc((void **) &e->blob, v.size()) != hipSuccess) {
@@ -902,6 +965,8 @@ int q2a_get_info(const q2a_engine * e, q2a_info * info) {
     info->n_audio_ctx = e->d.T; info->n_audio_state = e->d.D; info->n_audio_head = e->d.H;
     info->n_audio_layer = e->d.L; info->n_mels = e->d.M; info->wtype = e->wtype; info->n_out = e->d.TO;
     info->device = e->device; info->weight_bytes = e->blob_size; info->workspace_bytes = (int64_t) e->ws_bytes;
+    info->act = e->bf16 ? Q2A_ACT_BF16 : Q2A_ACT_REFERENCE;
+    info->reserved = 0;
     return Q2A_OK;
 }
 
@@ -1044,9 +1109,10 @@ int q2a_test_linear(q2a_engine * e, int layer, int which, const float * x, int M
     mat_dims(d, which, N, K);
     q2a_half * A = K == d.D ? e->actD : e->actF;
     const int mode = ln_mode(e);
-    if (mode == 0) {
+    if (mode == 0 || mode == 4) {
         const int64_t n = (int64_t) M * K;
-        hipLaunchKernelGGL(k_to_half, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, A, n);
+        if (mode == 0) hipLaunchKernelGGL(k_to_half, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, A, n);
+        else hipLaunchKernelGGL(k_to_bf16, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, A, n);
         LAUNCH(hipGetLastError());
     } else if (mode == 3) {
         const int64_t n = (int64_t) M * K;
@@ -1058,7 +1124,7 @@ int q2a_test_linear(q2a_engine * e, int layer, int which, const float * x, int M
     }
     q2a_gemm_args a = gemm_base(e, layer, which, A, M);
     a.outF = y; a.ldo = N;
-    LAUNCH(q2a_launch_gemm(a, Q2A_EPI_STORE_F, e->blk, s));
+    LAUNCH(q2a_launch_gemm(a, Q2A_EPI_STORE_F, e->gblk, s));
     return Q2A_OK;
 }
 

@@ -256,6 +256,9 @@ __global__ __launch_bounds__(256) void k_rownorm(const float * __restrict__ X, i
         const int m = row / nseg, seg = row - m * nseg;
         if (MODE == 0) {
             o[0] = (_Float16) y.x; o[1] = (_Float16) y.y; o[2] = (_Float16) y.z; o[3] = (_Float16) y.w;
+        } else if (MODE == 4) {   // bf16-activation mode: RNE to bf16, bits in the fp16-typed slots
+            o[0] = __builtin_bit_cast(_Float16, (__bf16) y.x); o[1] = __builtin_bit_cast(_Float16, (__bf16) y.y);
+            o[2] = __builtin_bit_cast(_Float16, (__bf16) y.z); o[3] = __builtin_bit_cast(_Float16, (__bf16) y.w);
         } else if (MODE == 3) {
             const float yy[4] = {y.x, y.y, y.z, y.w};
 #pragma unroll
@@ -363,6 +366,7 @@ hipError_t q2a_launch_layernorm(const q2a_ln_args & a, hipStream_t s) {
     const dim3 grid((a.M + 3) / 4), blk(256);
     if (a.mode == 0) hipLaunchKernelGGL((k_rownorm<0, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else if (a.mode == 3) hipLaunchKernelGGL((k_rownorm<3, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
+    else if (a.mode == 4) hipLaunchKernelGGL((k_rownorm<4, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else if (a.mode == 1 && a.D == 1280 && !getenv("Q2A_QUANT_V1"))
         hipLaunchKernelGGL((k_rownorm<1, true, false, 5>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else if (a.mode == 1) hipLaunchKernelGGL((k_rownorm<1, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);

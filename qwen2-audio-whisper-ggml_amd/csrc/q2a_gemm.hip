@@ -26,6 +26,7 @@ namespace {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void * lds_ptr_t;
@@ -74,6 +75,20 @@ __device__ __forceinline__ int64_t a_row_off(const q2a_gemm_args & p, int m) {
     return ((int64_t) (m / p.a_rpg) * p.a_gstride + (int64_t) (m % p.a_rpg) * p.a_step) * p.lda;
 }
 
+// one 16x16x32 MFMA on fp16 operands, or on the same bits read as bf16 (bf16-activation mode)
+template <bool BF>
+__device__ __forceinline__ f4 mma16(half8 a, half8 b, f4 c) {
+    if constexpr (BF) return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf8, a), __builtin_bit_cast(bf8, b), c, 0, 0, 0);
+    else return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+
+// 16-bit activation store: fp16 RNE, or bf16 RNE in the bf16-activation mode (bits in a _Float16 slot)
+template <bool BF>
+__device__ __forceinline__ _Float16 to16(float v) {
+    if constexpr (BF) return __builtin_bit_cast(_Float16, (__bf16) v);
+    else return (_Float16) v;
+}
+
 __device__ __forceinline__ half8 frag(const char * img, int row, int chunk) {
     return *(const half8 *) (img + row * ROWB + ((chunk ^ (row & 7)) << 4));
 }
@@ -98,7 +113,7 @@ constexpr int SBUF_OFF = 8 * 128 * ROWB;     // 128 KiB: scale staging after the
 constexpr int SBUF_BYTES = 25 * 1024;       // 21 pieces of 1 KiB (+3 pad slots for the uniform 3 glds per thread)
 constexpr int ALPHA_OFF = 24 * 1024;        //   + alpha = dy_{b-1}/dy_b per tile row (1 KiB), computed a block ahead
 
-template <int BLK, bool LUT>
+template <int BLK, bool LUT, bool BF>
 __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&acc)[8][4], char * lds_raw, int m0, int n0,
                                                 int lane, int wave, int wm, int wn) {
     constexpr int HT = 128 * ROWB;                        // one half-tile image (16 KiB)
@@ -287,8 +302,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             for (int i = 0; i < 4; ++i)
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
-                    acc[qm * 4 + i][qn * 2 + j] =
-                        __builtin_amdgcn_mfma_f32_16x16x32_f16(bf[qn][j][s2], af[i][s2], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+                    acc[qm * 4 + i][qn * 2 + j] = mma16<BF>(bf[qn][j][s2], af[i][s2], acc[qm * 4 + i][qn * 2 + j]);
     };
 #define Q2A_PB(N)                                               \
     asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory");       \
@@ -370,8 +384,10 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI, int BLK, int PIPE>
+template <int BM, int BN, int WM, int WN, int EPI, int BLK_, int PIPE>
 __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p) {
+    constexpr bool BF = BLK_ == Q2A_BLK_BF16;              // bf16 operands, no block scales
+    constexpr int BLK = BF ? 0 : BLK_;
     constexpr int NW = WM * WN;
     constexpr int MI = BM / WM / 16, NJ = BN / WN / 16;   // 16x16 tiles per wave
     constexpr int LA = BM / 8 / NW, LB = BN / 8 / NW;     // glds instructions per wave per stage
@@ -414,7 +430,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
     if constexpr (PIPE == 1) {
-        mainloop_8phase<BLK, LUT_EPI>(p, acc, lds_raw, m0, n0, lane, wave, wm, wn);
+        mainloop_8phase<BLK, LUT_EPI, BF>(p, acc, lds_raw, m0, n0, lane, wave, wm, wn);
     } else {
         // per-lane source rows of this wave's glds instructions (rows past M clamp to M-1: loaded, never stored)
         int64_t arow[LA], wrow[LB];
@@ -509,7 +525,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
     #pragma unroll
                     for (int j = 0; j < NJ; ++j) {
                         // W as the A operand: C^T tiles (lane = 4 consecutive columns of one row, see the epilogue)
-                        if (BLK == 0) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], a, acc[i][j], 0, 0, 0);
+                        if (BLK == 0) acc[i][j] = mma16<BF>(b[j], a, acc[i][j]);
                         else blk[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], a, blk[i][j], 0, 0, 0);
                     }
                 }
@@ -728,7 +744,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                 for (int j = 0; j < NJ; ++j)
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        ((_Float16 *) wl)[(j * 16 + 4 * q + r) * (PR + 4) + ii * 16 + l16] = (_Float16) val(ps * (PR / 16) + ii, j, r);
+                        ((_Float16 *) wl)[(j * 16 + 4 * q + r) * (PR + 4) + ii * 16 + l16] = to16<BF>(val(ps * (PR / 16) + ii, j, r));
             __syncthreads();
             const int prow = rbase + ps * PR;
             const int c = cbase - 2 * p.D + lane, h = c >> 6, d = c & 63;
@@ -759,11 +775,15 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                     if (EPI == Q2A_EPI_GELU_H && LUT_EPI) {
                         ha[r] = gelu_lut_c16(acc[i][2 * jp][r] + bias4[2 * jp][r], lut);
                         hb[r] = gelu_lut_c16(acc[i][2 * jp + 1][r] + bias4[2 * jp + 1][r], lut);
+                        if (BF) {   // the fp16 GELU value handed on as bf16
+                            ha[r] = to16<true>((float) ha[r]);
+                            hb[r] = to16<true>((float) hb[r]);
+                        }
                     } else {
                         const float va = val(i, 2 * jp, r), vb = val(i, 2 * jp + 1, r);
-                        ha[r] = (_Float16) va;
-                        hb[r] = (_Float16) vb;
-                        if (EPI == Q2A_EPI_QKV) {
+                        ha[r] = to16<BF>(va);
+                        hb[r] = to16<BF>(vb);
+                        if (EPI == Q2A_EPI_QKV && !BF) {
                             la[r] = (_Float16) (va - (float) ha[r]);
                             lb[r] = (_Float16) (vb - (float) hb[r]);
                         }
@@ -771,7 +791,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                 }
                 const uint4 hv = pair16(ha, hb);
                 uint4 lv;
-                if (EPI == Q2A_EPI_QKV) lv = pair16(la, lb);
+                if (EPI == Q2A_EPI_QKV && !BF) lv = pair16(la, lb);
                 if (m < p.M) {
                     const int col = 32 * jp + pcol;
                     if (EPI == Q2A_EPI_GELU_H) {
@@ -782,7 +802,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                     } else {
                         const int64_t o = (int64_t) m * p.D + cbase - part * p.D + col;
                         *(uint4 *) ((part == 0 ? p.qh : p.kh) + o) = hv;
-                        *(uint4 *) ((part == 0 ? p.ql : p.kl) + o) = lv;
+                        if (!BF) *(uint4 *) ((part == 0 ? p.ql : p.kl) + o) = lv;
                     }
                 }
             }
@@ -849,7 +869,7 @@ bool pipe8_ok(const q2a_gemm_args & a, int blk) {
     if (!pipe8_enabled() || !wide_tiles(a.M, a.N)) return false;
     const int64_t last = (int64_t) ((a.M - 1) / a.a_rpg) * a.a_gstride + (int64_t) ((a.M - 1) % a.a_rpg) * a.a_step;
     if ((last + 1) * a.lda >= (1ll << 32) || (int64_t) a.N * a.ldw >= (1ll << 32)) return false;
-    if (blk == 0) return (a.K / BK) % 2 == 0;
+    if (blk == 0 || blk == Q2A_BLK_BF16) return (a.K / BK) % 2 == 0;
     if (blk == 256) return (a.K / BK) % 4 == 0;
     return false;
 }
@@ -872,6 +892,13 @@ hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
             return big ? launch_cfg<128, 256, 2, 4, EPI, 256>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 256>(a, s);
         }
         if (blk == 32) return big ? launch_cfg<128, 256, 2, 4, EPI, 32>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 32>(a, s);
+        if constexpr (EPI == Q2A_EPI_QKV || EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_STORE_F) {
+            if (blk == Q2A_BLK_BF16) {
+                constexpr int B16 = Q2A_BLK_BF16;
+                if (p8) return launch_cfg<256, 256, 2, 4, EPI, B16, 1>(a, s);
+                return big ? launch_cfg<256, 256, 2, 4, EPI, B16>(a, s) : launch_cfg<128, 128, 2, 2, EPI, B16>(a, s);
+            }
+        }
         return hipErrorInvalidValue;
     }
 }
@@ -880,7 +907,7 @@ hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
 
 hipError_t q2a_launch_gemm(const q2a_gemm_args & a, int epi, int blk, hipStream_t s) {
     if (a.N % 128 != 0 || a.K % BK != 0 || a.M <= 0) return hipErrorInvalidValue;
-    if (blk && (a.K % blk != 0)) return hipErrorInvalidValue;
+    if (blk > 1 && (a.K % blk != 0)) return hipErrorInvalidValue;
     switch (epi) {
         case Q2A_EPI_QKV: return launch_epi<Q2A_EPI_QKV>(a, blk, s);
         case Q2A_EPI_RESID: return launch_epi<Q2A_EPI_RESID>(a, blk, s);

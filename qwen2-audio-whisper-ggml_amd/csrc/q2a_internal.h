@@ -63,7 +63,9 @@ struct q2a_gemm_args {
     int dy_ld;                        // row stride of dy/aext (M rounded up to 256)
 };
 
-// blk: 0 (plain fp16 GEMM), 256 (Q4_K x Q8_K), 32 (Q8_0/Q4_0 x Q8_0)
+// blk: 0 (plain fp16 GEMM), 256 (Q4_K x Q8_K), 32 (Q8_0/Q4_0 x Q8_0), Q2A_BLK_BF16 (bf16 x bf16 MFMA, no block
+// scales: the bf16-activation mode, whose fp16-typed operand and output pointers then hold bf16 bits)
+constexpr int Q2A_BLK_BF16 = 1;
 hipError_t q2a_launch_gemm(const q2a_gemm_args & a, int epi, int blk, hipStream_t s);
 // true when the launcher will use the 256-column tile configuration for this shape (Q2A_EPI_GELU_Q8K needs it)
 bool q2a_gemm_wide_tiles(int M, int N, int blk);
@@ -76,6 +78,7 @@ struct q2a_attn_args {
     int n_clips, T, D, H, TP;
     q2a_half * outH;     // [clips*T][D] fp16 (F16 path) or
     float * outF;        // [clips*T][D] f32  (quantized paths)
+    int bf16;            // bf16-activation mode: qh/kh/vt and outH hold bf16, ql/kl unused, one MFMA per QK^T step
 };
 hipError_t q2a_launch_attention(const q2a_attn_args & a, hipStream_t s);
 
@@ -104,6 +107,7 @@ hipError_t q2a_launch_mel(const q2a_mel_args & a, hipStream_t s);
 //   1: Q8_K as fp16 codes + dy[M][D/256] + aext (Q4_K weights)
 //   2: Q8_0 as fp16 codes + dy[M][D/32]  (Q8_0 / Q4_0 weights)
 //   3: fp16 split [hi | lo | hi] rows of 3D (F32 weights: exact-f32-class products against [Wh | Wh | Wl])
+//   4: bf16 RNE [M][D]                 (bf16-activation mode)
 struct q2a_ln_args {
     const float * X;
     int M, D;

@@ -31,7 +31,13 @@ class Q2AError(RuntimeError):
 class Info(C.Structure):
     _fields_ = [("n_audio_ctx", C.c_int32), ("n_audio_state", C.c_int32), ("n_audio_head", C.c_int32),
                 ("n_audio_layer", C.c_int32), ("n_mels", C.c_int32), ("wtype", C.c_int32), ("n_out", C.c_int32),
-                ("device", C.c_int32), ("weight_bytes", C.c_int64), ("workspace_bytes", C.c_int64)]
+                ("device", C.c_int32), ("weight_bytes", C.c_int64), ("workspace_bytes", C.c_int64),
+                ("act", C.c_int32), ("reserved", C.c_int32)]
+
+
+# activation contracts (include/q2a_encoder.h)
+ACT_REFERENCE = 0
+ACT_BF16 = 1
 
 
 _lib = None
@@ -48,8 +54,12 @@ def lib() -> C.CDLL:
         L.q2a_last_error.restype = C.c_char_p
         L.q2a_open.restype = vp
         L.q2a_open.argtypes = [C.c_char_p, C.c_int]
+        L.q2a_open_ex.restype = vp
+        L.q2a_open_ex.argtypes = [C.c_char_p, C.c_int, C.c_int]
         L.q2a_pack_model.restype = C.c_int64
         L.q2a_pack_model.argtypes = [C.c_char_p, C.POINTER(vp)]
+        L.q2a_pack_model_ex.restype = C.c_int64
+        L.q2a_pack_model_ex.argtypes = [C.c_char_p, C.c_int, C.POINTER(vp)]
         L.q2a_free_host_blob.argtypes = [vp]
         L.q2a_open_device_blob.restype = vp
         L.q2a_open_device_blob.argtypes = [vp, C.c_int64, C.c_int]
@@ -75,12 +85,12 @@ class Engine:
     """One encoder engine on one HIP device (the analogue of a whisper_context + whisper_state)."""
 
     def __init__(self, model_path: str | None = None, device: int = 0, device_blob: int | None = None,
-                 blob_size: int | None = None):
+                 blob_size: int | None = None, act: int = ACT_REFERENCE):
         L = lib()
-        if device_blob is not None:
+        if device_blob is not None:   # the blob carries its own activation contract
             h = L.q2a_open_device_blob(C.c_void_p(device_blob), C.c_int64(blob_size), device)
         else:
-            h = L.q2a_open(model_path.encode(), device)
+            h = L.q2a_open_ex(model_path.encode(), device, act)
         if not h:
             raise Q2AError(L.q2a_last_error().decode())
         self.h = h
@@ -151,10 +161,10 @@ class Engine:
                                         C.c_void_p(out_ptr), C.c_void_p(stream) if stream else None))
 
 
-def pack_model(path: str) -> bytes:
+def pack_model(path: str, act: int = ACT_REFERENCE) -> bytes:
     """Pack a model file into the device-layout blob (host bytes), e.g. for an RCCL broadcast."""
     p = C.c_void_p()
-    n = lib().q2a_pack_model(path.encode(), C.byref(p))
+    n = lib().q2a_pack_model_ex(path.encode(), act, C.byref(p))
     if n < 0:
         raise Q2AError(lib().q2a_last_error().decode())
     try:

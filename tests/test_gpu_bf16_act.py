@@ -1,0 +1,192 @@
+"""The bf16-activation contract (Q2A_ACT_BF16; BASELINE.json configs[4]: "Q8_0 + bf16 activations").
+
+This mode is deliberately NOT the reference's numerics (SURVEY.md §7 "Hard parts": Q8_0 + bf16 activations is a
+different numerical contract): the linear weights are dequantized like ggml's dequantize_row_* and rounded to bf16,
+every inter-op activation (LN outputs, Q/K/V, attention probabilities and output, GELU output) is bf16, products are
+exact in fp32 and accumulate in fp32. Two kinds of checks:
+  * kernel correctness, tight: the HIP path against a float64 torch emulation of exactly that contract
+    (one linear; one whole encoder block, small and wide-tile shapes);
+  * distance from the reference CPU Q8_0 path (golden fixtures), reported separately with its own bar.
+All tests need an MI355X."""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import rel_errors
+from q2a import ggmlfile
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+D_TINY, F_TINY, H_TINY = 256, 1024, 4
+
+
+@pytest.fixture(scope="module")
+def bf_engines(make_model):
+    import q2a
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need a HIP device")
+    cache = {}
+
+    def get(cfg, wt):
+        if (cfg, wt) not in cache:
+            cache[(cfg, wt)] = q2a.Engine(make_model(cfg, wt), device=0, act=q2a.ACT_BF16)
+        return cache[(cfg, wt)]
+
+    yield get
+    for e in cache.values():
+        e.close()
+
+
+def dequant(t: ggmlfile.Tensor) -> np.ndarray:
+    """ggml dequantize_row_* of a 2-D weight (F16 / Q8_0) -> float64 [rows][K]."""
+    K = t.ne[0]
+    rows = int(np.prod(t.ne)) // K
+    if t.type == 1:
+        return t.data.view(np.float16).astype(np.float64).reshape(rows, K)
+    assert t.type == 8, "Q8_0 / F16 only"
+    blk = t.data.reshape(rows, K // 32, 34)
+    d = blk[:, :, :2].copy().view(np.float16).astype(np.float32)            # [rows][nb][1]
+    q = blk[:, :, 2:].copy().view(np.int8).astype(np.float32)               # [rows][nb][32]
+    return (q * d).astype(np.float32).reshape(rows, K).astype(np.float64)   # q*d in f32, as ggml
+
+
+def bf(x: torch.Tensor) -> torch.Tensor:
+    """Round to bf16 (RNE) and back, in the tensor's own dtype."""
+    return x.to(torch.bfloat16).to(x.dtype)
+
+
+def w_bf16(mf, name) -> torch.Tensor:
+    return bf(torch.from_numpy(dequant(mf.t(name))).float()).double().cuda()
+
+
+def vec(mf, name) -> torch.Tensor:
+    return torch.from_numpy(mf.t(name).as_f32().reshape(-1).astype(np.float64)).cuda()
+
+
+def gelu_lut(x: torch.Tensor) -> torch.Tensor:
+    """ggml_vec_gelu_f32 with GGML_GELU_FP16 (ggml.c:2556-2570): fp16(gelu_f32(fp16(x))), x<=-10 -> 0, x>=10 -> x."""
+    h = x.float().half().float()
+    g = (0.5 * h * (1.0 + torch.tanh(0.7978845608028654 * h * (1.0 + 0.044715 * h * h)))).half().double()
+    g = torch.where(x <= -10, torch.zeros_like(g), g)
+    return torch.where(x >= 10, x.float().half().double(), g)
+
+
+def layer_norm(x: torch.Tensor, g: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    mu = x.mean(-1, keepdim=True)
+    var = ((x - mu) ** 2).mean(-1, keepdim=True)
+    return (x - mu) / torch.sqrt(var + 1e-5) * g + b
+
+
+def block_emulation(mf, layer: int, x: torch.Tensor, T: int, H: int) -> torch.Tensor:
+    """One encoder block (qwen2-whisper.cpp:2014-2155) under the bf16-activation contract, float64 otherwise."""
+    p = f"layers.{layer}."
+    D = x.shape[-1]
+    xb = x.double().reshape(-1, T, D)
+    a = bf(layer_norm(xb, vec(mf, p + "self_attn_layer_norm.weight"), vec(mf, p + "self_attn_layer_norm.bias")))
+    q = bf((a @ w_bf16(mf, p + "self_attn.q_proj.weight").T + vec(mf, p + "self_attn.q_proj.bias")) * 0.125)
+    k = bf(a @ w_bf16(mf, p + "self_attn.k_proj.weight").T)
+    v = bf(a @ w_bf16(mf, p + "self_attn.v_proj.weight").T + vec(mf, p + "self_attn.v_proj.bias"))
+    B = xb.shape[0]
+    qh, kh, vh = (t.reshape(B, T, H, 64).transpose(1, 2) for t in (q, k, v))
+    s = qh @ kh.transpose(-1, -2)
+    pr = torch.exp(s - s.amax(-1, keepdim=True))
+    o = (bf(pr) @ vh) / pr.sum(-1, keepdim=True)
+    o = bf(o.transpose(1, 2).reshape(B, T, D))
+    x1 = o @ w_bf16(mf, p + "self_attn.out_proj.weight").T + vec(mf, p + "self_attn.out_proj.bias") + xb
+    a2 = bf(layer_norm(x1, vec(mf, p + "final_layer_norm.weight"), vec(mf, p + "final_layer_norm.bias")))
+    h = bf(gelu_lut(a2 @ w_bf16(mf, p + "fc1.weight").T + vec(mf, p + "fc1.bias")))
+    x2 = h @ w_bf16(mf, p + "fc2.weight").T + vec(mf, p + "fc2.bias") + x1
+    return x2.reshape(-1, D)
+
+
+# ---------------------------------------------------------------- one linear: exact products, fp32 sums
+@pytest.mark.parametrize("M", [1500 + 7, 45000 + 17])   # 128x128 tiles / the 8-phase 256x256 kernel (N % 256 == 0)
+@pytest.mark.parametrize("which", [0, 1, 2, 3])
+def test_bf16_linear_matches_emulation(bf_engines, make_model, which, M):
+    e = bf_engines("tiny", "q8_0")
+    mf = ggmlfile.read(make_model("tiny", "q8_0"))
+    names = {0: ["self_attn.q_proj.weight", "self_attn.k_proj.weight", "self_attn.v_proj.weight"],
+             1: ["self_attn.out_proj.weight"], 2: ["fc1.weight"], 3: ["fc2.weight"]}[which]
+    w = torch.cat([w_bf16(mf, f"layers.1.{n}") for n in names])
+    N, K = w.shape
+    x = torch.from_numpy(np.random.default_rng(7 + which).standard_normal((M, K)).astype(np.float32)).cuda()
+    y = torch.empty((M, N), dtype=torch.float32, device="cuda")
+    e.test_linear(1, which, x.data_ptr(), M, y.data_ptr())
+    torch.cuda.synchronize()
+    ref = bf(x).double() @ w.T   # bf16 x bf16 products are exact; only the fp32 summation order differs
+    mx, l2 = rel_errors(y.cpu().numpy(), ref.cpu().numpy())
+    assert mx < 1e-5 and l2 < 1e-6, (mx, l2)
+
+
+# ---------------------------------------------------------------- one encoder block (attention included)
+@pytest.mark.parametrize("n_clips", [1, 30])   # 30 clips: M = 45 000, the wide-tile kernels
+def test_bf16_block_matches_emulation(bf_engines, make_model, n_clips):
+    """HIP block vs the float64 emulation of the same contract. The remaining difference is where a bf16
+    rounding of an intermediate lands on the other side of a tie from a 1-ulp fp32 difference, and the online
+    softmax rounding P against the running (not the final) row max; both are far below the contract's own error."""
+    e = bf_engines("tiny", "q8_0")
+    mf = ggmlfile.read(make_model("tiny", "q8_0"))
+    T = 1500
+    rng = np.random.default_rng(11)
+    x0 = (rng.standard_normal((T, D_TINY)) * 0.5).astype(np.float32)
+    x = torch.from_numpy(np.tile(x0, (n_clips, 1))).cuda()
+    ref = block_emulation(mf, 0, torch.from_numpy(x0).cuda(), T, H_TINY).cpu().numpy()
+    e.test_block(0, x.data_ptr(), n_clips)
+    torch.cuda.synchronize()
+    out = x.cpu().numpy().reshape(n_clips, T, D_TINY)
+    for c in sorted({0, n_clips - 1}):
+        mx, l2 = rel_errors(out[c], ref)
+        assert mx < 1e-3 and l2 < 5e-4, (c, mx, l2)   # measured 3.3e-4 / 1.8e-4
+    assert np.array_equal(out[0], out[-1])
+
+
+# ---------------------------------------------------------------- distance from the reference Q8_0 path
+def test_bf16_encoder_tiny_vs_reference_q8_0(bf_engines, make_clip, golden):
+    """Reported separately: the reference CPU Q8_0 path re-quantizes every activation to
+    Q8_0 (int8 per 32), this contract rounds them to bf16 — the two differ by the reference's own quantization noise."""
+    _, g = golden
+    e = bf_engines("tiny", "q8_0")
+    out, st = e.encode_host([make_clip(0)])
+    assert st[0] == 0
+    mx, l2 = rel_errors(out[0][g["rows_stride5"]], g["tiny_q8_0_c0_rows"])
+    assert l2 < 5e-3 and mx < 1e-2, (mx, l2)   # measured 2.1e-3 / 1.5e-3
+
+
+def test_bf16_encoder_full_size_vs_reference_q8_0(bf_engines, make_clip, golden):
+    _, g = golden
+    e = bf_engines("full", "q8_0")
+    clip = make_clip(0)
+    out, st = e.encode_host([clip, clip, clip])
+    assert (st == 0).all()
+    o = out[0].reshape(-1)
+    mxs, l2s = rel_errors(o[g["full_q8_0_c0_idx"]], g["full_q8_0_c0_val"])
+    rn = np.linalg.norm(out[0].astype(np.float64), axis=1)
+    rnerr = np.abs(rn - g["full_q8_0_c0_rownorm"]).max() / g["full_q8_0_c0_rownorm"].max()
+    assert l2s < 2e-2 and rnerr < 1e-2, (mxs, l2s, rnerr)   # measured rel-L2 1.0e-2
+    assert np.array_equal(out[0], out[2])   # no cross-clip state in the batch
+
+
+def test_bf16_blob_carries_contract(make_model, make_clip):
+    """The packed blob is self-describing: a device blob packed with Q2A_ACT_BF16 opens as a bf16 engine and
+    encodes bit for bit like q2a_open_ex (the multi-GPU broadcast path)."""
+    import q2a
+    path = make_model("tiny", "q8_0")
+    blob = q2a.pack_model(path, q2a.ACT_BF16)
+    dev = torch.frombuffer(bytearray(blob), dtype=torch.uint8).cuda()
+    e1 = q2a.Engine(device=0, device_blob=dev.data_ptr(), blob_size=dev.numel())
+    e2 = q2a.Engine(path, device=0, act=q2a.ACT_BF16)
+    e3 = q2a.Engine(path, device=0)
+    try:
+        assert e1.info.act == q2a.ACT_BF16 and e2.info.act == q2a.ACT_BF16 and e3.info.act == q2a.ACT_REFERENCE
+        clip = make_clip(0)
+        o1, _ = e1.encode_host([clip])
+        o2, _ = e2.encode_host([clip])
+        o3, _ = e3.encode_host([clip])
+        assert np.array_equal(o1, o2)
+        assert not np.array_equal(o1, o3)
+        assert math.isfinite(float(np.abs(o1).max()))
+    finally:
+        e1.close(); e2.close(); e3.close()
