@@ -20,6 +20,7 @@
 #include "q2a_internal.h"
 #include "q2a_quant.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace {
@@ -30,6 +31,27 @@ typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef float f2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) void * lds_ptr_t;
+
+// timing diagnostic Q2A_DIAG_NO_STORE (wrong results): the epilogue computes every value but its global stores
+// are predicated off by a condition the compiler cannot fold
+#ifdef Q2A_DIAG_NO_STORE
+#define Q2A_ST (p.K < 0)
+#else
+#define Q2A_ST true
+#endif
+
+// epilogue global store (Q2A_DIAG_NT_STORE: non-temporal, A/B timing of the store cache policy)
+template <class V>
+__device__ __forceinline__ void q2a_st(const V & v, V * ptr) {
+#ifdef Q2A_DIAG_NT_STORE
+    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+    typedef unsigned u2v __attribute__((ext_vector_type(2)));
+    if constexpr (sizeof(V) == 16) __builtin_nontemporal_store(__builtin_bit_cast(u4v, v), (u4v *) ptr);
+    else __builtin_nontemporal_store(__builtin_bit_cast(u2v, v), (u2v *) ptr);
+#else
+    *ptr = v;
+#endif
+}
 
 constexpr int BK = 64;
 constexpr int ROWB = BK * 2;   // bytes per LDS row (64 halves)
@@ -416,6 +438,12 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
     const int wm = wave / WN, wn = wave % WN;
 
     // XCD-contiguous bijective remap, then grouped rasterisation (GROUP_M M-tiles per N column)
+    if (PIPE && p.stagger_ns > 0 && blockIdx.x < 256) {
+        // desynchronise the CUs' tile rounds: CU group (blockIdx/8) % G of the first round starts group * ns / G later
+        const uint64_t dt = (uint64_t) (((blockIdx.x >> 3) % p.stagger_g) * (p.stagger_ns / p.stagger_g)) / 10;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__builtin_amdgcn_s_memrealtime() - t0 < dt) __builtin_amdgcn_s_sleep(8);
+    }
     const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, nwg = nbn * nbm;
     const int bid = blockIdx.x, xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
     const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
@@ -756,7 +784,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                 const bool wrap = t0 + 4 * a >= p.T;
                 const int clip = clip0 + (wrap ? 1 : 0), t = t0 + 4 * a - (wrap ? p.T : 0);
                 const uint2 v = *(const uint2 *) ((const _Float16 *) wl + lane * (PR + 4) + 4 * a);
-                *(uint2 *) (p.vt + (((int64_t) clip * p.H + h) * 64 + d) * p.TP + t) = v;
+                if (Q2A_ST) q2a_st(v, (uint2 *) (p.vt + (((int64_t) clip * p.H + h) * 64 + d) * p.TP + t));
             }
             __syncthreads();
         }
@@ -797,12 +825,12 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                     if (EPI == Q2A_EPI_GELU_H) {
                         const bool wrap = orr + ml >= p.o_rpg;
                         const int64_t row = (int64_t) (oq + (wrap ? 1 : 0)) * p.o_gstride + (orr + ml - (wrap ? p.o_rpg : 0)) + p.o_off;
-                        *(uint4 *) (p.outH + row * p.ldo + cbase + col) = hv;
+                        if (Q2A_ST) q2a_st(hv, (uint4 *) (p.outH + row * p.ldo + cbase + col));
                         if (p.o_dup) *(uint4 *) (p.outH + row * p.ldo + cbase + col + p.o_dup) = hv;
                     } else {
                         const int64_t o = (int64_t) m * p.D + cbase - part * p.D + col;
-                        *(uint4 *) ((part == 0 ? p.qh : p.kh) + o) = hv;
-                        if (!BF) *(uint4 *) ((part == 0 ? p.ql : p.kl) + o) = lv;
+                        if (Q2A_ST) q2a_st(hv, (uint4 *) ((part == 0 ? p.qh : p.kh) + o));
+                        if (!BF && Q2A_ST) q2a_st(lv, (uint4 *) ((part == 0 ? p.ql : p.kl) + o));
                     }
                 }
             }
@@ -835,7 +863,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                     if (EPI == Q2A_EPI_RESID) v[r] = v[r] + add[j][r];        // (acc + bias) + x
                     else if (EPI == Q2A_EPI_CONV2) v[r] = add[j][r] + v[r];   // pe + gelu(...)
                 }
-                *(f4 *) (orow + 16 * j) = v;
+                if (Q2A_ST) q2a_st(v, (f4 *) (orow + 16 * j));
             }
         }
     }
@@ -905,7 +933,11 @@ hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
 
 }  // namespace
 
-hipError_t q2a_launch_gemm(const q2a_gemm_args & a, int epi, int blk, hipStream_t s) {
+hipError_t q2a_launch_gemm(const q2a_gemm_args & a_in, int epi, int blk, hipStream_t s) {
+    static const int st_ns = [] { const char * v = getenv("Q2A_GEMM_STAGGER_NS"); return v ? atoi(v) : 0; }();
+    static const int st_g = [] { const char * v = getenv("Q2A_GEMM_STAGGER_G"); return v ? std::max(1, atoi(v)) : 2; }();
+    q2a_gemm_args a = a_in;
+    a.stagger_ns = st_ns; a.stagger_g = st_g;
     if (a.N % 128 != 0 || a.K % BK != 0 || a.M <= 0) return hipErrorInvalidValue;
     if (blk > 1 && (a.K % blk != 0)) return hipErrorInvalidValue;
     switch (epi) {

@@ -60,6 +60,7 @@ struct q2a_gemm_args {
     float * qdy;                      // Q2A_EPI_GELU_Q8K outputs: block-major d [N/256][dy_ld] and
     q2a_half * qaext;                 //   bsum operand [N/256][dy_ld][16] of the produced activation
     int nblk;
+    int stagger_ns, stagger_g;        // diagnostic (Q2A_GEMM_STAGGER_NS/_G): first-round phase offsets per CU group
     int dy_ld;                        // row stride of dy/aext (M rounded up to 256)
 };
 
