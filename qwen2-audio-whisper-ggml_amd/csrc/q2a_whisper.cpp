@@ -176,7 +176,11 @@ struct whisper_context * whisper_init_from_file_with_params_no_state(const char 
         return nullptr;
     }
     wlog(GGML_LOG_LEVEL_INFO, "whisper_init_from_file_with_params_no_state: loading model from '%s'\n", path_model);
-    q2a_engine * e = q2a_open(path_model, params.gpu_device);
+    // the reference API has no activation-precision knob: Q2A_ACT=bf16 selects the bf16-activation contract
+    // (BASELINE configs[4]) for an unchanged caller such as examples/main
+    const char * act_env = getenv("Q2A_ACT");
+    const int act = act_env && !strcmp(act_env, "bf16") ? Q2A_ACT_BF16 : Q2A_ACT_REFERENCE;
+    q2a_engine * e = q2a_open_ex(path_model, params.gpu_device, act);
     if (!e) { wlog(GGML_LOG_LEVEL_ERROR, "whisper_init: %s\n", q2a_last_error()); return nullptr; }
     whisper_context * ctx = new whisper_context();
     ctx->eng = e;

@@ -20,7 +20,7 @@ struct cli {
     std::string model = "models/ggml-base.en.bin";
     std::vector<std::string> files;
     int threads = 4, offset_ms = 0, duration_ms = 0, reps = 1, device = 0, processors = 1;
-    bool no_prints = false, batch = false, long_audio = false;
+    bool no_prints = false, batch = false, long_audio = false, bf16 = false;
     std::string dump;
 };
 
@@ -37,6 +37,8 @@ void usage(const char * argv0) {
             "  -la,       --long-audio     encode every 30 s window of each file in one batch\n"
             "  -oemb F,   --output-emb F   write embd_enc (f32, [windows/files][750][1280]) to F\n"
             "  -dev N,    --device N       HIP device\n"
+            "  -bf16,     --bf16-act       bf16-activation contract (Q2A_ACT_BF16, BASELINE configs[4]); not the\n"
+            "                              reference's numerics: see DESIGN.md\n"
             "  -np,       --no-prints      only print results\n",
             argv0);
 }
@@ -57,6 +59,7 @@ bool parse(int argc, char ** argv, cli & c) {
         else if (a == "-p" || a == "--processors") { if (!(v = next())) return false; c.processors = atoi(v); }
         else if (a == "-oemb" || a == "--output-emb") { if (!(v = next())) return false; c.dump = v; }
         else if (a == "-b" || a == "--batch") c.batch = true;
+        else if (a == "-bf16" || a == "--bf16-act") c.bf16 = true;
         else if (a == "-la" || a == "--long-audio") c.long_audio = true;
         else if (a == "-np" || a == "--no-prints") c.no_prints = true;
         else if (a[0] == '-' && a != "-") { fprintf(stderr, "error: unknown argument: %s\n", a.c_str()); return false; }
@@ -77,6 +80,7 @@ void quiet(enum ggml_log_level, const char *, void *) {}
 int main(int argc, char ** argv) {
     cli c;
     if (!parse(argc, argv, c)) { usage(argv[0]); return 1; }
+    if (c.bf16) setenv("Q2A_ACT", "bf16", 1);   // the whisper_* paths read it in whisper_init
     if (c.no_prints) whisper_log_set(quiet, nullptr);
     whisper_context_params cp = whisper_context_default_params();
     cp.gpu_device = c.device;
@@ -108,7 +112,7 @@ int main(int argc, char ** argv) {
         std::vector<const float *> ptr;
         std::vector<int32_t> ns;
         for (const auto & p : pcms) { ptr.push_back(p.data()); ns.push_back((int32_t) p.size()); }
-        q2a_engine * e = q2a_open(c.model.c_str(), c.device);
+        q2a_engine * e = q2a_open_ex(c.model.c_str(), c.device, c.bf16 ? Q2A_ACT_BF16 : Q2A_ACT_REFERENCE);
         if (!e) { fprintf(stderr, "error: %s\n", q2a_last_error()); return 3; }
         std::vector<float> out((size_t) ptr.size() * n_out * n_state);
         std::vector<int32_t> st(ptr.size());

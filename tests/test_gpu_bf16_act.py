@@ -190,3 +190,30 @@ def test_bf16_blob_carries_contract(make_model, make_clip):
         assert math.isfinite(float(np.abs(o1).max()))
     finally:
         e1.close(); e2.close(); e3.close()
+
+
+def test_bf16_through_whisper_api(make_model, make_clip, tmp_path):
+    """bin/q2a_main -bf16: whisper_init (Q2A_ACT=bf16, the path an unchanged examples/main takes) and the batched
+    entry point both give the q2a_open_ex(ACT_BF16) engine's output, bit for bit."""
+    import os
+    import subprocess
+    import wave
+    import q2a
+    from conftest import PKG
+    main = os.path.join(PKG, "bin", "q2a_main")
+    path = make_model("tiny", "q8_0")
+    s16 = np.clip(np.round(make_clip(0) * 32767.0), -32768, 32767).astype(np.int16)
+    with wave.open(str(tmp_path / "c0.wav"), "wb") as w:
+        w.setnchannels(1); w.setsampwidth(2); w.setframerate(16000); w.writeframes(s16.tobytes())
+    pcm = s16.astype(np.float32) / np.float32(32768.0)
+    e = q2a.Engine(path, device=0, act=q2a.ACT_BF16)
+    try:
+        ref, _ = e.encode_host([pcm])
+    finally:
+        e.close()
+    for extra in ([], ["-b"]):
+        out = tmp_path / f"emb{len(extra)}.f32"
+        subprocess.run([main, "-m", path, "-np", "-bf16", *extra, "-oemb", str(out), str(tmp_path / "c0.wav")],
+                       capture_output=True, text=True, timeout=300, check=True)
+        emb = np.fromfile(out, dtype=np.float32).reshape(ref[0].shape)
+        assert np.array_equal(emb, ref[0]), extra
