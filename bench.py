@@ -119,11 +119,20 @@ def main():
 
     ws, rank, local = dist_env()
     import torch
+    # Q2A_BENCH_REHEARSE=1: rehearse the N>1 path on a 1-GPU box (every rank on device 0, gloo collectives on host
+    # tensors); the numbers of such a run are not a scaling measurement
+    rehearse = os.environ.get("Q2A_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     torch.cuda.set_device(local)
+    coll_dev = "cpu" if rehearse else "cuda"
     dist = None
     if ws > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import q2a
     from q2a import dist as qd
 
@@ -144,7 +153,7 @@ def main():
     if dist is not None:
         dist.barrier()
     tb = time.time()
-    blob = qd.broadcast_blob(dist, blob_host, rank, "cuda")
+    blob = qd.broadcast_blob(dist, blob_host, rank, coll_dev).cuda()
     torch.cuda.synchronize()
     if dist is not None:
         t_bcast = time.time() - tb
@@ -187,7 +196,7 @@ def main():
     if not os.environ.get("Q2A_DIAG_BUILD"):   # diagnostic A/B libraries (diag/) compute garbage on purpose
         assert torch.isfinite(out).all().item(), "non-finite encoder output"
 
-    elapsed = qd.max_over_ranks(dist, elapsed, "cuda")
+    elapsed = qd.max_over_ranks(dist, elapsed, coll_dev)
 
     # PCIe-inclusive rate (outside `value`): pinned host PCM -> HBM, encode, embd_enc -> pinned host, 2 steps
     pcm_host = pcm.cpu().pin_memory()
@@ -200,7 +209,7 @@ def main():
         eng.encode_device(pcm.data_ptr(), N_SAMPLES, ns, out.data_ptr(), stream=cur)
         out_host.copy_(out, non_blocking=True)
     torch.cuda.synchronize()
-    pcie_rate = qd.max_over_ranks(dist, time.perf_counter() - tp, "cuda")
+    pcie_rate = qd.max_over_ranks(dist, time.perf_counter() - tp, coll_dev)
     pcie_rate = 2 * clips_per_gpu * ws * T_MEL / pcie_rate
     total_clips = clips_per_gpu * ws * args.steps
     value = total_clips * T_MEL / elapsed
