@@ -533,6 +533,7 @@ struct q2a_engine {
     q2a_half *qh = nullptr, *ql = nullptr, *kh = nullptr, *kl = nullptr, *vt = nullptr;
     float * attF = nullptr;
     float * hF = nullptr;
+    int2 * frange = nullptr;         // per mel filter: non-zero bin-group range (computed once from the blob)
     int TP = 0;
     int dy_ld = 0;
     bool force_encode = false;   // encode windows with under 1 s of audio too (whisper_full with duration_ms set)
@@ -779,6 +780,18 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
     return Q2A_OK;
 }
 
+int ensure_frange(q2a_engine * e, hipStream_t s) {
+    if (e->frange) return Q2A_OK;
+    if (hipMalloc((void **) &e->frange, (size_t) e->d.M * sizeof(int2)) != hipSuccess) {
+        (void) hipGetLastError();
+        e->frange = nullptr;
+        set_err("filter-range allocation failed");
+        return Q2A_ERR_OOM;
+    }
+    LAUNCH(q2a_launch_filter_ranges(e->g<const float *>(G_FILT), e->d.M, 201, e->frange, s));
+    return Q2A_OK;
+}
+
 // mel + conv frontend: PCM -> X [B*T][D] (conv graph qwen2-whisper.cpp:1892-1952 + pe add :2005)
 int run_frontend(q2a_engine * e, const float * pcm, int64_t stride, int B, int max_frames, hipStream_t s) {
     const dims & d = e->d;
@@ -790,6 +803,8 @@ int run_frontend(q2a_engine * e, const float * pcm, int64_t stride, int B, int m
     ma.pcm = pcm; ma.pcm_stride = stride; ma.n_samples = nsamp; ma.seek = seek; ma.n_clips = B;
     ma.n_mel = d.M; ma.n_bins = 201; ma.n_frames_win = d.TM; ma.max_frames = max_frames;
     ma.filters = e->g<const float *>(G_FILT); ma.tab = e->g<const float *>(G_TAB);
+    if (int rc = ensure_frange(e, s)) return rc;
+    ma.frange = e->frange;
     ma.mel = e->mel; ma.clip_max = cmax; ma.xc1 = e->xc1; ma.xc_parts = e->f32 ? 3 : 2;
     PLAUNCH(e, s, Q2A_PROF_MEL, q2a_launch_mel(ma, s));
     const int P1 = e->f32 ? 3 : 2, P2 = e->f32 ? 2 : 1;   // operand parts per mel row / per conv1 output row
@@ -955,6 +970,7 @@ void q2a_close(q2a_engine * e) {
     for (auto & r : e->pending) { (void) hipEventDestroy(r.a); (void) hipEventDestroy(r.b); }
     for (auto ev : e->pool) (void) hipEventDestroy(ev);
     if (e->own_blob && e->blob) (void) hipFree(e->blob);
+    if (e->frange) (void) hipFree(e->frange);
     if (e->meta_evt) (void) hipEventDestroy(e->meta_evt);
     if (e->stream) (void) hipStreamDestroy(e->stream);
     delete e;
@@ -1048,6 +1064,8 @@ int q2a_pcm_to_mel(q2a_engine * e, const float * pcm, int n_samples, float * mel
         ma.pcm = dpcm; ma.pcm_stride = n_samples; ma.n_samples = e->meta; ma.seek = e->meta + 1; ma.n_clips = 1;
         ma.n_mel = d.M; ma.n_bins = 201; ma.n_frames_win = d.TM; ma.max_frames = n_len;
         ma.filters = e->g<const float *>(G_FILT); ma.tab = e->g<const float *>(G_TAB);
+        if (int rc = ensure_frange(e, e->stream)) return rc;
+        ma.frange = e->frange;
         ma.mel = e->mel; ma.clip_max = e->meta + 3; ma.xc1 = e->xc1; ma.xc_parts = e->f32 ? 3 : 2;
         if (q2a_launch_mel(ma, s) != hipSuccess) { rc = Q2A_ERR_HIP; break; }
         if (hipMemcpyAsync(chunk.data(), e->mel, chunk.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||

@@ -28,7 +28,12 @@ __global__ __launch_bounds__(256) void k_mel_frames(const q2a_mel_args p) {
     __shared__ float s_a[4][2 * NFFT];
     __shared__ float s_b[4][2 * NFFT];
     __shared__ float s_pow[4][208];
+    __shared__ float s_tw[25][2];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (threadIdx.x < 25) {   // cos/sin cache entries 16 m (global_cache, qwen2-whisper.cpp:2402-2438)
+        s_tw[threadIdx.x][0] = p.tab[NFFT + 16 * threadIdx.x];
+        s_tw[threadIdx.x][1] = p.tab[2 * NFFT + 16 * threadIdx.x];
+    }
     const int c = blockIdx.y;
     const int i = blockIdx.x * 4 + w;
     const int n = p.n_samples[c];
@@ -63,17 +68,21 @@ __global__ __launch_bounds__(256) void k_mel_frames(const q2a_mel_args p) {
         }
     }
     __syncthreads();
-    // leaves: node id (0..15) takes x[id + 16 n], n = 0..24; DFT step 400/25 = 16
+    // leaves: node id (0..15) takes x[id + 16 n], n = 0..24; DFT step 400/25 = 16. The twiddle index
+    // (k t 16) mod 400 = 16 ((k t) mod 25) is stepped incrementally (same index, no integer division) and the 25
+    // twiddles it can take are read from an LDS copy of the reference's cos/sin cache entries
     float * cur = s_a[w];
     if (do_fft) {
         for (int o = lane; o < NFFT; o += 64) {
-            const int id = o / 25, k = o % 25;
+            const int id = o / 25, k = o - 25 * (o / 25);
             float re = 0, im = 0;
+            int m = 0;
             for (int t = 0; t < 25; ++t) {
-                const int idx = (k * t * 16) % NFFT;
                 const float x = s_in[w][id + 16 * t];
-                re += x * cosv[idx];
-                im -= x * sinv[idx];
+                re += x * s_tw[m][0];
+                im -= x * s_tw[m][1];
+                m += k;
+                m = m >= 25 ? m - 25 : m;
             }
             cur[2 * o + 0] = re;
             cur[2 * o + 1] = im;
@@ -114,8 +123,12 @@ __global__ __launch_bounds__(256) void k_mel_frames(const q2a_mel_args p) {
         const float * f = p.filters + (int64_t) j * p.n_bins;
         double sum = 0.0;
         int k = 0;
-        for (k = 0; k < p.n_bins - 3; k += 4) sum += P[k] * f[k] + P[k + 1] * f[k + 1] + P[k + 2] * f[k + 2] + P[k + 3] * f[k + 3];
-        for (; k < p.n_bins; k++) sum += P[k] * f[k];
+        // only the 4-aligned groups holding non-zero filter weights (p.frange): an all-zero group adds exactly
+        // +0.0 to a non-negative double sum, so skipping it leaves the reference's result bit for bit
+        const int kb = p.frange ? p.frange[j].x : 0;
+        const int ke = p.frange ? p.frange[j].y : p.n_bins - 3;
+        for (k = kb; k < ke; k += 4) sum += P[k] * f[k] + P[k + 1] * f[k + 1] + P[k + 2] * f[k + 2] + P[k + 3] * f[k + 3];
+        for (k = (p.n_bins - 3 + 3) / 4 * 4; k < p.n_bins; k++) sum += P[k] * f[k];   // the reference's tail
         const float v = (float) log10(fmax(sum, 1e-10));
         if (in_win) mel_out[(int64_t) j * p.n_frames_win + win] = v;
         lmax = fmaxf(lmax, v);
@@ -351,6 +364,24 @@ __global__ __launch_bounds__(256) void k_pool_ln(const q2a_pool_args p) {
 }
 
 }  // namespace
+
+// per mel filter: [first, end) of the 4-aligned bin groups of the reference's unrolled sum (k < n_bins - 3) that
+// hold a non-zero weight (an empty range when none do)
+__global__ void k_filter_ranges(const float * filters, int n_mel, int n_bins, int2 * out) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_mel) return;
+    const float * f = filters + (int64_t) j * n_bins;
+    int first = -1, last = -1;
+    const int kt = (n_bins - 3 + 3) / 4 * 4;   // bins covered by the 4-way groups (where that loop exits)
+    for (int k = 0; k < kt; ++k)
+        if (f[k] != 0.0f) { if (first < 0) first = k; last = k; }
+    out[j] = first < 0 ? make_int2(0, 0) : make_int2(first / 4 * 4, last / 4 * 4 + 4);
+}
+
+hipError_t q2a_launch_filter_ranges(const float * filters, int n_mel, int n_bins, int2 * out, hipStream_t s) {
+    hipLaunchKernelGGL(k_filter_ranges, dim3((n_mel + 127) / 128), dim3(128), 0, s, filters, n_mel, n_bins, out);
+    return hipGetLastError();
+}
 
 hipError_t q2a_launch_mel(const q2a_mel_args & a, hipStream_t s) {
     if (a.n_bins > 208 || a.n_mel > 128 * 4) return hipErrorInvalidValue;

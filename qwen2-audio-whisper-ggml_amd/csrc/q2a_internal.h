@@ -95,6 +95,7 @@ struct q2a_mel_args {
     int max_frames;             // max n_len over the batch (grid extent)
     const float * filters;      // [n_mel][n_bins]
     const float * tab;          // hann[400] | cos[400] | sin[400]
+    const int2 * frange;        // [n_mel] non-zero 4-aligned bin-group range per filter (q2a_launch_filter_ranges), or NULL
     float * mel;                // [clips][n_mel][n_frames_win] raw log10 values
     int32_t * clip_max;         // [clips] ordered-int encoding of the max over ALL frames
     q2a_half * xc1;             // [clips][n_frames_win+2][parts*n_mel] conv1 operand (hi|lo or hi|lo|hi per row),
@@ -102,6 +103,7 @@ struct q2a_mel_args {
     int xc_parts;               // 2 (F16 conv kernel) or 3 (F32 conv kernel, all-F32 model files)
 };
 hipError_t q2a_launch_mel(const q2a_mel_args & a, hipStream_t s);
+hipError_t q2a_launch_filter_ranges(const float * filters, int n_mel, int n_bins, int2 * out, hipStream_t s);
 
 // LayerNorm over rows of X [M][D] (ggml_norm + mul + add, eps 1e-5), output by mode:
 //   0: fp16 [M][D]                     (F16 weights)
