@@ -540,6 +540,8 @@ struct q2a_engine {
     // fc1 epilogue quantization (Q2A_FUSE_Q8K=1): correct, but at present no faster than the fp16 GELU output
     // plus the bandwidth-bound quantizer, so off by default
     int fuse_q8k = [] { const char * v = getenv("Q2A_FUSE_Q8K"); return v ? atoi(v) : -1; }();
+    // Q4_K fc1: GELU in the GEMM epilogue (1) or deferred to the Q8_K quantizer (0, default; A/B: Q2A_GELU_IN_EPI=1)
+    int gelu_in_epi = [] { const char * v = getenv("Q2A_GELU_IN_EPI"); return v ? atoi(v) : 0; }();
 
     // optional per-kernel-class timing with HIP events on the launch stream (q2a_profile_*)
     bool prof = false;
@@ -762,6 +764,14 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
             // fused fc1 + GELU + Q8_K quantization of the fc2 input (one Q8_K block per 256-column tile)
             a.outH = e->actF; a.ldo = d.F; a.qdy = e->dyF; a.qaext = e->aextF;
             PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_Q8K, e->blk, s));
+        } else if (mode == 1 && !e->gelu_in_epi) {
+            // fc1 writes its fp16 pre-activation (plain stores); the Q8_K quantizer of the fc2 input applies the
+            // GELU table from LDS on the way (same codes as the GELU epilogue + quantizer below)
+            q2a_half * hH = (q2a_half *) e->hF;
+            a.outH = hH; a.ldo = d.F; a.o_rpg = M; a.o_gstride = 0; a.o_off = 0;
+            PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_PRE_H, e->blk, s));
+            PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_gelu_quant_q8k(hH, M, d.F, e->g<const uint16_t *>(G_GELU_C), e->actF,
+                                                                   e->dyF, e->aextF, e->dy_ld, s));
         } else {
             // GELU output is exactly fp16-valued (LUT): keep it as fp16, then quantize for fc2
             q2a_half * hH = (q2a_half *) e->hF;

@@ -2,6 +2,7 @@
 // -ffp-contract=off): log-mel frontend, LayerNorm (+ activation quantizers), AvgPool + final LayerNorm.
 // All are HBM/latency-bound; they are fused so that each tensor is read once and written once.
 #include "q2a_internal.h"
+#include <algorithm>
 #include <cstdlib>
 #include "q2a_quant.h"
 
@@ -309,6 +310,44 @@ __global__ __launch_bounds__(256) void k_quant_q8k_h16(const q2a_half * __restri
     quant_q8k_row16(v, sub, outH + blk * 256 + sub * 16, dy + (int64_t) bf * ld + m, aext + ((int64_t) bf * ld + m) * 16);
 }
 
+// GELU + Q8_K of the fc1 pre-activation (Q2A_EPI_PRE_H output): persistent workgroups of 16 waves each stage the
+// 80 KiB compact GELU table into LDS once, then quantize 4 blocks per wave per iteration like k_quant_q8k_h16.
+// Per element: -inf (x <= -10) -> 0; h >= 10 -> h; else lut[h] (the table's own value at 10.0 is 10.0), which is
+// gelu_lut_c16(x) of the fused epilogue for every x.
+constexpr int GQ_THREADS = 1024;
+__global__ __launch_bounds__(GQ_THREADS) void k_gelu_quant_q8k_h16(const q2a_half * __restrict__ X, int64_t nblocks, int bpr,
+                                                                   const uint16_t * __restrict__ gelu_c, q2a_half * outH,
+                                                                   float * dy, q2a_half * aext, int ld) {
+    __shared__ __attribute__((aligned(16))) uint16_t lut[Q2A_GELU_C_BYTES / 2];
+    for (int i = threadIdx.x; i < Q2A_GELU_C_BYTES / 16; i += GQ_THREADS)
+        ((uint4 *) lut)[i] = ((const uint4 *) gelu_c)[i];
+    __syncthreads();
+    const int lane = threadIdx.x & 63, sub = lane & 15;
+    const int64_t waves = (int64_t) gridDim.x * (GQ_THREADS / 64);
+    typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
+    for (int64_t wg4 = (int64_t) blockIdx.x * (GQ_THREADS / 64) + (threadIdx.x >> 6); wg4 * 4 < nblocks; wg4 += waves) {
+        const int64_t blk = wg4 * 4 + (lane >> 4);
+        if (blk >= nblocks) continue;
+        const int64_t m = blk / bpr;
+        const int bf = (int) (blk - m * bpr);
+        const h8_t * src = (const h8_t *) (X + blk * 256 + sub * 16);
+        const h8_t h0 = __builtin_nontemporal_load(src), h1 = __builtin_nontemporal_load(src + 1);
+        float v[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const _Float16 h = e < 8 ? h0[e] : h1[e - 8];
+            uint16_t u;
+            __builtin_memcpy(&u, &h, 2);
+            const uint16_t g = lut[(u & 0x7FFF) + ((u & 0x8000) ? Q2A_GELU_C_HALF : 0)];
+            _Float16 gh;
+            __builtin_memcpy(&gh, &g, 2);
+            const float x = (float) h;
+            v[e] = u == 0xFC00 ? 0.0f : x >= 10.0f ? x : (float) gh;
+        }
+        quant_q8k_row16(v, sub, outH + blk * 256 + sub * 16, dy + (int64_t) bf * ld + m, aext + ((int64_t) bf * ld + m) * 16);
+    }
+}
+
 // AvgPool1d(k=2,s=2) over time (ggml.c:15077-15125: drow = 0; += a; += b; /= 2) + final LayerNorm -> f32
 __global__ __launch_bounds__(256) void k_pool_ln(const q2a_pool_args p) {
     const int lane = threadIdx.x & 63;
@@ -402,6 +441,19 @@ hipError_t q2a_launch_layernorm(const q2a_ln_args & a, hipStream_t s) {
         hipLaunchKernelGGL((k_rownorm<1, true, false, 5>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else if (a.mode == 1) hipLaunchKernelGGL((k_rownorm<1, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else hipLaunchKernelGGL((k_rownorm<2, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
+    return hipGetLastError();
+}
+
+hipError_t q2a_launch_gelu_quant_q8k(const q2a_half * XH, int M, int K, const uint16_t * gelu_c, q2a_half * outH,
+                                     float * dy, q2a_half * aext, int dy_ld, hipStream_t s) {
+    if (K % 256 != 0 || M <= 0) return hipErrorInvalidValue;
+    int dev = 0, ncu = 256;
+    (void) hipGetDevice(&dev);
+    (void) hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t nb = (int64_t) M * (K / 256);
+    const int64_t need = (nb + 4 * (GQ_THREADS / 64) - 1) / (4 * (GQ_THREADS / 64));
+    const unsigned grid = (unsigned) std::min<int64_t>(need, 2 * (int64_t) ncu);   // two 80 KiB tables per CU
+    hipLaunchKernelGGL(k_gelu_quant_q8k_h16, dim3(grid), dim3(GQ_THREADS), 0, s, XH, nb, K / 256, gelu_c, outH, dy, aext, dy_ld);
     return hipGetLastError();
 }
 

@@ -788,10 +788,11 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
             }
             __syncthreads();
         }
-    } else if (EPI == Q2A_EPI_QKV || EPI == Q2A_EPI_GELU_H) {
+    } else if (EPI == Q2A_EPI_QKV || EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_PRE_H) {
         // output row remap (conv1's padded per-clip rows): one division per wave, its rows span < o_rpg
-        const int oq = (EPI == Q2A_EPI_GELU_H && p.o_rpg < p.M) ? rbase / p.o_rpg : 0;
-        const int orr = EPI == Q2A_EPI_GELU_H ? rbase - oq * p.o_rpg : 0;
+        constexpr bool REMAP = EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_PRE_H;
+        const int oq = (REMAP && p.o_rpg < p.M) ? rbase / p.o_rpg : 0;
+        const int orr = REMAP ? rbase - oq * p.o_rpg : 0;
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
             const int ml = i * 16 + l16, m = rbase + ml;
@@ -807,6 +808,10 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                             ha[r] = to16<true>((float) ha[r]);
                             hb[r] = to16<true>((float) hb[r]);
                         }
+                    } else if (EPI == Q2A_EPI_PRE_H) {   // pre-activation; x <= -10 marked -inf (GELU = 0)
+                        const float va = val(i, 2 * jp, r), vb = val(i, 2 * jp + 1, r);
+                        ha[r] = va <= -10.0f ? (_Float16) -INFINITY : (_Float16) va;
+                        hb[r] = vb <= -10.0f ? (_Float16) -INFINITY : (_Float16) vb;
                     } else {
                         const float va = val(i, 2 * jp, r), vb = val(i, 2 * jp + 1, r);
                         ha[r] = to16<BF>(va);
@@ -822,7 +827,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                 if (EPI == Q2A_EPI_QKV && !BF) lv = pair16(la, lb);
                 if (m < p.M) {
                     const int col = 32 * jp + pcol;
-                    if (EPI == Q2A_EPI_GELU_H) {
+                    if (REMAP) {
                         const bool wrap = orr + ml >= p.o_rpg;
                         const int64_t row = (int64_t) (oq + (wrap ? 1 : 0)) * p.o_gstride + (orr + ml - (wrap ? p.o_rpg : 0)) + p.o_off;
                         if (Q2A_ST) q2a_st(hv, (uint4 *) (p.outH + row * p.ldo + cbase + col));
@@ -948,6 +953,7 @@ hipError_t q2a_launch_gemm(const q2a_gemm_args & a_in, int epi, int blk, hipStre
         case Q2A_EPI_GELU_F: return launch_epi<Q2A_EPI_GELU_F>(a, blk, s);
         case Q2A_EPI_STORE_F: return launch_epi<Q2A_EPI_STORE_F>(a, blk, s);
         case Q2A_EPI_GELU_Q8K: return launch_epi<Q2A_EPI_GELU_Q8K>(a, blk, s);
+        case Q2A_EPI_PRE_H: return launch_epi<Q2A_EPI_PRE_H>(a, blk, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -17,6 +17,8 @@ enum q2a_epi {
     Q2A_EPI_STORE_F = 5,    // outF[m][n] = acc                                   (unit tests)
     Q2A_EPI_GELU_Q8K = 6,   // gelu_lut(acc + bias) quantized to Q8_K in-tile: codes -> outH, d -> dy, bsums -> aext
                             // (fc1 on the Q4_K path; needs the 256-column tile = one Q8_K block per row)
+    Q2A_EPI_PRE_H = 7,      // outH[m][n] = x <= -10 ? -inf : fp16(x), x = acc + bias[n]: the fc1 pre-activation,
+                            // whose GELU (the fp16 LUT) the Q8_K quantizer applies (q2a_launch_gelu_quant_q8k)
 };
 
 // compact GELU table: entries for fp16 bits 0x0000..0x4900 (+0..+10) then 0x8000..0xC900 (-0..-10), padded to
@@ -136,6 +138,10 @@ struct q2a_quant_args {
     int dy_ld;
 };
 hipError_t q2a_launch_quant_act(const q2a_quant_args & a, hipStream_t s);
+// GELU (compact fp16 LUT image gelu_c, staged in LDS) of an fp16 pre-activation written by Q2A_EPI_PRE_H, then Q8_K
+// quantization — the same codes as Q2A_EPI_GELU_H + q2a_launch_quant_act(mode 1, XH). XH [M][K], K % 256 == 0.
+hipError_t q2a_launch_gelu_quant_q8k(const q2a_half * XH, int M, int K, const uint16_t * gelu_c, q2a_half * outH,
+                                     float * dy, q2a_half * aext, int dy_ld, hipStream_t s);
 
 // One ggml weight matrix [N][K] (raw ggml rows, host memory; F16 / Q4_K / Q8_0 / Q4_0) packed into the GEMM's
 // operand layout: fp16 W' [N][K] plus the block-major scale arrays, at byte offsets off[0..5] = W, DX, DMIN, WEXT,

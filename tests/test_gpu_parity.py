@@ -252,3 +252,23 @@ def test_block_batched_matches_oracle_layer0(engines, make_model, make_clip, wt,
     for c in (0, B - 1):
         mx, l2 = rel_errors(out[c], dumps["x2"])
         assert l2 < tol_l2, (c, mx, l2)
+
+
+# ---------------------------------------------------------------- deferred GELU (Q4_K fc1 -> Q8_K quantizer)
+@pytest.mark.parametrize("n_clips", [1, 30])
+def test_deferred_gelu_equals_epilogue_gelu(make_model, make_clip, n_clips, monkeypatch):
+    """Q4_K fc1 writes its fp16 pre-activation (Q2A_EPI_PRE_H) and the Q8_K quantizer applies the GELU table; the
+    codes, hence every output bit, must equal the GELU-epilogue + quantizer path (Q2A_GELU_IN_EPI=1)."""
+    import q2a
+    path = make_model("tiny", "q4_k")
+    clips = [make_clip(0)] * n_clips
+    monkeypatch.setenv("Q2A_GELU_IN_EPI", "1")
+    e1 = q2a.Engine(path, device=0)
+    monkeypatch.setenv("Q2A_GELU_IN_EPI", "0")
+    e0 = q2a.Engine(path, device=0)
+    try:
+        o1, _ = e1.encode_host(clips)
+        o0, _ = e0.encode_host(clips)
+        assert np.array_equal(o0, o1)
+    finally:
+        e0.close(); e1.close()
