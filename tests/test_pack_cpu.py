@@ -1,0 +1,71 @@
+"""CPU checks of the host-side packer behind q2a_pack_model_ex (no GPU needed: packing is host code).
+
+The blob is self-describing (csrc/q2a_engine.hip `blob_header`): its header records the activation contract, and
+under Q2A_ACT_BF16 every linear weight is ggml's dequantize_row_* rounded to bf16 — checked here bit
+for bit against a numpy restatement of dequantize_row_q8_0 (ggml-quants.c) for the fused q|k|v matrix of layer 0.
+"""
+import ctypes as C
+import struct
+
+import numpy as np
+import pytest
+
+from q2a import ggmlfile
+
+# blob_header layout: u32 magic, version | 11 x i32 hparams | i32 wtype, blk, n_bins, act | u64 total |
+# u64 goff[11] | u64 loff[64][32]
+OFF_WTYPE, OFF_BLK, OFF_ACT, OFF_TOTAL, OFF_GOFF = 52, 56, 64, 72, 80
+G_COUNT, L_COUNT, L_MAT0, A_COUNT, A_W, A_DX = 11, 32, 8, 6, 0, 1
+
+
+def header(blob: bytes):
+    wtype, blk = struct.unpack_from("<ii", blob, OFF_WTYPE)
+    act, = struct.unpack_from("<i", blob, OFF_ACT)
+    total, = struct.unpack_from("<Q", blob, OFF_TOTAL)
+    loff0 = struct.unpack_from(f"<{L_COUNT}Q", blob, OFF_GOFF + 8 * G_COUNT)
+    return wtype, blk, act, total, loff0
+
+
+def bf16_bits(x: np.ndarray) -> np.ndarray:
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    return ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+
+
+def dequant_q8_0(t) -> np.ndarray:
+    K = t.ne[0]
+    rows = int(np.prod(t.ne)) // K
+    blk = t.data.reshape(rows, K // 32, 34)
+    d = blk[:, :, :2].copy().view(np.float16).astype(np.float32)
+    q = blk[:, :, 2:].copy().view(np.int8).astype(np.float32)
+    return (q * d).reshape(rows, K)
+
+
+def test_bf16_blob_holds_dequantized_bf16_weights(make_model):
+    import q2a
+    path = make_model("tiny", "q8_0")
+    ref_blob = q2a.pack_model(path)
+    bf_blob = q2a.pack_model(path, q2a.ACT_BF16)
+    wt, blk, act, total, _ = header(ref_blob)
+    assert (wt, blk, act, total) == (8, 32, q2a.ACT_REFERENCE, len(ref_blob))
+    wt, blk, act, total, loff0 = header(bf_blob)
+    assert (wt, blk, act, total) == (8, 0, q2a.ACT_BF16, len(bf_blob))
+    assert loff0[L_MAT0 + A_DX] == 0   # no block-scale arrays in the bf16 layout
+    mf = ggmlfile.read(path)
+    D = 256
+    want = np.concatenate([bf16_bits(dequant_q8_0(mf.t(f"layers.0.self_attn.{n}_proj.weight"))) for n in "qkv"])
+    off = loff0[L_MAT0 + A_W]
+    got = np.frombuffer(bf_blob, dtype=np.uint16, count=3 * D * D, offset=off).reshape(3 * D, D)
+    assert np.array_equal(got, want)
+
+
+def test_unknown_activation_contract_is_rejected(make_model):
+    """q2a_open_ex / q2a_pack_model_ex validate the contract before touching a device."""
+    import q2a
+    path = make_model("tiny", "f16")
+    L = q2a.lib()
+    assert not L.q2a_open_ex(path.encode(), 0, 7)
+    assert b"activation mode" in L.q2a_last_error()
+    p = C.c_void_p()
+    assert L.q2a_pack_model_ex(path.encode(), 7, C.byref(p)) < 0
+    with pytest.raises(q2a.Q2AError):
+        q2a.pack_model(path, 7)
