@@ -264,7 +264,9 @@ def main():
                    "seq_len": T_MEL, "parallelism": f"dp{ws}"},
         "clips_per_s": round(total_clips / elapsed, 3),
         "tflops_total": round(FLOP_PER_CLIP * total_clips / elapsed / 1e12, 1),
-        "roofline": {"bound": "mfma", "kernel": "gemm_fc1 (k_gemm<GELU, blk>), M=%d N=5120 K=1280" % (T * clips_per_gpu),
+        "roofline": {"bound": "mfma", "kernel": "gemm_fc1 (k_gemm<256,256,2,4,%s>), M=%d N=5120 K=1280" % (
+                         {"q4_k": "PRE_H,256,1", "f16": "GELU_H,0,1", "q8_0": "GELU_H,32,0"}[wt] if "bf16" not in args.config
+                         else "GELU_H,BF16,1", T * clips_per_gpu),
                      "achieved": round(achieved, 1), "peak": PEAK_FP16_MFMA_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_FP16_MFMA_TFLOPS, 4), "traffic": traffic,
                      "traffic_unit": "bytes/launch", "traffic_source": traffic_src,

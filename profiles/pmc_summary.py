@@ -13,7 +13,7 @@ import re
 import sys
 from collections import defaultdict
 
-EPI = {0: "qkv", 1: "resid", 2: "gelu_h", 3: "conv2", 4: "gelu_f", 5: "store_f", 6: "gelu_q8k"}
+EPI = {0: "qkv", 1: "resid", 2: "gelu_h", 3: "conv2", 4: "gelu_f", 5: "store_f", 6: "gelu_q8k", 7: "pre_h"}
 
 
 def classify(name: str) -> str:
@@ -31,7 +31,7 @@ def classify(name: str) -> str:
         return "conv2"
     if epi == 2 and blk == 0:
         return "gelu_h_fp16 (conv1, and fc1 on F16 models)"
-    if epi in (2, 4, 6):
+    if epi in (2, 4, 6, 7):
         return "gemm_fc1"
     return EPI.get(epi, str(epi))
 

@@ -34,6 +34,11 @@ typedef __attribute__((address_space(3))) void * lds_ptr_t;
 
 // timing diagnostic Q2A_DIAG_NO_STORE (wrong results): the epilogue computes every value but its global stores
 // are predicated off by a condition the compiler cannot fold
+#ifdef Q2A_DIAG_NO_VT_STORE   // timing diagnostic: only the V^T scatter stores predicated off
+#define Q2A_ST_VT (p.K < 0)
+#else
+#define Q2A_ST_VT true
+#endif
 #ifdef Q2A_DIAG_NO_STORE
 #define Q2A_ST (p.K < 0)
 #else
@@ -784,7 +789,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                 const bool wrap = t0 + 4 * a >= p.T;
                 const int clip = clip0 + (wrap ? 1 : 0), t = t0 + 4 * a - (wrap ? p.T : 0);
                 const uint2 v = *(const uint2 *) ((const _Float16 *) wl + lane * (PR + 4) + 4 * a);
-                if (Q2A_ST) q2a_st(v, (uint2 *) (p.vt + (((int64_t) clip * p.H + h) * 64 + d) * p.TP + t));
+                if (Q2A_ST && Q2A_ST_VT) q2a_st(v, (uint2 *) (p.vt + (((int64_t) clip * p.H + h) * 64 + d) * p.TP + t));
             }
             __syncthreads();
         }
