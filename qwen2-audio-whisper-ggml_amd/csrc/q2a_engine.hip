@@ -533,6 +533,7 @@ struct q2a_engine {
     q2a_half *qh = nullptr, *ql = nullptr, *kh = nullptr, *kl = nullptr, *vt = nullptr;
     float * attF = nullptr;
     float * hF = nullptr;
+    float * part = nullptr;          // split-K partials of the small-tile residual GEMMs (NULL: big batches)
     int2 * frange = nullptr;         // per mel filter: non-zero bin-group range (computed once from the blob)
     int TP = 0;
     int dy_ld = 0;
@@ -613,7 +614,13 @@ int reserve(q2a_engine * e, int B) {
     const size_t o_kh = take((size_t) BT * d.D * 2);
     const size_t o_kl = take((size_t) BT * d.D * 2);
     const size_t o_vt = take((size_t) B * d.H * 64 * e->TP * 2);
-    size_t o_dyD = 0, o_dyF = 0, o_aD = 0, o_aF = 0, o_att = 0, o_hF = 0;
+    size_t o_dyD = 0, o_dyF = 0, o_aD = 0, o_aF = 0, o_att = 0, o_hF = 0, o_part = 0;
+    // split-K partials of the small-tile residual GEMMs (O-proj, fc2): up to 4 x [rows][D] f32. Sized for every
+    // row count that takes the small-tile path (M <= 26 112 at D = 1280), whatever the capacity, so whether a
+    // batch splits never depends on what the engine encoded before
+    const int64_t split_rows = std::min<int64_t>(BT, 32768);
+    const bool split = !q2a_gemm_wide_tiles((int) split_rows, d.D, e->gblk);
+    if (split) o_part = take((size_t) 4 * split_rows * d.D * 4);
     const int64_t MP = (BT + 255) / 256 * 256;   // padded row stride of the block-major scale arrays
     e->dy_ld = (int) MP;
     if (quant) {
@@ -646,6 +653,7 @@ int reserve(q2a_engine * e, int B) {
     e->qh = (q2a_half *) (b + o_qh); e->ql = (q2a_half *) (b + o_ql);
     e->kh = (q2a_half *) (b + o_kh); e->kl = (q2a_half *) (b + o_kl);
     e->vt = (q2a_half *) (b + o_vt);
+    e->part = split ? (float *) (b + o_part) : nullptr;
     if (quant) {
         e->dyD = (float *) (b + o_dyD); e->dyF = (float *) (b + o_dyF);
         e->aextD = (q2a_half *) (b + o_aD); e->aextF = (q2a_half *) (b + o_aF);
@@ -746,6 +754,7 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         q2a_gemm_args a = gemm_base(e, l, 1, e->actD, M);
         a.bias = e->lv<const float *>(l, L_BO);
         a.outF = e->X; a.ldo = d.D;
+        a.part = e->part; a.split_stride = (int64_t) M * d.D;
         PLAUNCH(e, s, Q2A_PROF_GEMM_O, q2a_launch_gemm(a, Q2A_EPI_RESID, e->gblk, s));
     }
     q2a_ln_args ln2{e->X, M, d.D, e->lv<const float *>(l, L_LN2W), e->lv<const float *>(l, L_LN2B), mode, e->actD, e->dyD, e->aextD, e->dy_ld};
@@ -785,6 +794,7 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         q2a_gemm_args a = gemm_base(e, l, 3, e->actF, M);
         a.bias = e->lv<const float *>(l, L_B2);
         a.outF = e->X; a.ldo = d.D;
+        a.part = e->part; a.split_stride = (int64_t) M * d.D;
         PLAUNCH(e, s, Q2A_PROF_GEMM_FC2, q2a_launch_gemm(a, Q2A_EPI_RESID, e->gblk, s));
     }
     return Q2A_OK;

@@ -449,9 +449,11 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (__builtin_amdgcn_s_memrealtime() - t0 < dt) __builtin_amdgcn_s_sleep(8);
     }
-    const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, nwg = nbn * nbm;
+    const int ksplit = (!PIPE && BLK == 0 && EPI == Q2A_EPI_RESID && p.ksplit > 1) ? p.ksplit : 1;
+    const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, ntl = nbn * nbm, nwg = ntl * ksplit;
     const int bid = blockIdx.x, xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
-    const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+    const int wgid_all = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+    const int ks = wgid_all / ntl, wgid = wgid_all - ks * ntl;   // K-split index, tile index
     const int gsize = GROUP_M * nbn, g = wgid / gsize, gr = wgid % gsize;
     const int gm = min(GROUP_M, nbm - g * GROUP_M);
     const int tm = g * GROUP_M + gr % gm, tn = gr / gm;
@@ -530,8 +532,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                 for (int j = 0; j < (BLK ? NJ : 1); ++j) blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
         }
 
-        const int nk = p.K / BK;
-        stage(LDS_STAGE(0), 0);
+        const int nk = p.K / BK / ksplit;                 // K-steps of this split
+        const int kb0 = ks * nk * BK;                     // its first K element
+        stage(LDS_STAGE(0), kb0);
         if (BLK == 32) scale_load(0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (BLK == 32) scale_store(0);
@@ -539,7 +542,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
 
         for (int kt = 0; kt < nk; ++kt) {
             const int cur = kt & 1;
-            if (kt + 1 < nk) stage(LDS_STAGE(cur ^ 1), (kt + 1) * BK);
+            if (kt + 1 < nk) stage(LDS_STAGE(cur ^ 1), kb0 + (kt + 1) * BK);
             // Q4_K: block kt/4's scales are fetched at its first K-step and land in LDS at its end (3 steps early);
             // Q8_0: the next K-step's two blocks are fetched one step ahead into the other buffer.
             const bool sload = BLK == 256 ? (kt % 4 == 0) : (BLK == 32 && kt + 1 < nk);
@@ -845,6 +848,16 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                 }
             }
         }
+    } else if (EPI == Q2A_EPI_RESID && ksplit > 1) {
+        // split-K partial: raw accumulators to part[ks] ([M][N] f32); bias and residual in the reduce pass
+        float * pb = p.part + (int64_t) ks * p.split_stride;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+            const int m = rbase + i * 16 + l16;
+            if (m >= p.M) continue;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) *(f4 *) (pb + (int64_t) m * p.N + cbase + j * 16 + 4 * q) = acc[i][j];
+        }
     } else {
         // f32 outputs: residual add (O-proj, fc2), GELU (+ positional rows for conv2), plain store
         const int pq = EPI == Q2A_EPI_CONV2 ? rbase / p.T : 0;
@@ -880,10 +893,36 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
 #undef LDS_STAGE
 }
 
+// split-K reduce: out[m][n] = ((p_0 + p_1 + ...) + bias[n]) + out[m][n], partials summed in split order
+__global__ void k_split_reduce(const float * __restrict__ part, int S, int64_t stride, int M, int N, const float * bias,
+                               float * out, int64_t ldo) {
+    const int64_t i4 = ((int64_t) blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i4 >= (int64_t) M * N) return;
+    const int m = (int) (i4 / N), n = (int) (i4 - (int64_t) m * N);
+    f4 acc = *(const f4 *) (part + i4);
+    for (int s = 1; s < S; ++s) {
+        const f4 v = *(const f4 *) (part + s * stride + i4);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = acc[r] + v[r];
+    }
+    const f4 b = *(const f4 *) (bias + n);
+    f4 * o = (f4 *) (out + (int64_t) m * ldo + n);
+    f4 x = *o;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x[r] = (acc[r] + b[r]) + x[r];
+    *o = x;
+}
+
 template <int BM, int BN, int WM, int WN, int EPI, int BLK, int PIPE = 0>
 hipError_t launch_cfg(const q2a_gemm_args & a, hipStream_t s) {
-    const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM);
+    const bool split = !PIPE && (BLK == 0 || BLK == Q2A_BLK_BF16) && EPI == Q2A_EPI_RESID && a.ksplit > 1;
+    const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM) * (split ? a.ksplit : 1);
     hipLaunchKernelGGL((k_gemm<BM, BN, WM, WN, EPI, BLK, PIPE>), dim3(nwg), dim3(WM * WN * 64), 0, s, a);
+    if (split) {
+        const int64_t n4 = (int64_t) a.M * a.N / 4;
+        hipLaunchKernelGGL(k_split_reduce, dim3((unsigned) ((n4 + 255) / 256)), dim3(256), 0, s, a.part, a.ksplit,
+                           a.split_stride, a.M, a.N, a.bias, a.outF, a.ldo);
+    }
     return hipGetLastError();
 }
 
@@ -943,11 +982,21 @@ hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
 
 }  // namespace
 
+int q2a_gemm_resid_ksplit(int M, int N, int K, int blk) {
+    static const int off = [] { const char * v = getenv("Q2A_GEMM_NO_SPLITK"); return v ? atoi(v) : 0; }();
+    if (off || !(blk == 0 || blk == Q2A_BLK_BF16) || wide_tiles(M, N) || N % 128) return 0;
+    const int nk = K / BK;
+    const int S = K >= 4096 ? 4 : K >= 1024 ? 2 : 0;
+    return S && nk % S == 0 ? S : 0;
+}
+
 hipError_t q2a_launch_gemm(const q2a_gemm_args & a_in, int epi, int blk, hipStream_t s) {
     static const int st_ns = [] { const char * v = getenv("Q2A_GEMM_STAGGER_NS"); return v ? atoi(v) : 0; }();
     static const int st_g = [] { const char * v = getenv("Q2A_GEMM_STAGGER_G"); return v ? std::max(1, atoi(v)) : 2; }();
     q2a_gemm_args a = a_in;
     a.stagger_ns = st_ns; a.stagger_g = st_g;
+    if (epi != Q2A_EPI_RESID || !a.part || a.ldo != a.N) a.ksplit = 0;
+    else a.ksplit = q2a_gemm_resid_ksplit(a.M, a.N, a.K, blk);
     if (a.N % 128 != 0 || a.K % BK != 0 || a.M <= 0) return hipErrorInvalidValue;
     if (blk > 1 && (a.K % blk != 0)) return hipErrorInvalidValue;
     switch (epi) {

@@ -62,10 +62,18 @@ struct q2a_gemm_args {
     float * qdy;                      // Q2A_EPI_GELU_Q8K outputs: block-major d [N/256][dy_ld] and
     q2a_half * qaext;                 //   bsum operand [N/256][dy_ld][16] of the produced activation
     int nblk;
+    // deterministic split-K of the small-tile residual GEMMs (set by the launcher): split s of ksplit writes its
+    // partial sum to part + s * split_stride ([M][N] f32) and a reduce pass applies ((p0 + p1 ...) + bias) + x
+    int ksplit;
+    float * part;
+    int64_t split_stride;
     int stagger_ns, stagger_g;        // diagnostic (Q2A_GEMM_STAGGER_NS/_G): first-round phase offsets per CU group
     int dy_ld;                        // row stride of dy/aext (M rounded up to 256)
 };
 
+// the launcher's split factor for a small-tile Q2A_EPI_RESID GEMM (0 = none): a function of K only, so every batch
+// size on the small-tile path sums in the same order (batch and single-clip results stay bit-identical)
+int q2a_gemm_resid_ksplit(int M, int N, int K, int blk);
 // blk: 0 (plain fp16 GEMM), 256 (Q4_K x Q8_K), 32 (Q8_0/Q4_0 x Q8_0), Q2A_BLK_BF16 (bf16 x bf16 MFMA, no block
 // scales: the bf16-activation mode, whose fp16-typed operand and output pointers then hold bf16 bits)
 constexpr int Q2A_BLK_BF16 = 1;
