@@ -60,7 +60,7 @@ __device__ __forceinline__ void q2a_st(const V & v, V * ptr) {
 
 constexpr int BK = 64;
 constexpr int ROWB = BK * 2;   // bytes per LDS row (64 halves)
-constexpr int GROUP_M = 8;
+constexpr int GROUP_M = 4;   // swept 2..32 at the batched shapes (Q2A_GEMM_GROUP_M): 4 best by ~1 %
 
 __device__ __forceinline__ float gelu_lut(float x, const uint16_t * tab) {
     // ggml_vec_gelu_f32 with GGML_GELU_FP16 (ggml.c:2556-2570)
@@ -454,9 +454,10 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
     const int bid = blockIdx.x, xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
     const int wgid_all = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
     const int ks = wgid_all / ntl, wgid = wgid_all - ks * ntl;   // K-split index, tile index
-    const int gsize = GROUP_M * nbn, g = wgid / gsize, gr = wgid % gsize;
-    const int gm = min(GROUP_M, nbm - g * GROUP_M);
-    const int tm = g * GROUP_M + gr % gm, tn = gr / gm;
+    const int GM = p.group_m > 0 ? p.group_m : GROUP_M;
+    const int gsize = GM * nbn, g = wgid / gsize, gr = wgid % gsize;
+    const int gm = min(GM, nbm - g * GM);
+    const int tm = g * GM + gr % gm, tn = gr / gm;
     const int m0 = tm * BM, n0 = tn * BN;
 
     f4 acc[MI][NJ];
@@ -993,8 +994,10 @@ int q2a_gemm_resid_ksplit(int M, int N, int K, int blk) {
 hipError_t q2a_launch_gemm(const q2a_gemm_args & a_in, int epi, int blk, hipStream_t s) {
     static const int st_ns = [] { const char * v = getenv("Q2A_GEMM_STAGGER_NS"); return v ? atoi(v) : 0; }();
     static const int st_g = [] { const char * v = getenv("Q2A_GEMM_STAGGER_G"); return v ? std::max(1, atoi(v)) : 2; }();
+    static const int grp = [] { const char * v = getenv("Q2A_GEMM_GROUP_M"); return v ? atoi(v) : 0; }();
     q2a_gemm_args a = a_in;
     a.stagger_ns = st_ns; a.stagger_g = st_g;
+    a.group_m = grp;
     if (epi != Q2A_EPI_RESID || !a.part || a.ldo != a.N) a.ksplit = 0;
     else a.ksplit = q2a_gemm_resid_ksplit(a.M, a.N, a.K, blk);
     if (a.N % 128 != 0 || a.K % BK != 0 || a.M <= 0) return hipErrorInvalidValue;
