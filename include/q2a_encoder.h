@@ -123,6 +123,8 @@ enum {
     Q2A_PROF_QUANT, Q2A_PROF_GEMM_O, Q2A_PROF_GEMM_FC1, Q2A_PROF_GEMM_FC2, Q2A_PROF_POOL, Q2A_PROF_CLASSES
 };
 int q2a_profile_enable(q2a_engine * e, int on);
+/* time only the classes whose bit (1 << Q2A_PROF_*) is set (0 = off): fewer event pairs in a timed loop */
+int q2a_profile_enable_mask(q2a_engine * e, unsigned mask);
 /* accumulated milliseconds and launch counts per class (waits for the recorded events); reset != 0 clears */
 int q2a_profile_read(q2a_engine * e, double * ms, int64_t * counts, int n, int reset);
 

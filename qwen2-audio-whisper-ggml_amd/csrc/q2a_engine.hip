@@ -549,6 +549,7 @@ struct q2a_engine {
     struct rec { int cls; hipEvent_t a, b; };
     std::vector<rec> pending;
     std::vector<hipEvent_t> pool;
+    unsigned prof_mask = ~0u;        // classes timed when prof is on (bit = Q2A_PROF_*)
     double prof_ms[Q2A_PROF_CLASSES] = {};
     int64_t prof_n[Q2A_PROF_CLASSES] = {};
 
@@ -704,13 +705,14 @@ hipEvent_t prof_event(q2a_engine * e) {
 #define PLAUNCH(e, s, cls, call)                                                      \
     do {                                                                              \
         q2a_engine::rec r_{cls, nullptr, nullptr};                                    \
-        if ((e)->prof) { r_.a = prof_event(e); r_.b = prof_event(e); (void) hipEventRecord(r_.a, s); } \
+        const bool on_ = (e)->prof && (((e)->prof_mask >> (cls)) & 1);                 \
+        if (on_) { r_.a = prof_event(e); r_.b = prof_event(e); (void) hipEventRecord(r_.a, s); } \
         hipError_t e_ = (call);                                                       \
         if (e_ != hipSuccess) {                                                       \
             set_err("%s: %s", #call, hipGetErrorString(e_));                        \
             return Q2A_ERR_HIP;                                                       \
         }                                                                             \
-        if ((e)->prof) { (void) hipEventRecord(r_.b, s); (e)->pending.push_back(r_); } \
+        if (on_) { (void) hipEventRecord(r_.b, s); (e)->pending.push_back(r_); }      \
     } while (0)
 
 int ln_mode(const q2a_engine * e) { return e->bf16 ? 4 : e->f32 ? 3 : e->blk == 0 ? 0 : e->blk == 256 ? 1 : 2; }
@@ -1111,6 +1113,14 @@ int q2a_pcm_to_mel(q2a_engine * e, const float * pcm, int n_samples, float * mel
 int q2a_profile_enable(q2a_engine * e, int on) {
     if (!e) return Q2A_ERR_ARG;
     e->prof = on != 0;
+    e->prof_mask = ~0u;
+    return Q2A_OK;
+}
+
+int q2a_profile_enable_mask(q2a_engine * e, unsigned mask) {
+    if (!e) return Q2A_ERR_ARG;
+    e->prof = mask != 0;
+    e->prof_mask = mask;
     return Q2A_OK;
 }
 
