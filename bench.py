@@ -113,7 +113,7 @@ def main():
     ap.add_argument("--config", default="q4k64", choices=sorted(CONFIGS))
     ap.add_argument("--clips", type=int, default=0, help="override clips per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-reps", type=int, default=2)
+    ap.add_argument("--cpu-reps", type=int, default=4)   # ~13 s of reference CPU work on 16 threads
     ap.add_argument("--workdir", default=os.environ.get("Q2A_BENCH_DIR", os.path.join(tempfile.gettempdir(), "q2a_bench")))
     args = ap.parse_args()
 
