@@ -8,20 +8,32 @@
 
 namespace {
 
+// The Q8_K scale comes from the signed value of the FIRST element (in row order) whose |x| is the block maximum
+// (quantize_row_q8_K_ref's strict '>' scan, :3793-3798). Found in two cheap steps instead of carrying
+// (|x|, x, index) through every reduction step: (1) a plain max of |x| over the block's lanes, (2) a ballot of
+// the lanes holding an element equal to it — the lowest such lane holds the first occurrence (elements are laid out
+// in lane order), and its own first matching element gives the sign. `first_e` = that lane's first index with
+// |x| == amax (or 4/16 if none); lane order = element order within the block.
+__device__ __forceinline__ float first_max_value(float amax, float local_first, bool has, int lane, int group_lanes) {
+    const unsigned long long m = __ballot(has);
+    const int g0 = lane & ~(group_lanes - 1);
+    const unsigned long long gm = group_lanes == 64 ? m : (m >> g0) & ((1ull << group_lanes) - 1);
+    const int src = g0 + (gm ? __builtin_ctzll(gm) : 0);
+    const float v = __shfl(local_first, src);
+    return gm ? v : amax;
+}
+
 // quantize one 256-block (one float4 per lane) to Q8_K codes; writes codes, d and the bsum hi/lo operand
 __device__ __forceinline__ void quant_q8k_block(float4 y, int lane, q2a_half * codes, float * dy_out, q2a_half * aext) {
     // max |x| and the signed value of its FIRST occurrence (strict '>' scan, :3793-3798)
-    float av[4] = {fabsf(y.x), fabsf(y.y), fabsf(y.z), fabsf(y.w)};
     float vv[4] = {y.x, y.y, y.z, y.w};
-    float amax = av[0], mx = vv[0];
-    int idx = lane * 4;
-    for (int e = 1; e < 4; ++e)
-        if (av[e] > amax) { amax = av[e]; mx = vv[e]; idx = lane * 4 + e; }
-    for (int o = 32; o > 0; o >>= 1) {
-        const float a2 = __shfl_xor(amax, o), m2 = __shfl_xor(mx, o);
-        const int i2 = __shfl_xor(idx, o);
-        if (a2 > amax || (a2 == amax && i2 < idx)) { amax = a2; mx = m2; idx = i2; }
-    }
+    float amax = fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w)));
+    for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+    float lf = 0.f;
+    bool has = false;
+    for (int e = 3; e >= 0; --e)
+        if (fabsf(vv[e]) == amax) { lf = vv[e]; has = true; }
+    const float mx = first_max_value(amax, lf, has, lane, 64);
     int q[4] = {0, 0, 0, 0};
     float d = 1.f;   // all-zero block (ggml stores 0): the codes are 0 so d never contributes; a nonzero d keeps
                      // the block-ratio rescaling of the wide Q4_K GEMM finite
@@ -62,17 +74,18 @@ __device__ __forceinline__ float swz_xor_f(float v, int o) { return __int_as_flo
 
 __device__ __forceinline__ void quant_q8k_row16(const float (&v)[16], int sub, q2a_half * codes, float * dy_out,
                                                 q2a_half * aext) {
-    float amax = fabsf(v[0]), mx = v[0];
-    int idx = sub * 16;
+    float amax = fabsf(v[0]);
 #pragma unroll
-    for (int e = 1; e < 16; ++e)
-        if (fabsf(v[e]) > amax) { amax = fabsf(v[e]); mx = v[e]; idx = sub * 16 + e; }
+    for (int e = 1; e < 16; ++e) amax = fmaxf(amax, fabsf(v[e]));
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) {
-        const float a2 = swz_xor_f(amax, o), m2 = swz_xor_f(mx, o);
-        const int i2 = swz_xor_i(idx, o);
-        if (a2 > amax || (a2 == amax && i2 < idx)) { amax = a2; mx = m2; idx = i2; }
-    }
+    for (int o = 1; o < 16; o <<= 1) amax = fmaxf(amax, swz_xor_f(amax, o));
+    float lf = 0.f;
+    bool has = false;
+#pragma unroll
+    for (int e = 15; e >= 0; --e)
+        if (fabsf(v[e]) == amax) { lf = v[e]; has = true; }
+    const int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    const float mx = first_max_value(amax, lf, has, lane, 16);
     int q[16];
     float d = 1.f;   // all-zero block: see quant_q8k_block
     if (amax != 0.f) {
@@ -107,24 +120,21 @@ template <int NB>
 __device__ __forceinline__ void quant_q8k_blocks(const float4 (&y)[NB], int lane, q2a_half * codes, int64_t code_stride,
                                                  float * dy_out, int64_t dy_stride, q2a_half * aext, int64_t aext_stride) {
     float amax[NB], mx[NB];
-    int idx[NB];
+#pragma unroll
+    for (int u = 0; u < NB; ++u) amax[u] = fmaxf(fmaxf(fabsf(y[u].x), fabsf(y[u].y)), fmaxf(fabsf(y[u].z), fabsf(y[u].w)));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int u = 0; u < NB; ++u) amax[u] = fmaxf(amax[u], __shfl_xor(amax[u], o));
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
         const float vv[4] = {y[u].x, y[u].y, y[u].z, y[u].w};
-        amax[u] = fabsf(vv[0]); mx[u] = vv[0]; idx[u] = lane * 4;
+        float lf = 0.f;
+        bool has = false;
 #pragma unroll
-        for (int e = 1; e < 4; ++e)
-            if (fabsf(vv[e]) > amax[u]) { amax[u] = fabsf(vv[e]); mx[u] = vv[e]; idx[u] = lane * 4 + e; }
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        float a2[NB], m2[NB];
-        int i2[NB];
-#pragma unroll
-        for (int u = 0; u < NB; ++u) { a2[u] = __shfl_xor(amax[u], o); m2[u] = __shfl_xor(mx[u], o); i2[u] = __shfl_xor(idx[u], o); }
-#pragma unroll
-        for (int u = 0; u < NB; ++u)
-            if (a2[u] > amax[u] || (a2[u] == amax[u] && i2[u] < idx[u])) { amax[u] = a2[u]; mx[u] = m2[u]; idx[u] = i2[u]; }
+        for (int e = 3; e >= 0; --e)
+            if (fabsf(vv[e]) == amax[u]) { lf = vv[e]; has = true; }
+        mx[u] = first_max_value(amax[u], lf, has, lane, 64);
     }
     int s[NB];
 #pragma unroll
