@@ -238,17 +238,21 @@ __global__ __launch_bounds__(256) void k_rownorm(const float * __restrict__ X, i
             if (c < nch) v[u] = x4[c];
         }
     }
-    if constexpr (MODE == 1 && LN && NBQ > 0) {
+    if constexpr (MODE == 1 && NBQ > 0) {
         // whole row resident: the NBQ Q8_K blocks of the row quantized with interleaved reductions
         float4 y[NBQ];
 #pragma unroll
         for (int u = 0; u < NBQ; ++u) {
-            const int c = lane + 64 * u;
-            const float4 gg = ((const float4 *) g)[c], bb = ((const float4 *) b)[c];
-            y[u].x = (v[u].x * scale) * gg.x + bb.x;
-            y[u].y = (v[u].y * scale) * gg.y + bb.y;
-            y[u].z = (v[u].z * scale) * gg.z + bb.z;
-            y[u].w = (v[u].w * scale) * gg.w + bb.w;
+            if (LN) {
+                const int c = lane + 64 * u;
+                const float4 gg = ((const float4 *) g)[c], bb = ((const float4 *) b)[c];
+                y[u].x = (v[u].x * scale) * gg.x + bb.x;
+                y[u].y = (v[u].y * scale) * gg.y + bb.y;
+                y[u].z = (v[u].z * scale) * gg.z + bb.z;
+                y[u].w = (v[u].w * scale) * gg.w + bb.w;
+            } else {
+                y[u] = v[u];
+            }
         }
         quant_q8k_blocks<NBQ>(y, lane, outH + (int64_t) row * D + 4 * lane, 256, dy + row, ld, aext + (int64_t) row * 16,
                               (int64_t) ld * 16);
@@ -473,6 +477,8 @@ hipError_t q2a_launch_quant_act(const q2a_quant_args & a, hipStream_t s) {
         hipLaunchKernelGGL((k_rownorm<1, false, true>), grid, blk, 0, s, X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext, nseg, a.dy_ld);
     } else if (a.mode == 2 && a.XH) {
         hipLaunchKernelGGL((k_rownorm<2, false, true>), grid, blk, 0, s, X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext, nseg, a.dy_ld);
+    } else if (a.mode == 1 && seg == 1280 && nseg == 1) {   // f32 rows of D = 1280 (attention output): 5 blocks interleaved
+        hipLaunchKernelGGL((k_rownorm<1, false, false, 5>), grid, blk, 0, s, X, a.M, seg, nullptr, nullptr, a.outH, a.dy, a.aext, 1, a.dy_ld);
     } else if (a.mode == 1) {
         hipLaunchKernelGGL((k_rownorm<1, false>), grid, blk, 0, s, X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext, nseg, a.dy_ld);
     } else if (a.mode == 2) {
