@@ -36,16 +36,30 @@ __device__ __forceinline__ _Float16 to16(float v) {
 }
 
 constexpr int KT = 64;            // keys per LDS tile
-constexpr int KROW = 144;         // bytes per K image row (64 halves + 16 B pad)
-constexpr int VROW = 136;         // bytes per V^T image row (64 halves + 8 B pad)
-constexpr int KIMG = KT * KROW;   // 9216
-constexpr int VIMG = 64 * VROW;   // 8704
-constexpr int STAGE = 2 * KIMG + VIMG;
+// LDS images per mode. F32-class (3 MFMAs per step, 174 VGPRs, 2 workgroups per CU): rows padded to 144 B (K) /
+// 136 B (V^T). bf16 (one MFMA per step, fewer registers): unpadded 128-B rows, XOR-swizzled — the K image's 16-B
+// chunk ch of row r at chunk ch ^ ((r >> 1) & 7), the V^T image's 8-B chunk c at c ^ ((r >> 1) & 15), conflict-free
+// for ds_read_b128 (16-lane groups of distinct rows) and ds_read_b64 (32 distinct rows) — 48 KiB per workgroup, so
+// three fit a CU (measured: padded 2/CU 33.4 ms/step, swizzled 3/CU 31.8; the swizzle alone costs address VALU)
+template <bool SW> struct attn_lds;
+template <> struct attn_lds<false> {
+    static constexpr int KROW = 144, VROW = 136;
+    static __device__ __forceinline__ int k(int, int ch) { return ch << 4; }
+    static __device__ __forceinline__ int v(int, int c8) { return c8 << 3; }
+};
+template <> struct attn_lds<true> {
+    static constexpr int KROW = 128, VROW = 128;
+    static __device__ __forceinline__ int k(int r, int ch) { return (ch ^ ((r >> 1) & 7)) << 4; }
+    static __device__ __forceinline__ int v(int r, int c8) { return (c8 ^ ((r >> 1) & 15)) << 3; }
+};
 constexpr float L2E = 1.4426950408889634f;   // exp(x) = exp2(x * log2 e)
 
 // BF: bf16-activation mode (Q, K, V^T, P and the output in bf16; S = K.Q^T is one MFMA per 16-deep step)
 template <bool BF>
-__global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
+__global__ __launch_bounds__(256, BF ? 3 : 2) void k_attn(const q2a_attn_args p) {
+    typedef attn_lds<BF> LY;
+    constexpr int KROW = LY::KROW, VROW = LY::VROW;
+    constexpr int KIMG = KT * KROW, VIMG = 64 * VROW, STAGE = 2 * KIMG + VIMG;
     __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int T = p.T, D = p.D;
@@ -93,11 +107,11 @@ __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
 #define Q2A_STORE_ONE(st_, c_, kh_, kl_, v_)                                                        \
     do {                                                                                            \
         const int r_ = (c_) >> 3, ch_ = (c_) & 7;                                                   \
-        *(uint4 *) ((st_) + r_ * KROW + ch_ * 16) = (kh_);                                          \
-        if (!BF) *(uint4 *) ((st_) + KIMG + r_ * KROW + ch_ * 16) = (kl_);                          \
-        uint2 * vv_ = (uint2 *) ((st_) + 2 * KIMG + r_ * VROW + ch_ * 16);                          \
-        vv_[0] = make_uint2((v_).x, (v_).y);                                                        \
-        vv_[1] = make_uint2((v_).z, (v_).w);                                                        \
+        *(uint4 *) ((st_) + r_ * KROW + LY::k(r_, ch_)) = (kh_);                                     \
+        if (!BF) *(uint4 *) ((st_) + KIMG + r_ * KROW + LY::k(r_, ch_)) = (kl_);                     \
+        char * vr_ = (st_) + 2 * KIMG + r_ * VROW;                                                  \
+        *(uint2 *) (vr_ + LY::v(r_, 2 * ch_)) = make_uint2((v_).x, (v_).y);                          \
+        *(uint2 *) (vr_ + LY::v(r_, 2 * ch_ + 1)) = make_uint2((v_).z, (v_).w);                      \
     } while (0)
 #define Q2A_STORE_TILE(buf_)                                                                        \
     do {                                                                                            \
@@ -137,7 +151,7 @@ __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
             const int krow = kb * 32 + col;
 #pragma unroll
             for (int st = 0; st < 4; ++st) {
-                const int off = krow * KROW + (2 * st + hi) * 16;
+                const int off = krow * KROW + LY::k(krow, 2 * st + hi);
                 const half8 ah = *(const half8 *) (kh_img + off);
                 sc[kb] = mma32<BF>(ah, qh[st], sc[kb]);
                 if (!BF) {
@@ -186,12 +200,13 @@ __global__ __launch_bounds__(256, 2) void k_attn(const q2a_attn_args p) {
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int dt = 0; dt < 2; ++dt) {
-                const char * vrow = vt_img + (dt * 32 + col) * VROW;
+                const int vr = dt * 32 + col;
+                const char * vrow = vt_img + vr * VROW;
 #pragma unroll
                 for (int sp = 0; sp < 2; ++sp) {
-                    const int kbyte = 2 * (kb * 32 + 16 * sp + 4 * hi);
-                    const half4 v0 = *(const half4 *) (vrow + kbyte);
-                    const half4 v1 = *(const half4 *) (vrow + kbyte + 16);
+                    const int c8 = 8 * kb + 4 * sp + hi;   // 8-B chunk of keys 32kb + 16sp + 4hi .. +3
+                    const half4 v0 = *(const half4 *) (vrow + LY::v(vr, c8));
+                    const half4 v1 = *(const half4 *) (vrow + LY::v(vr, c8 + 2));
                     const half8 va = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
                     o[dt] = mma32<BF>(va, pf[kb][sp], o[dt]);
                 }
