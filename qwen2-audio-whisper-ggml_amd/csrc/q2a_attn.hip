@@ -41,6 +41,9 @@ constexpr int KT = 64;            // keys per LDS tile
 // chunk ch of row r at chunk ch ^ ((r >> 1) & 7), the V^T image's 8-B chunk c at c ^ ((r >> 1) & 15), conflict-free
 // for ds_read_b128 (16-lane groups of distinct rows) and ds_read_b64 (32 distinct rows) — 48 KiB per workgroup, so
 // three fit a CU (measured: padded 2/CU 33.4 ms/step, swizzled 3/CU 31.8; the swizzle alone costs address VALU)
+#ifndef Q2A_ATTN_F32_OCC
+#define Q2A_ATTN_F32_OCC 2
+#endif
 template <bool SW> struct attn_lds;
 template <> struct attn_lds<false> {
     static constexpr int KROW = 144, VROW = 136;
@@ -56,7 +59,7 @@ constexpr float L2E = 1.4426950408889634f;   // exp(x) = exp2(x * log2 e)
 
 // BF: bf16-activation mode (Q, K, V^T, P and the output in bf16; S = K.Q^T is one MFMA per 16-deep step)
 template <bool BF>
-__global__ __launch_bounds__(256, BF ? 3 : 2) void k_attn(const q2a_attn_args p) {
+__global__ __launch_bounds__(256, BF ? 3 : Q2A_ATTN_F32_OCC) void k_attn(const q2a_attn_args p) {
     typedef attn_lds<BF> LY;
     constexpr int KROW = LY::KROW, VROW = LY::VROW;
     constexpr int KIMG = KT * KROW, VIMG = 64 * VROW, STAGE = 2 * KIMG + VIMG;
