@@ -39,9 +39,14 @@ GGML_API void ggml_backend_q2a_get_device_memory(int device, size_t * free, size
 
 GGML_API ggml_backend_reg_t ggml_backend_q2a_reg(void);             /* ggml-cuda.h:43 */
 
-/* statistics of the last graph_compute on this backend (test / profiling aid): nodes executed per kind */
+/* statistics of the last graph_compute on this backend (test / profiling aid): kernels launched per node kind; nodes
+ * folded into their producer's kernel (MUL_MAT -> ADD bias [-> GELU | ADD residual], NORM -> MUL -> ADD;
+ * GGML_Q2A_NO_FUSE=1 disables it); whether the launches were replayed from a captured HIP graph (a cgraph seen
+ * before; GGML_Q2A_NO_GRAPH=1 disables it) */
 typedef struct {
     int n_nodes, n_mul_mat_fast, n_mul_mat_f32, n_attn_fused, n_other;
+    int n_graph_replayed;
+    int n_fused;
 } ggml_backend_q2a_stats;
 GGML_API void ggml_backend_q2a_get_stats(ggml_backend_t backend, ggml_backend_q2a_stats * stats);
 

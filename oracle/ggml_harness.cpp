@@ -56,8 +56,9 @@ int cmd_encode(int argc, char ** argv) {
     whisper_full_params p;
     memset(&p, 0, sizeof(p));
     p.n_threads = 4;
-    double best = 1e30, total = 0;
+    double best = 1e30, total = 0, best_mel = 1e30, best_enc = 1e30;
     for (int r = 0; r < reps; ++r) {
+        const int64_t mel0 = ctx->state->t_mel_us, enc0 = ctx->state->t_encode_us;
         auto t0 = std::chrono::steady_clock::now();
         const int rc = whisper_full(ctx, p, pcm.data(), (int) pcm.size());
         auto t1 = std::chrono::steady_clock::now();
@@ -65,6 +66,9 @@ int cmd_encode(int argc, char ** argv) {
         const double s = std::chrono::duration<double>(t1 - t0).count();
         total += s;
         best = std::min(best, s);
+        // the reference's own phase clocks (qwen2-whisper.cpp:2335, 2651): CPU log-mel, then conv + encoder graphs
+        best_mel = std::min(best_mel, 1e-6 * (double) (ctx->state->t_mel_us - mel0));
+        best_enc = std::min(best_enc, 1e-6 * (double) (ctx->state->t_encode_us - enc0));
     }
     ggml_backend_q2a_stats st;
     memset(&st, 0, sizeof(st));
@@ -78,10 +82,11 @@ int cmd_encode(int argc, char ** argv) {
     fclose(f);
     printf("{\"ne0\": %lld, \"ne1\": %lld, \"reps\": %d, \"best_s\": %.6f, \"mean_s\": %.6f, \"backend\": \"%s\", "
            "\"embd_buffer\": \"%s\", \"n_splits_encode\": %d, \"nodes\": %d, \"mul_mat_fast\": %d, \"mul_mat_f32\": %d, "
-           "\"attn_fused\": %d, \"other\": %d}\n",
+           "\"attn_fused\": %d, \"other\": %d, \"graph_replayed\": %d, \"fused\": %d, \"best_mel_s\": %.6f, \"best_encode_s\": %.6f}\n",
            (long long) e->ne[0], (long long) e->ne[1], reps, best, total / reps, ggml_backend_name(be),
            ggml_backend_buffer_name(e->buffer), ggml_backend_sched_get_n_splits(ctx->state->sched_encode.sched),
-           st.n_nodes, st.n_mul_mat_fast, st.n_mul_mat_f32, st.n_attn_fused, st.n_other);
+           st.n_nodes, st.n_mul_mat_fast, st.n_mul_mat_f32, st.n_attn_fused, st.n_other, st.n_graph_replayed, st.n_fused, best_mel,
+           best_enc);
     whisper_free(ctx);
     return 0;
 }

@@ -30,6 +30,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #define Q2A_HIP(x)                                                                                   \
@@ -66,18 +67,20 @@ __device__ __forceinline__ void st_from_f32(char * p, int type, float v) {
     else *(float *) p = v;
 }
 
-// dst = src (any strides, F32/F16 either side), one thread per element of dst's logical shape
+// dst = src (any strides, F32/F16 either side), one thread per element of dst's logical shape. I = uint32_t when
+// the element count fits (32-bit divisions: several times cheaper than the 64-bit ones)
+template <typename I>
 __global__ void k_copy(tview s, int st, tview d, int dt, int64_t n) {
-    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int64_t i0 = i % d.ne[0], r = i / d.ne[0];
-    const int64_t i1 = r % d.ne[1], r2 = r / d.ne[1];
-    const int64_t i2 = r2 % d.ne[2], i3 = r2 / d.ne[2];
+    const I i = (I) ((int64_t) blockIdx.x * blockDim.x + threadIdx.x);
+    if ((int64_t) i >= n) return;
+    const I i0 = i % (I) d.ne[0], r = i / (I) d.ne[0];
+    const I i1 = r % (I) d.ne[1], r2 = r / (I) d.ne[1];
+    const I i2 = r2 % (I) d.ne[2], i3 = r2 / (I) d.ne[2];
     // ggml_dup walks both tensors in their own logical (row-major) element order; with equal element counts the
     // flat index i maps to the source's own (i0, i1, i2, i3)
-    const int64_t j0 = i % s.ne[0], q = i / s.ne[0];
-    const int64_t j1 = q % s.ne[1], q2 = q / s.ne[1];
-    const int64_t j2 = q2 % s.ne[2], j3 = q2 / s.ne[2];
+    const I j0 = i % (I) s.ne[0], q = i / (I) s.ne[0];
+    const I j1 = q % (I) s.ne[1], q2 = q / (I) s.ne[1];
+    const I j2 = q2 % (I) s.ne[2], j3 = q2 / (I) s.ne[2];
     const char * sp = s.base + voff(s, j0, j1, j2, j3);
     char * dp = d.base + voff(d, i0, i1, i2, i3);
     if (st == dt && st == GGML_TYPE_F16) *(uint16_t *) dp = *(const uint16_t *) sp;
@@ -125,6 +128,60 @@ __global__ void k_unary(tview a, tview d, int64_t n, float scale, const uint16_t
     *(float *) (d.base + voff(d, i0, i1, i2, i3)) = y;
 }
 
+// Row-wise fast path of ADD / MUL (b broadcast per ggml_can_repeat with b.ne0 == ne0 or 1), SCALE and GELU when
+// every operand's rows are f32-contiguous: one wave per row, the row index decomposed once per wave in 32 bits (the
+// generic kernels above pay six 64-bit divisions per element), float4 accesses when rows are 16-B aligned.
+// OP: 0 add, 1 mul, 2 scale, 3 GELU. Same float operations as the generic kernels.
+__device__ __forceinline__ float gelu_tab_f(float x, const uint16_t * gelu_tab) {
+    if (x <= -10.0f) return 0.0f;
+    if (x >= 10.0f) return x;
+    const _Float16 h = (_Float16) x;
+    uint16_t u;
+    __builtin_memcpy(&u, &h, 2);
+    const uint16_t g = gelu_tab[u];
+    _Float16 gh;
+    __builtin_memcpy(&gh, &g, 2);
+    return (float) gh;
+}
+
+template <int OP, bool V4>
+__global__ __launch_bounds__(256) void k_rows(tview a, tview b, tview d, int nrows, float scale, const uint16_t * gelu_tab) {
+    const int r = (int) blockIdx.x * 4 + (int) (threadIdx.x >> 6);
+    if (r >= nrows) return;
+    const int lane = threadIdx.x & 63;
+    const int ne0 = (int) d.ne[0], ne1 = (int) d.ne[1], ne2 = (int) d.ne[2];
+    const int i1 = r % ne1, t = r / ne1, i2 = t % ne2, i3 = t / ne2;
+    const float * x = (const float *) (a.base + i1 * a.nb[1] + i2 * a.nb[2] + i3 * a.nb[3]);
+    float * y = (float *) (d.base + i1 * d.nb[1] + i2 * d.nb[2] + i3 * d.nb[3]);
+    const float * z = x;
+    bool zs = false;
+    if (OP < 2) {
+        z = (const float *) (b.base + (i1 % (int) b.ne[1]) * b.nb[1] + (i2 % (int) b.ne[2]) * b.nb[2] +
+                             (i3 % (int) b.ne[3]) * b.nb[3]);
+        zs = b.ne[0] == 1;
+    }
+    auto f = [&](float u, float v) -> float {
+        if (OP == 0) return u + v;
+        if (OP == 1) return u * v;
+        if (OP == 2) return u * scale;
+        return gelu_tab_f(u, gelu_tab);
+    };
+    if (V4) {
+        const int n4 = ne0 >> 2;
+        for (int j = lane; j < n4; j += 64) {
+            const f4 u = ((const f4 *) x)[j];
+            f4 v = u;
+            if (OP < 2) v = zs ? f4{z[0], z[0], z[0], z[0]} : ((const f4 *) z)[j];
+            f4 o;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) o[k] = f(u[k], v[k]);
+            ((f4 *) y)[j] = o;
+        }
+    } else {
+        for (int j = lane; j < ne0; j += 64) y[j] = f(x[j], OP < 2 ? z[zs ? 0 : j] : 0.0f);
+    }
+}
+
 __device__ __forceinline__ double block_sum_d(double v, double * red) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -170,6 +227,54 @@ __global__ __launch_bounds__(256) void k_norm(tview a, tview d, float eps) {
     const float variance = (float) (s2 / n);
     const float scale = 1.0f / sqrtf(variance + eps);
     for (int i = threadIdx.x; i < n; i += blockDim.x) y[i] = (x[i] - mean) * scale;
+}
+
+// NORM (+ the MUL by the LayerNorm weight and ADD of its bias when the graph chains them, qwen2-whisper.cpp:2002-2006)
+// with the row held in registers (ne0 <= 2048): one HBM read instead of three. Same summation order as k_norm;
+// y = (x - mean) * scale, then y * w, then + b, each rounded to f32 (no contraction).
+template <bool AFF>
+__global__ __launch_bounds__(256) void k_norm_row(tview a, tview d, float eps, const float * w, const float * bb) {
+    __shared__ double red[4];
+    const int r = (int) blockIdx.x;
+    const int ne1 = (int) a.ne[1], ne2 = (int) a.ne[2];
+    const int i1 = r % ne1, t = r / ne1, i2 = t % ne2, i3 = t / ne2;
+    const float * x = (const float *) (a.base + i1 * a.nb[1] + i2 * a.nb[2] + i3 * a.nb[3]);
+    float * y = (float *) (d.base + i1 * d.nb[1] + i2 * d.nb[2] + i3 * d.nb[3]);
+    const int n = (int) a.ne[0];
+    float v[8];
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int i = threadIdx.x + k * 256;
+        v[k] = i < n ? x[i] : 0.0f;
+        if (i < n) s += (double) v[k];
+    }
+    s = block_sum_d(s, red);
+    const float mean = (float) (s / n);
+    double s2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int i = threadIdx.x + k * 256;
+        if (i < n) {
+            const float c = v[k] - mean;
+            s2 += (double) (c * c);
+        }
+    }
+    s2 = block_sum_d(s2, red);
+    const float variance = (float) (s2 / n);
+    const float scale = 1.0f / sqrtf(variance + eps);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int i = threadIdx.x + k * 256;
+        if (i < n) {
+            float o = (v[k] - mean) * scale;
+            if (AFF) {
+                o = o * w[i];
+                o = o + bb[i];
+            }
+            y[i] = o;
+        }
+    }
 }
 
 // SOFT_MAX without mask (ggml.c:13854-13950): w = x*scale, max, e = exp(w - max) with a double sum,
@@ -347,6 +452,7 @@ struct q2a_device_ctx {
     ggml_backend_device dev;
     std::mutex mu;
     std::vector<packed_w> wcache;
+    uint64_t wgen = 0;                 // bumped whenever a packed weight is evicted (captured graphs hold its pointer)
     uint16_t * gelu_tab = nullptr;     // device copy of the 64 Ki-entry fp16 GELU table (lazy)
 };
 
@@ -368,6 +474,12 @@ struct q2a_backend_ctx {
     void * scratch = nullptr;
     size_t scratch_bytes = 0;
     ggml_backend_q2a_stats stats{};
+    // HIP graphs of recent graph_computes: the sched hands the same cgraphs (same nodes, buffers, parameters) on
+    // every whisper_full — the conv graph, then the encoder graph — so a cgraph seen a second time has its launches
+    // captured once and is replayed from then on
+    struct captured { uint64_t sig; int seen; hipGraphExec_t exec; ggml_backend_q2a_stats stats; uint64_t used; };
+    std::vector<captured> graphs;
+    uint64_t graph_clock = 0;
 };
 
 q2a_reg_ctx * reg_ctx();
@@ -390,6 +502,7 @@ void invalidate(int device, const void * p, size_t n) {
         if (w.raw < a + n && a < w.raw + w.raw_bytes) {
             (void) hipSetDevice(device);
             (void) hipFree(w.dev);
+            ++d->wgen;
             d->wcache[i] = d->wcache.back();
             d->wcache.pop_back();
         } else {
@@ -555,7 +668,11 @@ const packed_w * get_packed(q2a_backend_ctx * b, const ggml_tensor * w) {
     return &d->wcache.back();
 }
 
-void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op) {
+// epi: Q2A_EPI_STORE_F (bias optional), Q2A_EPI_GELU_F (bias, GELU), Q2A_EPI_RESID (bias, + resid rows); the result
+// goes to `out` (op itself, or the last node of a fused MUL_MAT -> ADD [-> GELU | ADD] chain)
+void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = nullptr, int epi = Q2A_EPI_STORE_F,
+                 const float * bias = nullptr, const float * resid = nullptr) {
+    if (!out) out = op;
     const ggml_tensor * w = op->src[0];
     const ggml_tensor * x = op->src[1];
     const int K = (int) w->ne[0], N = (int) w->ne[1];
@@ -581,7 +698,8 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op) {
     memset(&a, 0, sizeof(a));
     a.A = A; a.lda = K; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
     a.M = M; a.N = N; a.K = K; a.ldw = K;
-    a.outF = (float *) op->data; a.ldo = N;
+    a.outF = (float *) out->data; a.ldo = N;
+    a.bias = bias; a.store_bias = bias != nullptr; a.resid = resid;
     a.gelu_tab = gelu_table(b->device);
     if (blk == 0) {
         a.W = (const q2a_half *) w->data;
@@ -600,7 +718,7 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op) {
             a.aext = aext;
         }
     }
-    Q2A_HIP(q2a_launch_gemm(a, Q2A_EPI_STORE_F, blk, b->stream));
+    Q2A_HIP(q2a_launch_gemm(a, epi, blk, b->stream));
 }
 
 void run_mm_f32(q2a_backend_ctx * b, ggml_tensor * op) {
@@ -704,11 +822,74 @@ bool op_supported(const ggml_tensor * op) {
     }
 }
 
-ggml_status graph_compute(ggml_backend_t backend, ggml_cgraph * g) {
-    q2a_backend_ctx * b = (q2a_backend_ctx *) backend->context;
-    Q2A_HIP(hipSetDevice(b->device));
+// the launcher would take the 8-phase kernels, whose GELU epilogue reads a compact LDS table this backend does not build
+bool mm_is_pipe8(const ggml_tensor * op) {
+    const int64_t M = op->src[1]->ne[1] * op->src[1]->ne[2] * op->src[1]->ne[3];
+    return q2a_gemm_wide_tiles((int) M, (int) op->src[0]->ne[1], 0);
+}
+
+bool rows_f32(const ggml_tensor * t) { return t->type == GGML_TYPE_F32 && t->nb[0] == 4; }
+bool row_vec_f32(const ggml_tensor * t, int64_t n) {
+    return rows_f32(t) && t->ne[0] == n && t->ne[1] == 1 && t->ne[2] == 1 && t->ne[3] == 1 && ((uintptr_t) t->data & 15) == 0;
+}
+bool aligned16(const ggml_tensor * t) {
+    return ((uintptr_t) t->data & 15) == 0 && t->nb[1] % 16 == 0 && t->nb[2] % 16 == 0 && t->nb[3] % 16 == 0;
+}
+
+// ADD / MUL / SCALE / GELU on the row kernel when the shapes allow it (true), else false (generic kernel)
+bool launch_rows(q2a_backend_ctx * b, int op_kind, const ggml_tensor * a, const ggml_tensor * y, const ggml_tensor * z,
+                 float scale) {
+    if (!rows_f32(a) || !rows_f32(y) || (z && !rows_f32(z))) return false;
+    for (int k = 0; k < 4; ++k) if (a->ne[k] != y->ne[k]) return false;
+    const int64_t ne0 = y->ne[0], nrows = y->ne[1] * y->ne[2] * y->ne[3];
+    if (ne0 <= 0 || nrows <= 0 || ne0 > (1 << 30) || nrows > (1ll << 30) * 2 - 4) return false;
+    const bool zs = z && z->ne[0] == 1 && ne0 != 1;
+    if (z && !zs && z->ne[0] != ne0) return false;
+    const bool v4 = ne0 % 4 == 0 && aligned16(a) && aligned16(y) && (!z || zs || aligned16(z));
+    const tview ta = tv(a), tz = z ? tv(z) : ta, ty = tv(y);
+    const dim3 grid((unsigned) ((nrows + 3) / 4));
+    const uint16_t * gt = op_kind == 3 ? gelu_table(b->device) : nullptr;
+#define Q2A_ROWS(OP)                                                                                                  \
+    do {                                                                                                              \
+        if (v4) hipLaunchKernelGGL((k_rows<OP, true>), grid, dim3(256), 0, b->stream, ta, tz, ty, (int) nrows, scale, gt); \
+        else hipLaunchKernelGGL((k_rows<OP, false>), grid, dim3(256), 0, b->stream, ta, tz, ty, (int) nrows, scale, gt);   \
+    } while (0)
+    switch (op_kind) {
+        case 0: Q2A_ROWS(0); break;
+        case 1: Q2A_ROWS(1); break;
+        case 2: Q2A_ROWS(2); break;
+        default: Q2A_ROWS(3); break;
+    }
+#undef Q2A_ROWS
+    return true;
+}
+
+ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
+    static const bool no_fuse = [] { const char * v = getenv("GGML_Q2A_NO_FUSE"); return v && atoi(v); }();
     b->stats = ggml_backend_q2a_stats{};
     const int nn = ggml_graph_n_nodes(g);
+    // consumers per tensor within this graph: a node is folded into its producer's kernel only when it is the
+    // producer's sole consumer (views count as consumers) and the producer is not a graph output
+    std::unordered_map<const ggml_tensor *, int> uses;
+    if (!no_fuse) {
+        uses.reserve((size_t) nn * 2);
+        for (int j = 0; j < nn; ++j) {
+            const ggml_tensor * t = ggml_graph_node(g, j);
+            for (int k = 0; k < GGML_MAX_SRC; ++k) if (t->src[k]) uses[t->src[k]]++;
+        }
+    }
+    auto sole = [&](const ggml_tensor * producer, const ggml_tensor * consumer) {
+        if (no_fuse || (producer->flags & GGML_TENSOR_FLAG_OUTPUT)) return false;
+        auto it = uses.find(producer);
+        if (it == uses.end() || it->second != 1) return false;
+        for (int k = 0; k < GGML_MAX_SRC; ++k) if (consumer->src[k] == producer) return true;
+        return false;
+    };
+    auto node = [&](int j) -> ggml_tensor * { return j < nn ? ggml_graph_node(g, j) : nullptr; };
+    auto same_shape_rows = [](const ggml_tensor * x, const ggml_tensor * y) {
+        for (int k = 0; k < 4; ++k) if (x->ne[k] != y->ne[k]) return false;
+        return ggml_is_contiguous(x) && ggml_is_contiguous(y) && x->type == GGML_TYPE_F32 && y->type == GGML_TYPE_F32;
+    };
     for (int i = 0; i < nn; ++i) {
         ggml_tensor * op = ggml_graph_node(g, i);
         if (ggml_is_empty(op) || op->op == GGML_OP_NONE || op->op == GGML_OP_RESHAPE || op->op == GGML_OP_VIEW ||
@@ -723,33 +904,86 @@ ggml_status graph_compute(ggml_backend_t backend, ggml_cgraph * g) {
             case GGML_OP_MUL_MAT: {
                 const int used = try_fused_attention(b, g, i);
                 if (used) { i += used - 1; break; }
-                if (mm_fast_ok(op)) { run_mm_fast(b, op); b->stats.n_mul_mat_fast++; }
-                else { run_mm_f32(b, op); b->stats.n_mul_mat_f32++; }
+                if (!mm_fast_ok(op)) { run_mm_f32(b, op); b->stats.n_mul_mat_f32++; break; }
+                // MUL_MAT -> ADD(bias row) [-> GELU | -> ADD(residual)] on the GEMM epilogue
+                // (qwen2-whisper.cpp:2029-2037, 2120-2154): same f32 operations, one kernel, no [N][M] round trips
+                ggml_tensor * n1 = node(i + 1), * n2 = node(i + 2);
+                if (n1 && n1->op == GGML_OP_ADD && n1->src[0] == op && sole(op, n1) && row_vec_f32(n1->src[1], op->ne[0]) &&
+                    same_shape_rows(op, n1) && ((uintptr_t) n1->data & 15) == 0) {
+                    const float * bias = (const float *) n1->src[1]->data;
+                    if (n2 && n2->op == GGML_OP_UNARY && ggml_get_unary_op(n2) == GGML_UNARY_OP_GELU && n2->src[0] == n1 &&
+                        sole(n1, n2) && same_shape_rows(n1, n2) && ((uintptr_t) n2->data & 15) == 0 && !mm_is_pipe8(op)) {
+                        run_mm_fast(b, op, n2, Q2A_EPI_GELU_F, bias);
+                        b->stats.n_fused += 2;
+                        i += 2;
+                    } else if (n2 && n2->op == GGML_OP_ADD && sole(n1, n2) && same_shape_rows(n1, n2) &&
+                               ((uintptr_t) n2->data & 15) == 0) {
+                        const ggml_tensor * r = n2->src[0] == n1 ? n2->src[1] : n2->src[0];
+                        if (r != n1 && same_shape_rows(n1, r) && ((uintptr_t) r->data & 15) == 0) {
+                            run_mm_fast(b, op, n2, Q2A_EPI_RESID, bias, (const float *) r->data);
+                            b->stats.n_fused += 2;
+                            i += 2;
+                        } else {
+                            run_mm_fast(b, op, n1, Q2A_EPI_STORE_F, bias);
+                            b->stats.n_fused += 1;
+                            i += 1;
+                        }
+                    } else {
+                        run_mm_fast(b, op, n1, Q2A_EPI_STORE_F, bias);
+                        b->stats.n_fused += 1;
+                        i += 1;
+                    }
+                } else {
+                    run_mm_fast(b, op);
+                }
+                b->stats.n_mul_mat_fast++;
                 break;
             }
-            case GGML_OP_ADD:
-                hipLaunchKernelGGL(k_binary<0>, grid1(n), dim3(256), 0, st, tv(s0), tv(s1), tv(op), n);
-                b->stats.n_other++;
-                break;
-            case GGML_OP_MUL:
-                hipLaunchKernelGGL(k_binary<1>, grid1(n), dim3(256), 0, st, tv(s0), tv(s1), tv(op), n);
+            case GGML_OP_ADD: case GGML_OP_MUL:
+                if (!launch_rows(b, op->op == GGML_OP_ADD ? 0 : 1, s0, op, s1, 1.0f)) {
+                    if (op->op == GGML_OP_ADD)
+                        hipLaunchKernelGGL(k_binary<0>, grid1(n), dim3(256), 0, st, tv(s0), tv(s1), tv(op), n);
+                    else
+                        hipLaunchKernelGGL(k_binary<1>, grid1(n), dim3(256), 0, st, tv(s0), tv(s1), tv(op), n);
+                }
                 b->stats.n_other++;
                 break;
             case GGML_OP_SCALE: {
                 float sc;
                 memcpy(&sc, op->op_params, 4);
-                hipLaunchKernelGGL(k_unary<0>, grid1(n), dim3(256), 0, st, tv(s0), tv(op), n, sc, (const uint16_t *) nullptr);
+                if (!launch_rows(b, 2, s0, op, nullptr, sc))
+                    hipLaunchKernelGGL(k_unary<0>, grid1(n), dim3(256), 0, st, tv(s0), tv(op), n, sc, (const uint16_t *) nullptr);
                 b->stats.n_other++;
                 break;
             }
             case GGML_OP_UNARY:
-                hipLaunchKernelGGL(k_unary<1>, grid1(n), dim3(256), 0, st, tv(s0), tv(op), n, 1.0f, gelu_table(b->device));
+                if (!launch_rows(b, 3, s0, op, nullptr, 1.0f))
+                    hipLaunchKernelGGL(k_unary<1>, grid1(n), dim3(256), 0, st, tv(s0), tv(op), n, 1.0f, gelu_table(b->device));
                 b->stats.n_other++;
                 break;
             case GGML_OP_NORM: {
                 float eps;
                 memcpy(&eps, op->op_params, 4);
-                hipLaunchKernelGGL(k_norm, dim3((unsigned) ggml_nrows(op)), dim3(256), 0, st, tv(s0), tv(op), eps);
+                const unsigned rows = (unsigned) ggml_nrows(op);
+                if (op->ne[0] > 2048 || ggml_nrows(op) > (1ll << 31) - 1) {
+                    hipLaunchKernelGGL(k_norm, dim3(rows), dim3(256), 0, st, tv(s0), tv(op), eps);
+                    b->stats.n_other++;
+                    break;
+                }
+                // NORM -> MUL(weight row) -> ADD(bias row) (qwen2-whisper.cpp:2002-2006, 2124-2128, 2176-2180)
+                ggml_tensor * n1 = node(i + 1), * n2 = node(i + 2);
+                if (n1 && n2 && n1->op == GGML_OP_MUL && n1->src[0] == op && sole(op, n1) &&
+                    row_vec_f32(n1->src[1], op->ne[0]) && n2->op == GGML_OP_ADD && n2->src[0] == n1 && sole(n1, n2) &&
+                    row_vec_f32(n2->src[1], op->ne[0]) && rows_f32(n2) && n1->type == GGML_TYPE_F32 &&
+                    ggml_are_same_shape(op, n2)) {
+                    hipLaunchKernelGGL(k_norm_row<true>, dim3(rows), dim3(256), 0, st, tv(s0), tv(n2), eps,
+                                       (const float *) n1->src[1]->data, (const float *) n2->src[1]->data);
+                    b->stats.n_fused += 2;
+                    i += 2;
+                } else {
+                    hipLaunchKernelGGL(k_norm_row<false>, dim3(rows), dim3(256), 0, st, tv(s0), tv(op), eps,
+                                       (const float *) nullptr, (const float *) nullptr);
+                }
                 b->stats.n_other++;
                 break;
             }
@@ -762,7 +996,10 @@ ggml_status graph_compute(ggml_backend_t backend, ggml_cgraph * g) {
             }
             case GGML_OP_CONT: case GGML_OP_DUP: case GGML_OP_CPY: {
                 ggml_tensor * dst = op->op == GGML_OP_CPY ? op->src[1] : op;
-                hipLaunchKernelGGL(k_copy, grid1(n), dim3(256), 0, st, tv(s0), (int) s0->type, tv(dst), (int) dst->type, n);
+                if (n < (1ll << 31))
+                    hipLaunchKernelGGL(k_copy<uint32_t>, grid1(n), dim3(256), 0, st, tv(s0), (int) s0->type, tv(dst), (int) dst->type, n);
+                else
+                    hipLaunchKernelGGL(k_copy<int64_t>, grid1(n), dim3(256), 0, st, tv(s0), (int) s0->type, tv(dst), (int) dst->type, n);
                 b->stats.n_other++;
                 break;
             }
@@ -793,6 +1030,82 @@ ggml_status graph_compute(ggml_backend_t backend, ggml_cgraph * g) {
     return GGML_STATUS_SUCCESS;
 }
 
+// everything a captured launch depends on: per node its op, parameters, shape, strides and the addresses of the
+// node and its sources; plus the weight-cache generation (packed weight pointers are baked into the graph)
+uint64_t graph_signature(ggml_cgraph * g, uint64_t wgen) {
+    uint64_t h = 1469598103934665603ull ^ wgen;
+    auto mix = [&](uint64_t v) { h = (h ^ v) * 1099511628211ull; };
+    const int nn = ggml_graph_n_nodes(g);
+    mix((uint64_t) nn);
+    for (int i = 0; i < nn; ++i) {
+        const ggml_tensor * t = ggml_graph_node(g, i);
+        mix((uint64_t) t->op); mix((uint64_t) t->type); mix((uint64_t) (uintptr_t) t->data);
+        for (int k = 0; k < 4; ++k) { mix((uint64_t) t->ne[k]); mix((uint64_t) t->nb[k]); }
+        for (int k = 0; k < 8; ++k) mix((uint64_t) (uint32_t) t->op_params[k]);
+        for (int s = 0; s < GGML_MAX_SRC && t->src[s]; ++s) {
+            const ggml_tensor * u = t->src[s];
+            mix((uint64_t) (uintptr_t) u->data); mix((uint64_t) u->type);
+            for (int k = 0; k < 4; ++k) { mix((uint64_t) u->ne[k]); mix((uint64_t) u->nb[k]); }
+        }
+    }
+    return h;
+}
+
+ggml_status graph_compute(ggml_backend_t backend, ggml_cgraph * g) {
+    q2a_backend_ctx * b = (q2a_backend_ctx *) backend->context;
+    Q2A_HIP(hipSetDevice(b->device));
+    static const bool no_graph = [] { const char * v = getenv("GGML_Q2A_NO_GRAPH"); return v && atoi(v); }();
+    if (no_graph) return run_nodes(b, g);
+    constexpr size_t max_graphs = 8;
+    q2a_device_ctx * d = dev_ctx(b->device);
+    const uint64_t sig = graph_signature(g, d->wgen);
+    q2a_backend_ctx::captured * c = nullptr;
+    for (auto & e : b->graphs) if (e.sig == sig) c = &e;
+    if (!c) {   // first sighting: run directly (packs weights, sizes the scratch), remember the signature
+        if (b->graphs.size() == max_graphs) {
+            auto lru = std::min_element(b->graphs.begin(), b->graphs.end(),
+                                        [](const auto & x, const auto & y) { return x.used < y.used; });
+            if (lru->exec) (void) hipGraphExecDestroy(lru->exec);
+            b->graphs.erase(lru);
+        }
+        b->graphs.push_back({sig, 1, nullptr, {}, ++b->graph_clock});
+        return run_nodes(b, g);
+    }
+    c->used = ++b->graph_clock;
+    if (c->exec) {   // replay
+        if (hipGraphLaunch(c->exec, b->stream) == hipSuccess) {
+            b->stats = c->stats;
+            b->stats.n_graph_replayed = 1;
+            return GGML_STATUS_SUCCESS;
+        }
+        (void) hipGetLastError();
+        (void) hipGraphExecDestroy(c->exec);
+        c->exec = nullptr;
+        return run_nodes(b, g);
+    }
+    if (++c->seen == 2) {   // second sighting (weights packed, scratch sized): capture once, then launch
+        hipGraph_t graph = nullptr;
+        if (hipStreamBeginCapture(b->stream, hipStreamCaptureModeThreadLocal) == hipSuccess) {
+            const ggml_status st = run_nodes(b, g);
+            const hipError_t ec = hipStreamEndCapture(b->stream, &graph);
+            hipGraphExec_t exec = nullptr;
+            if (st == GGML_STATUS_SUCCESS && ec == hipSuccess && graph &&
+                hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0) == hipSuccess) {
+                (void) hipGraphDestroy(graph);
+                c->exec = exec;
+                c->stats = b->stats;
+                if (hipGraphLaunch(exec, b->stream) == hipSuccess) return GGML_STATUS_SUCCESS;
+                (void) hipGraphExecDestroy(exec);
+                c->exec = nullptr;
+            } else if (graph) {
+                (void) hipGraphDestroy(graph);
+            }
+        }
+        (void) hipGetLastError();   // capture refused or failed: nothing ran; run the nodes directly below
+    }
+    return run_nodes(b, g);
+}
+
 // ---- backend ------------------------------------------------------------------------------------
 ggml_guid_t q2a_guid() {
     static ggml_guid guid = {0x51, 0x32, 0x41, 0x2d, 0x67, 0x66, 0x78, 0x39, 0x35, 0x30, 0x4d, 0x49, 0x33, 0x35, 0x35, 0x58};
@@ -805,6 +1118,7 @@ void be_free(ggml_backend_t be) {
     (void) hipSetDevice(b->device);
     (void) hipStreamSynchronize(b->stream);
     if (b->scratch) (void) hipFree(b->scratch);
+    for (auto & e : b->graphs) if (e.exec) (void) hipGraphExecDestroy(e.exec);
     (void) hipStreamDestroy(b->stream);
     delete b;
     delete be;

@@ -740,13 +740,14 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
     f4 bias4[NJ];
 #pragma unroll
     for (int j = 0; j < NJ; ++j)
-        bias4[j] = (EPI == Q2A_EPI_STORE_F) ? f4{0.f, 0.f, 0.f, 0.f} : *(const f4 *) (p.bias + cbase + j * 16 + 4 * q);
+        bias4[j] = (EPI == Q2A_EPI_STORE_F && !p.store_bias) ? f4{0.f, 0.f, 0.f, 0.f}
+                                                               : *(const f4 *) (p.bias + cbase + j * 16 + 4 * q);
     const float vscale = (EPI == Q2A_EPI_QKV && part == 0) ? p.qscale : 1.0f;
     const uint16_t * lut = (const uint16_t *) lds_raw;
     // per-element value before the store: bias, GELU (LDS table when staged), Q scale
     auto val = [&](int i, int j, int r) -> float {
         float v = acc[i][j][r];
-        if (EPI != Q2A_EPI_STORE_F) v = v + bias4[j][r];
+        if (EPI != Q2A_EPI_STORE_F || p.store_bias) v = v + bias4[j][r];
         if (LUT_EPI && EPI != Q2A_EPI_GELU_H) v = gelu_lut_c(v, lut);
         else if (!LUT_EPI && (EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_GELU_F || EPI == Q2A_EPI_CONV2)) v = gelu_lut(v, p.gelu_tab);
         if (EPI == Q2A_EPI_QKV) v = v * vscale;   // ggml_scale after the bias add (:2054), exact 2^-3
@@ -870,8 +871,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
             float * orow = p.outF + (int64_t) m * p.ldo + cbase + 4 * q;
             f4 add[NJ];
             if (EPI == Q2A_EPI_RESID) {
+                const float * rrow = p.resid ? p.resid + (int64_t) m * p.ldo + cbase + 4 * q : orow;
 #pragma unroll
-                for (int j = 0; j < NJ; ++j) add[j] = *(const f4 *) (orow + 16 * j);
+                for (int j = 0; j < NJ; ++j) add[j] = *(const f4 *) (rrow + 16 * j);
             } else if (EPI == Q2A_EPI_CONV2) {
                 const int tpos = pt0 + ml >= p.T ? pt0 + ml - p.T : pt0 + ml;
                 const float * perow = p.pe + (int64_t) tpos * p.ldo + cbase + 4 * q;
@@ -896,7 +898,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
 
 // split-K reduce: out[m][n] = ((p_0 + p_1 + ...) + bias[n]) + out[m][n], partials summed in split order
 __global__ void k_split_reduce(const float * __restrict__ part, int S, int64_t stride, int M, int N, const float * bias,
-                               float * out, int64_t ldo) {
+                               float * out, int64_t ldo, const float * resid) {
     const int64_t i4 = ((int64_t) blockIdx.x * blockDim.x + threadIdx.x) * 4;
     if (i4 >= (int64_t) M * N) return;
     const int m = (int) (i4 / N), n = (int) (i4 - (int64_t) m * N);
@@ -908,7 +910,7 @@ __global__ void k_split_reduce(const float * __restrict__ part, int S, int64_t s
     }
     const f4 b = *(const f4 *) (bias + n);
     f4 * o = (f4 *) (out + (int64_t) m * ldo + n);
-    f4 x = *o;
+    f4 x = resid ? *(const f4 *) (resid + (int64_t) m * ldo + n) : *o;
 #pragma unroll
     for (int r = 0; r < 4; ++r) x[r] = (acc[r] + b[r]) + x[r];
     *o = x;
@@ -922,7 +924,7 @@ hipError_t launch_cfg(const q2a_gemm_args & a, hipStream_t s) {
     if (split) {
         const int64_t n4 = (int64_t) a.M * a.N / 4;
         hipLaunchKernelGGL(k_split_reduce, dim3((unsigned) ((n4 + 255) / 256)), dim3(256), 0, s, a.part, a.ksplit,
-                           a.split_stride, a.M, a.N, a.bias, a.outF, a.ldo);
+                           a.split_stride, a.M, a.N, a.bias, a.outF, a.ldo, a.resid);
     }
     return hipGetLastError();
 }

@@ -81,3 +81,35 @@ def test_reference_whisper_full_on_backend_full_size(harness, make_model, make_c
         assert mxs < 1e-3 and l2s < 1e-3 and rnerr < 1e-4, (mxs, l2s, rnerr)
     else:   # inherent activation re-quantization flips, as for the engine
         assert l2s < 2e-2 and rnerr < 2e-3, (mxs, l2s, rnerr)
+
+
+@pytest.mark.parametrize("wt", ["f16", "q4_k"])
+def test_backend_graph_replay_matches_direct(harness, make_model, make_clip, tmp_path, wt):
+    """graph_compute captures a cgraph it has seen before into a HIP graph and replays it (ggml-q2a.hip
+    graph_compute): the third whisper_full replays both the conv and the encoder graph, and its embd_enc equals the
+    per-node launches (GGML_Q2A_NO_GRAPH=1) bit for bit."""
+    model, clip = make_model("tiny", wt), make_clip(0)
+    direct, info_d = run(harness, model, clip, tmp_path, {"GGML_Q2A_NO_GRAPH": "1"}, reps=3)
+    assert info_d["graph_replayed"] == 0, info_d
+    replay, info_r = run(harness, model, clip, tmp_path, reps=3)
+    assert info_r["graph_replayed"] == 1, info_r
+    for k in ("nodes", "mul_mat_fast", "attn_fused", "other"):
+        assert info_r[k] == info_d[k], (k, info_r, info_d)
+    assert np.array_equal(replay, direct)
+
+
+@pytest.mark.parametrize("wt", ["f16", "q4_k", "q8_0", "q4_0"])
+def test_backend_fusions_match_per_node(harness, make_model, make_clip, tmp_path, wt):
+    """Nodes folded into their producer's kernel (MUL_MAT -> ADD bias [-> GELU | ADD residual] on the GEMM epilogue,
+    NORM -> MUL -> ADD in one row kernel) compute the same f32 operations as the per-node launches
+    (GGML_Q2A_NO_FUSE=1): embd_enc is bit-identical."""
+    model, clip = make_model("tiny", wt), make_clip(1)
+    plain, info_p = run(harness, model, clip, tmp_path, {"GGML_Q2A_NO_FUSE": "1"})
+    assert info_p["fused"] == 0, info_p
+    fused, info_f = run(harness, model, clip, tmp_path)
+    L = 2
+    # per layer: Q and V bias, O bias + residual, fc1 bias + GELU, fc2 bias + residual, two LayerNorm affines;
+    # plus the final LayerNorm affine
+    assert info_f["fused"] == 12 * L + 2, info_f
+    assert info_f["other"] < info_p["other"], (info_f, info_p)
+    assert np.array_equal(fused, plain)
