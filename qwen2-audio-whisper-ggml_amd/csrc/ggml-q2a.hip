@@ -230,50 +230,72 @@ __global__ __launch_bounds__(256) void k_norm(tview a, tview d, float eps) {
 }
 
 // NORM (+ the MUL by the LayerNorm weight and ADD of its bias when the graph chains them, qwen2-whisper.cpp:2002-2006)
-// with the row held in registers (ne0 <= 2048): one HBM read instead of three. Same summation order as k_norm;
-// y = (x - mean) * scale, then y * w, then + b, each rounded to f32 (no contraction).
-template <bool AFF>
-__global__ __launch_bounds__(256) void k_norm_row(tview a, tview d, float eps, const float * w, const float * bb) {
-    __shared__ double red[4];
-    const int r = (int) blockIdx.x;
+// with one wave per row and the row held in registers (ne0 <= 2048): one HBM read instead of three and no block
+// barriers. Mean and variance are double sums (ggml.c:11941-11990); y = (x - mean) * scale, then y * w, then + b,
+// each rounded to f32 (no contraction). V4: ne0 % 4 == 0 and 16-B aligned rows.
+template <bool AFF, bool V4>
+__global__ __launch_bounds__(256) void k_norm_row(tview a, tview d, float eps, const float * w, const float * bb, int nrows) {
+    const int r = (int) blockIdx.x * 4 + (int) (threadIdx.x >> 6);
+    if (r >= nrows) return;
+    const int lane = threadIdx.x & 63;
     const int ne1 = (int) a.ne[1], ne2 = (int) a.ne[2];
     const int i1 = r % ne1, t = r / ne1, i2 = t % ne2, i3 = t / ne2;
     const float * x = (const float *) (a.base + i1 * a.nb[1] + i2 * a.nb[2] + i3 * a.nb[3]);
     float * y = (float *) (d.base + i1 * d.nb[1] + i2 * d.nb[2] + i3 * d.nb[3]);
     const int n = (int) a.ne[0];
-    float v[8];
+    constexpr int C = V4 ? 8 : 32;           // per-lane chunks: float4s (V4) or floats
+    constexpr int W = V4 ? 4 : 1;
+    float v[C][W];
     double s = 0.0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int i = threadIdx.x + k * 256;
-        v[k] = i < n ? x[i] : 0.0f;
-        if (i < n) s += (double) v[k];
+    for (int k = 0; k < C; ++k) {
+        const int j = lane + 64 * k;
+        const bool ok = j * W < n;
+        if (V4) {
+            const f4 u = ok ? ((const f4 *) x)[j] : f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < W; ++q) v[k][q] = u[q];
+        } else {
+            v[k][0] = ok ? x[j] : 0.0f;
+        }
+        if (ok) {
+#pragma unroll
+            for (int q = 0; q < W; ++q) s += (double) v[k][q];
+        }
     }
-    s = block_sum_d(s, red);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
     const float mean = (float) (s / n);
     double s2 = 0.0;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int i = threadIdx.x + k * 256;
-        if (i < n) {
-            const float c = v[k] - mean;
-            s2 += (double) (c * c);
+    for (int k = 0; k < C; ++k) {
+        if ((lane + 64 * k) * W < n) {
+#pragma unroll
+            for (int q = 0; q < W; ++q) {
+                const float c = v[k][q] - mean;
+                s2 += (double) (c * c);
+            }
         }
     }
-    s2 = block_sum_d(s2, red);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s2 += __shfl_xor(s2, o, 64);
     const float variance = (float) (s2 / n);
     const float scale = 1.0f / sqrtf(variance + eps);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int i = threadIdx.x + k * 256;
-        if (i < n) {
-            float o = (v[k] - mean) * scale;
+    for (int k = 0; k < C; ++k) {
+        const int j = lane + 64 * k;
+        if (j * W >= n) continue;
+        float o[W];
+#pragma unroll
+        for (int q = 0; q < W; ++q) {
+            o[q] = (v[k][q] - mean) * scale;
             if (AFF) {
-                o = o * w[i];
-                o = o + bb[i];
+                o[q] = o[q] * w[j * W + q];
+                o[q] = o[q] + bb[j * W + q];
             }
-            y[i] = o;
         }
+        if (V4) ((f4 *) y)[j] = f4{o[0], o[W > 1 ? 1 : 0], o[W > 2 ? 2 : 0], o[W > 3 ? 3 : 0]};
+        else y[j] = o[0];
     }
 }
 
@@ -329,10 +351,22 @@ __global__ void k_pool1d_avg(tview s, tview d, int k, int64_t n) {
     *(float *) (d.base + voff(d, i0, i1, i2, i3)) = acc;
 }
 
-// fp32 -> fp16 (RNE) of a contiguous F32 activation block (ggml_fp32_to_fp16_row, the F16 vec_dot_type)
+// fp32 -> fp16 (RNE) of a contiguous F32 activation block (ggml_fp32_to_fp16_row, the F16 vec_dot_type); 8 per
+// thread (two 16-B loads, one 16-B store) when n % 8 == 0 and both ends are 16-B aligned
 __global__ void k_f32_to_f16(const float * x, _Float16 * y, int64_t n) {
     const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) y[i] = (_Float16) x[i];
+}
+__global__ void k_f32_to_f16_x8(const f4 * x, uint4 * y, int64_t n8) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n8) return;
+    const f4 u = x[2 * i], v = x[2 * i + 1];
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    const h8 h = {(_Float16) u[0], (_Float16) u[1], (_Float16) u[2], (_Float16) u[3],
+                  (_Float16) v[0], (_Float16) v[1], (_Float16) v[2], (_Float16) v[3]};
+    uint4 o;
+    __builtin_memcpy(&o, &h, 16);
+    y[i] = o;
 }
 
 // Batched exact-f32 GEMM: dst[i3][i2][i1][i0] = sum_k src0[i3/r3][i2/r2][i0][k] * src1[i3][i2][i1][k]
@@ -406,22 +440,42 @@ __global__ __launch_bounds__(256) void k_mm_f32(mm_args p) {
 }
 
 // attention operands for the fused path: per-head fp16 hi/lo halves of Q (already scaled) and K, V^T
+template <bool WITH_V>
 __global__ void k_attn_prep(tview q, tview k, tview v, _Float16 * qh, _Float16 * ql, _Float16 * kh, _Float16 * kl,
                             _Float16 * vt, int T, int H, int TP, int64_t n) {
     // element (d, t, h): q/k/v views have ne = [64, T, H]; q,k -> [t][h*64+d], v -> vt[h][d][t]
     const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int d = (int) (i & 63);
-    const int64_t r = i >> 6;
-    const int t = (int) (r % T), h = (int) (r / T);
+    const int r = (int) (i >> 6);
+    const int t = r % T, h = r / T;
     const float qv = *(const float *) (q.base + voff(q, d, t, h, 0));
     const float kv = *(const float *) (k.base + voff(k, d, t, h, 0));
-    const float vv = *(const float *) (v.base + voff(v, t, d, h, 0));
     const int64_t o = (int64_t) t * H * 64 + h * 64 + d;
     const _Float16 a = (_Float16) qv, b = (_Float16) kv;
     qh[o] = a; ql[o] = (_Float16) (qv - (float) a);
     kh[o] = b; kl[o] = (_Float16) (kv - (float) b);
-    vt[((int64_t) h * 64 + d) * TP + t] = (_Float16) vv;
+    if (WITH_V) {
+        const float vv = *(const float *) (v.base + voff(v, t, d, h, 0));
+        vt[((int64_t) h * 64 + d) * TP + t] = (_Float16) vv;
+    }
+}
+
+// V^T operand of the fused attention, produced at the graph's CONT(permute(V)) node (qwen2-whisper.cpp:2081-2089)
+// from the CONT's source view (ne = [T, 64, H]; the CONT would copy it verbatim): vt[h][d][t] = fp16 V(t, d, h),
+// zero for T <= t < TP. One 64(t) x 64(d) tile per workgroup through LDS: reads run along d, writes along t.
+__global__ __launch_bounds__(256) void k_vt_tile(tview v, _Float16 * vt, int T, int TP) {
+    __shared__ float tile[64][65];
+    const int t0 = (int) blockIdx.x * 64, h = (int) blockIdx.y;
+    for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+        const int tt = idx >> 6, dd = idx & 63, t = t0 + tt;
+        tile[tt][dd] = t < T ? *(const float *) (v.base + voff(v, t, dd, h, 0)) : 0.0f;
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+        const int dd = idx >> 6, tt = idx & 63;
+        vt[((int64_t) h * 64 + dd) * TP + t0 + tt] = (_Float16) tile[tt][dd];
+    }
 }
 
 // fused attention output [t][h*64+d] (f32) -> the KQV node's layout dst (ne = [64, T, H])
@@ -472,6 +526,8 @@ struct q2a_backend_ctx {
     std::string name;
     hipStream_t stream = nullptr;
     void * scratch = nullptr;
+    _Float16 * vt_buf = nullptr;       // V^T operand of the fused attention, written at the V CONT node
+    size_t vt_bytes = 0;
     size_t scratch_bytes = 0;
     ggml_backend_q2a_stats stats{};
     // HIP graphs of recent graph_computes: the sched hands the same cgraphs (same nodes, buffers, parameters) on
@@ -671,7 +727,7 @@ const packed_w * get_packed(q2a_backend_ctx * b, const ggml_tensor * w) {
 // epi: Q2A_EPI_STORE_F (bias optional), Q2A_EPI_GELU_F (bias, GELU), Q2A_EPI_RESID (bias, + resid rows); the result
 // goes to `out` (op itself, or the last node of a fused MUL_MAT -> ADD [-> GELU | ADD] chain)
 void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = nullptr, int epi = Q2A_EPI_STORE_F,
-                 const float * bias = nullptr, const float * resid = nullptr) {
+                 const float * bias = nullptr, const float * resid = nullptr, float oscale = 0.0f) {
     if (!out) out = op;
     const ggml_tensor * w = op->src[0];
     const ggml_tensor * x = op->src[1];
@@ -683,13 +739,20 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
     const size_t a_bytes = ((size_t) M * K * 2 + 255) & ~size_t(255);
     const size_t dy_bytes = blk ? ((size_t) (K / blk) * MP * 4 + 255) & ~size_t(255) : 0;
     const size_t ae_bytes = blk == 256 ? (size_t) (K / 256) * MP * 32 : 0;
-    char * s = (char *) scratch(b, a_bytes + dy_bytes + ae_bytes);
+    // fp16 small-tile GEMMs (a single clip) split K like the engine's residual GEMMs (q2a_gemm_resid_ksplit: up to
+    // 4 partial [M][N] f32 planes, reduced in split order with the bias / residual / scale of the epilogue)
+    const bool split = blk == 0 && (epi == Q2A_EPI_RESID || epi == Q2A_EPI_STORE_F) && q2a_gemm_resid_ksplit(M, N, K, 0) > 1;
+    const size_t part_bytes = split ? (size_t) 4 * M * N * 4 : 0;
+    char * s = (char *) scratch(b, a_bytes + dy_bytes + ae_bytes + part_bytes);
     q2a_half * A = (q2a_half *) s;
     float * dy = (float *) (s + a_bytes);
     q2a_half * aext = (q2a_half *) (s + a_bytes + dy_bytes);
     if (blk == 0) {
         const int64_t n = (int64_t) M * K;
-        hipLaunchKernelGGL(k_f32_to_f16, grid1(n), dim3(256), 0, b->stream, (const float *) x->data, A, n);
+        if (n % 8 == 0 && ((uintptr_t) x->data & 15) == 0 && ((uintptr_t) A & 15) == 0)
+            hipLaunchKernelGGL(k_f32_to_f16_x8, grid1(n / 8), dim3(256), 0, b->stream, (const f4 *) x->data, (uint4 *) A, n / 8);
+        else
+            hipLaunchKernelGGL(k_f32_to_f16, grid1(n), dim3(256), 0, b->stream, (const float *) x->data, A, n);
     } else {
         q2a_quant_args qa{(const float *) x->data, nullptr, M, K, blk == 256 ? 1 : 2, A, dy, aext, MP};
         Q2A_HIP(q2a_launch_quant_act(qa, b->stream));
@@ -699,7 +762,12 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
     a.A = A; a.lda = K; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
     a.M = M; a.N = N; a.K = K; a.ldw = K;
     a.outF = (float *) out->data; a.ldo = N;
-    a.bias = bias; a.store_bias = bias != nullptr; a.resid = resid;
+    a.bias = bias; a.store_bias = bias != nullptr; a.resid = resid; a.out_scale = oscale;
+    if (split) {
+        a.part = (float *) (s + a_bytes + dy_bytes + ae_bytes);
+        a.split_stride = (int64_t) M * N;
+        a.split_store = 1;
+    }
     a.gelu_tab = gelu_table(b->device);
     if (blk == 0) {
         a.W = (const q2a_half *) w->data;
@@ -738,51 +806,85 @@ void run_mm_f32(q2a_backend_ctx * b, ggml_tensor * op) {
 // KQ = MUL_MAT(K, Q) -> SOFT_MAX(KQ, no mask) -> KQV = MUL_MAT(V, KQ_soft_max), heads of 64 (qwen2-whisper.cpp:
 // 2052-2106): when nodes i..i+2 form exactly this chain and KQ / KQ_soft_max feed nothing else, run it as the
 // engine's flash kernel and skip the 20 x T x T score tensors. Returns the number of nodes consumed (0 = no match).
-int try_fused_attention(q2a_backend_ctx * b, ggml_cgraph * g, int i) {
+// KQ -> SOFT_MAX -> KQV at nodes i..i+2 with K, Q, V views the fused kernel accepts (no other consumer of the score
+// tensors); returns the KQV node or null
+ggml_tensor * match_attention(ggml_cgraph * g, int i) {
     static const bool off = [] { const char * v = getenv("GGML_Q2A_NO_FUSED_ATTN"); return v && atoi(v); }();
-    if (off || i + 2 >= ggml_graph_n_nodes(g)) return 0;
+    if (off || i + 2 >= ggml_graph_n_nodes(g)) return nullptr;
     ggml_tensor * kq = ggml_graph_node(g, i);
     ggml_tensor * sm = ggml_graph_node(g, i + 1);
     ggml_tensor * kqv = ggml_graph_node(g, i + 2);
-    if (kq->op != GGML_OP_MUL_MAT || sm->op != GGML_OP_SOFT_MAX || kqv->op != GGML_OP_MUL_MAT) return 0;
-    if (sm->src[0] != kq || sm->src[1] != nullptr || kqv->src[1] != sm) return 0;
+    if (kq->op != GGML_OP_MUL_MAT || sm->op != GGML_OP_SOFT_MAX || kqv->op != GGML_OP_MUL_MAT) return nullptr;
+    if (sm->src[0] != kq || sm->src[1] != nullptr || kqv->src[1] != sm) return nullptr;
     float scale, max_bias;
     memcpy(&scale, (const float *) sm->op_params + 0, 4);
     memcpy(&max_bias, (const float *) sm->op_params + 1, 4);
-    if (scale != 1.0f || max_bias != 0.0f) return 0;
+    if (scale != 1.0f || max_bias != 0.0f) return nullptr;
     // the score tensors must be used by this chain only
     for (int j = 0; j < ggml_graph_n_nodes(g); ++j) {
         ggml_tensor * n = ggml_graph_node(g, j);
         if (n == sm || n == kqv) continue;
         for (int s = 0; s < GGML_MAX_SRC; ++s)
-            if (n->src[s] == kq || n->src[s] == sm) return 0;
+            if (n->src[s] == kq || n->src[s] == sm) return nullptr;
     }
-    if ((kq->flags | sm->flags) & GGML_TENSOR_FLAG_OUTPUT) return 0;
+    if ((kq->flags | sm->flags) & GGML_TENSOR_FLAG_OUTPUT) return nullptr;
     const ggml_tensor * K = kq->src[0];
     const ggml_tensor * Q = kq->src[1];
     const ggml_tensor * V = kqv->src[0];
     const int64_t T = Q->ne[1], H = Q->ne[2];
     auto f32 = [](const ggml_tensor * t) { return t->type == GGML_TYPE_F32 && t->nb[0] == 4 && t->ne[3] == 1; };
-    if (!f32(K) || !f32(Q) || !f32(V) || kqv->type != GGML_TYPE_F32 || kqv->ne[3] != 1) return 0;
-    if (Q->ne[0] != 64 || K->ne[0] != 64 || K->ne[1] != T || K->ne[2] != H) return 0;
-    if (V->ne[0] != T || V->ne[1] != 64 || V->ne[2] != H) return 0;
-    if (kqv->ne[0] != 64 || kqv->ne[1] != T || kqv->ne[2] != H) return 0;
+    if (!f32(K) || !f32(Q) || !f32(V) || kqv->type != GGML_TYPE_F32 || kqv->ne[3] != 1) return nullptr;
+    if (Q->ne[0] != 64 || K->ne[0] != 64 || K->ne[1] != T || K->ne[2] != H) return nullptr;
+    if (V->ne[0] != T || V->ne[1] != 64 || V->ne[2] != H) return nullptr;
+    if (kqv->ne[0] != 64 || kqv->ne[1] != T || kqv->ne[2] != H) return nullptr;
+    if (T * H * 64 >= (1ll << 31)) return nullptr;
+    return kqv;
+}
+
+_Float16 * vt_buffer(q2a_backend_ctx * b, size_t bytes) {
+    if (bytes > b->vt_bytes) {
+        Q2A_HIP(hipStreamSynchronize(b->stream));
+        if (b->vt_buf) Q2A_HIP(hipFree(b->vt_buf));
+        b->vt_buf = nullptr;
+        Q2A_HIP(hipMalloc((void **) &b->vt_buf, bytes));
+        b->vt_bytes = bytes;
+    }
+    return b->vt_buf;
+}
+
+// vt_ready: V^T was already written into b->vt_buf at V's CONT node. merged: the CONT of permute(KQV, 0,2,1,3)
+// that follows (qwen2-whisper.cpp:2105-2107), whose [t][h*64+d] rows are exactly the fused kernel's output rows —
+// the kernel writes them there directly. Returns the number of nodes consumed.
+int run_fused_attention(q2a_backend_ctx * b, ggml_cgraph * g, int i, bool vt_ready, ggml_tensor * merged) {
+    ggml_tensor * kq = ggml_graph_node(g, i);
+    ggml_tensor * kqv = ggml_graph_node(g, i + 2);
+    const ggml_tensor * K = kq->src[0];
+    const ggml_tensor * Q = kq->src[1];
+    const ggml_tensor * V = kqv->src[0];
+    const int64_t T = Q->ne[1], H = Q->ne[2];
     const int TP = (int) ((T + 63) / 64 * 64);
     const int64_t D = H * 64, n = T * D;
     const size_t hb = ((size_t) n * 2 + 255) & ~size_t(255);
     const size_t vb = ((size_t) H * 64 * TP * 2 + 255) & ~size_t(255);
     char * s = (char *) scratch(b, 4 * hb + vb + (size_t) n * 4);
     _Float16 *qh = (_Float16 *) s, *ql = (_Float16 *) (s + hb), *kh = (_Float16 *) (s + 2 * hb), *kl = (_Float16 *) (s + 3 * hb);
-    _Float16 * vt = (_Float16 *) (s + 4 * hb);
-    float * o = (float *) (s + 4 * hb + vb);
-    Q2A_HIP(hipMemsetAsync(vt, 0, vb, b->stream));   // V^T tail columns past T are read as zero weights
-    hipLaunchKernelGGL(k_attn_prep, grid1(n), dim3(256), 0, b->stream, tv(Q), tv(K), tv(V), qh, ql, kh, kl, vt, (int) T, (int) H, TP, n);
+    _Float16 * vt = vt_ready ? b->vt_buf : (_Float16 *) (s + 4 * hb);
+    float * o = merged ? (float *) merged->data : (float *) (s + 4 * hb + vb);
+    if (vt_ready) {
+        hipLaunchKernelGGL(k_attn_prep<false>, grid1(n), dim3(256), 0, b->stream, tv(Q), tv(K), tv(V), qh, ql, kh, kl, vt,
+                           (int) T, (int) H, TP, n);
+    } else {
+        Q2A_HIP(hipMemsetAsync(vt, 0, vb, b->stream));   // V^T tail columns past T are read as zero weights
+        hipLaunchKernelGGL(k_attn_prep<true>, grid1(n), dim3(256), 0, b->stream, tv(Q), tv(K), tv(V), qh, ql, kh, kl, vt,
+                           (int) T, (int) H, TP, n);
+    }
     q2a_attn_args at{(const q2a_half *) qh, (const q2a_half *) ql, (const q2a_half *) kh, (const q2a_half *) kl,
                      (const q2a_half *) vt, 1, (int) T, (int) D, (int) H, TP, nullptr, o};
     Q2A_HIP(q2a_launch_attention(at, b->stream));
-    hipLaunchKernelGGL(k_attn_out, grid1(n), dim3(256), 0, b->stream, (const float *) o, tv(kqv), (int) T, (int) H, n);
+    if (!merged)
+        hipLaunchKernelGGL(k_attn_out, grid1(n), dim3(256), 0, b->stream, (const float *) o, tv(kqv), (int) T, (int) H, n);
     b->stats.n_attn_fused++;
-    return 3;
+    return merged ? 5 : 3;
 }
 
 bool op_supported(const ggml_tensor * op) {
@@ -890,6 +992,33 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
         for (int k = 0; k < 4; ++k) if (x->ne[k] != y->ne[k]) return false;
         return ggml_is_contiguous(x) && ggml_is_contiguous(y) && x->type == GGML_TYPE_F32 && y->type == GGML_TYPE_F32;
     };
+    // the SCALE node fed by `prod` (directly or through one contiguous RESHAPE view) at node j, when every link is the
+    // sole consumer of the one before: its bytes are prod's bytes times the scale
+    auto scale_after = [&](ggml_tensor * prod, int j) -> ggml_tensor * {
+        ggml_tensor * t = node(j);
+        if (t && t->op == GGML_OP_RESHAPE && t->src[0] == prod && sole(prod, t)) {
+            prod = t;
+            t = node(j + 1);
+        }
+        if (!t || t->op != GGML_OP_SCALE || t->src[0] != prod || !sole(prod, t) || t->type != GGML_TYPE_F32 ||
+            !ggml_is_contiguous(t) || !ggml_is_contiguous(prod) || ggml_nelements(t) != ggml_nelements(prod) ||
+            ((uintptr_t) t->data & 15) != 0 || *(const float *) t->op_params == 0.0f)
+            return nullptr;
+        return t;
+    };
+    // V CONT nodes feeding a fused attention as its sole consumer: they produce the attention's V^T operand
+    std::unordered_map<const ggml_tensor *, int> vprep;
+    const ggml_tensor * vt_ready_for = nullptr;
+    if (!no_fuse) {
+        for (int j = 0; j + 2 < nn; ++j) {
+            ggml_tensor * kqv = match_attention(g, j);
+            if (!kqv) continue;
+            ggml_tensor * V = kqv->src[0];
+            if (V->op == GGML_OP_CONT && sole(V, kqv) && V->src[0] && V->src[0]->type == GGML_TYPE_F32 &&
+                ggml_are_same_shape(V, V->src[0]) && V->ne[1] == 64)
+                vprep[V] = j;
+        }
+    }
     for (int i = 0; i < nn; ++i) {
         ggml_tensor * op = ggml_graph_node(g, i);
         if (ggml_is_empty(op) || op->op == GGML_OP_NONE || op->op == GGML_OP_RESHAPE || op->op == GGML_OP_VIEW ||
@@ -902,8 +1031,24 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
         hipStream_t st = b->stream;
         switch (op->op) {
             case GGML_OP_MUL_MAT: {
-                const int used = try_fused_attention(b, g, i);
-                if (used) { i += used - 1; break; }
+                if (ggml_tensor * kqv = match_attention(g, i)) {
+                    ggml_tensor * merged = nullptr;
+                    ggml_tensor * p = node(i + 3), * c = node(i + 4);
+                    if (p && c && p->op == GGML_OP_PERMUTE && p->src[0] == kqv && sole(kqv, p) && c->op == GGML_OP_CONT &&
+                        c->src[0] == p && sole(p, c)) {
+                        const int32_t * ax = (const int32_t *) p->op_params;
+                        if (ax[0] == 0 && ax[1] == 2 && ax[2] == 1 && ax[3] == 3 && c->type == GGML_TYPE_F32 &&
+                            ggml_is_contiguous(c) && c->ne[0] == 64 * kqv->ne[2] && c->ne[1] == kqv->ne[1] &&
+                            c->ne[2] == 1 && c->ne[3] == 1 && ((uintptr_t) c->data & 15) == 0)
+                            merged = c;
+                    }
+                    const bool vt_ready = kqv->src[0] == vt_ready_for;
+                    const int used = run_fused_attention(b, g, i, vt_ready, merged);
+                    if (merged) b->stats.n_fused += 1;
+                    if (vt_ready) vt_ready_for = nullptr;
+                    i += used - 1;
+                    break;
+                }
                 if (!mm_fast_ok(op)) { run_mm_f32(b, op); b->stats.n_mul_mat_f32++; break; }
                 // MUL_MAT -> ADD(bias row) [-> GELU | -> ADD(residual)] on the GEMM epilogue
                 // (qwen2-whisper.cpp:2029-2037, 2120-2154): same f32 operations, one kernel, no [N][M] round trips
@@ -916,6 +1061,11 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                         run_mm_fast(b, op, n2, Q2A_EPI_GELU_F, bias);
                         b->stats.n_fused += 2;
                         i += 2;
+                    } else if (ggml_tensor * sc = scale_after(n1, i + 2)) {
+                        // Q: MUL_MAT -> ADD(bq) -> [RESHAPE] -> SCALE (qwen2-whisper.cpp:2029-2054)
+                        run_mm_fast(b, op, sc, Q2A_EPI_STORE_F, bias, nullptr, *(const float *) sc->op_params);
+                        b->stats.n_fused += 2;
+                        while (ggml_graph_node(g, i) != sc) ++i;
                     } else if (n2 && n2->op == GGML_OP_ADD && sole(n1, n2) && same_shape_rows(n1, n2) &&
                                ((uintptr_t) n2->data & 15) == 0) {
                         const ggml_tensor * r = n2->src[0] == n1 ? n2->src[1] : n2->src[0];
@@ -972,17 +1122,22 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                 }
                 // NORM -> MUL(weight row) -> ADD(bias row) (qwen2-whisper.cpp:2002-2006, 2124-2128, 2176-2180)
                 ggml_tensor * n1 = node(i + 1), * n2 = node(i + 2);
-                if (n1 && n2 && n1->op == GGML_OP_MUL && n1->src[0] == op && sole(op, n1) &&
+                const bool aff = n1 && n2 && n1->op == GGML_OP_MUL && n1->src[0] == op && sole(op, n1) &&
                     row_vec_f32(n1->src[1], op->ne[0]) && n2->op == GGML_OP_ADD && n2->src[0] == n1 && sole(n1, n2) &&
                     row_vec_f32(n2->src[1], op->ne[0]) && rows_f32(n2) && n1->type == GGML_TYPE_F32 &&
-                    ggml_are_same_shape(op, n2)) {
-                    hipLaunchKernelGGL(k_norm_row<true>, dim3(rows), dim3(256), 0, st, tv(s0), tv(n2), eps,
-                                       (const float *) n1->src[1]->data, (const float *) n2->src[1]->data);
+                    ggml_are_same_shape(op, n2);
+                ggml_tensor * out = aff ? n2 : op;
+                const bool v4 = op->ne[0] % 4 == 0 && aligned16(s0) && aligned16(out);
+                const float * w = aff ? (const float *) n1->src[1]->data : nullptr;
+                const float * bb = aff ? (const float *) n2->src[1]->data : nullptr;
+                const dim3 grid((rows + 3) / 4);
+                if (aff && v4) hipLaunchKernelGGL((k_norm_row<true, true>), grid, dim3(256), 0, st, tv(s0), tv(out), eps, w, bb, (int) rows);
+                else if (aff) hipLaunchKernelGGL((k_norm_row<true, false>), grid, dim3(256), 0, st, tv(s0), tv(out), eps, w, bb, (int) rows);
+                else if (v4) hipLaunchKernelGGL((k_norm_row<false, true>), grid, dim3(256), 0, st, tv(s0), tv(out), eps, w, bb, (int) rows);
+                else hipLaunchKernelGGL((k_norm_row<false, false>), grid, dim3(256), 0, st, tv(s0), tv(out), eps, w, bb, (int) rows);
+                if (aff) {
                     b->stats.n_fused += 2;
                     i += 2;
-                } else {
-                    hipLaunchKernelGGL(k_norm_row<false>, dim3(rows), dim3(256), 0, st, tv(s0), tv(op), eps,
-                                       (const float *) nullptr, (const float *) nullptr);
                 }
                 b->stats.n_other++;
                 break;
@@ -995,6 +1150,15 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                 break;
             }
             case GGML_OP_CONT: case GGML_OP_DUP: case GGML_OP_CPY: {
+                if (vprep.count(op) && !vt_ready_for) {   // V of a fused attention: its V^T operand instead of the f32 copy
+                    // (one pending at a time: a second V before the first attention is copied normally)
+                    const int T = (int) op->ne[0], H = (int) op->ne[2], TP = (T + 63) / 64 * 64;
+                    _Float16 * vt = vt_buffer(b, (size_t) H * 64 * TP * 2);
+                    hipLaunchKernelGGL(k_vt_tile, dim3((unsigned) (TP / 64), (unsigned) H), dim3(256), 0, st, tv(op->src[0]), vt, T, TP);
+                    vt_ready_for = op;
+                    b->stats.n_other++;
+                    break;
+                }
                 ggml_tensor * dst = op->op == GGML_OP_CPY ? op->src[1] : op;
                 if (n < (1ll << 31))
                     hipLaunchKernelGGL(k_copy<uint32_t>, grid1(n), dim3(256), 0, st, tv(s0), (int) s0->type, tv(dst), (int) dst->type, n);
@@ -1118,6 +1282,7 @@ void be_free(ggml_backend_t be) {
     (void) hipSetDevice(b->device);
     (void) hipStreamSynchronize(b->stream);
     if (b->scratch) (void) hipFree(b->scratch);
+    if (b->vt_buf) (void) hipFree(b->vt_buf);
     for (auto & e : b->graphs) if (e.exec) (void) hipGraphExecDestroy(e.exec);
     (void) hipStreamDestroy(b->stream);
     delete b;

@@ -449,7 +449,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (__builtin_amdgcn_s_memrealtime() - t0 < dt) __builtin_amdgcn_s_sleep(8);
     }
-    const int ksplit = (!PIPE && BLK == 0 && EPI == Q2A_EPI_RESID && p.ksplit > 1) ? p.ksplit : 1;
+    const int ksplit = (!PIPE && BLK == 0 && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) && p.ksplit > 1) ? p.ksplit : 1;
     const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, ntl = nbn * nbm, nwg = ntl * ksplit;
     const int bid = blockIdx.x, xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
     const int wgid_all = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
@@ -751,6 +751,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
         if (LUT_EPI && EPI != Q2A_EPI_GELU_H) v = gelu_lut_c(v, lut);
         else if (!LUT_EPI && (EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_GELU_F || EPI == Q2A_EPI_CONV2)) v = gelu_lut(v, p.gelu_tab);
         if (EPI == Q2A_EPI_QKV) v = v * vscale;   // ggml_scale after the bias add (:2054), exact 2^-3
+        if (EPI == Q2A_EPI_STORE_F && p.out_scale != 0.0f) v = v * p.out_scale;
         return v;
     };
     typedef _Float16 h4v __attribute__((ext_vector_type(4)));
@@ -850,7 +851,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                 }
             }
         }
-    } else if (EPI == Q2A_EPI_RESID && ksplit > 1) {
+    } else if ((EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) && ksplit > 1) {
         // split-K partial: raw accumulators to part[ks] ([M][N] f32); bias and residual in the reduce pass
         float * pb = p.part + (int64_t) ks * p.split_stride;
 #pragma unroll
@@ -896,9 +897,11 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
 #undef LDS_STAGE
 }
 
-// split-K reduce: out[m][n] = ((p_0 + p_1 + ...) + bias[n]) + out[m][n], partials summed in split order
+// split-K reduce: out[m][n] = ((p_0 + p_1 + ...) + bias[n]) + x[m][n], partials summed in split order; x = resid rows
+// or out itself. RES = 0 (Q2A_EPI_STORE_F): ((p_0 + p_1 + ...) [+ bias[n]]) [* oscale]
+template <int RES>
 __global__ void k_split_reduce(const float * __restrict__ part, int S, int64_t stride, int M, int N, const float * bias,
-                               float * out, int64_t ldo, const float * resid) {
+                               float * out, int64_t ldo, const float * resid, float oscale) {
     const int64_t i4 = ((int64_t) blockIdx.x * blockDim.x + threadIdx.x) * 4;
     if (i4 >= (int64_t) M * N) return;
     const int m = (int) (i4 / N), n = (int) (i4 - (int64_t) m * N);
@@ -908,23 +911,41 @@ __global__ void k_split_reduce(const float * __restrict__ part, int S, int64_t s
 #pragma unroll
         for (int r = 0; r < 4; ++r) acc[r] = acc[r] + v[r];
     }
-    const f4 b = *(const f4 *) (bias + n);
     f4 * o = (f4 *) (out + (int64_t) m * ldo + n);
-    f4 x = resid ? *(const f4 *) (resid + (int64_t) m * ldo + n) : *o;
+    if (RES) {
+        const f4 b = *(const f4 *) (bias + n);
+        f4 x = resid ? *(const f4 *) (resid + (int64_t) m * ldo + n) : *o;
 #pragma unroll
-    for (int r = 0; r < 4; ++r) x[r] = (acc[r] + b[r]) + x[r];
-    *o = x;
+        for (int r = 0; r < 4; ++r) x[r] = (acc[r] + b[r]) + x[r];
+        *o = x;
+    } else {
+        if (bias) {
+            const f4 b = *(const f4 *) (bias + n);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] = acc[r] + b[r];
+        }
+        if (oscale != 0.0f) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) acc[r] = acc[r] * oscale;
+        }
+        *o = acc;
+    }
 }
 
 template <int BM, int BN, int WM, int WN, int EPI, int BLK, int PIPE = 0>
 hipError_t launch_cfg(const q2a_gemm_args & a, hipStream_t s) {
-    const bool split = !PIPE && (BLK == 0 || BLK == Q2A_BLK_BF16) && EPI == Q2A_EPI_RESID && a.ksplit > 1;
+    const bool split = !PIPE && (BLK == 0 || BLK == Q2A_BLK_BF16) && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) &&
+                       a.ksplit > 1;
     const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM) * (split ? a.ksplit : 1);
     hipLaunchKernelGGL((k_gemm<BM, BN, WM, WN, EPI, BLK, PIPE>), dim3(nwg), dim3(WM * WN * 64), 0, s, a);
     if (split) {
         const int64_t n4 = (int64_t) a.M * a.N / 4;
-        hipLaunchKernelGGL(k_split_reduce, dim3((unsigned) ((n4 + 255) / 256)), dim3(256), 0, s, a.part, a.ksplit,
-                           a.split_stride, a.M, a.N, a.bias, a.outF, a.ldo, a.resid);
+        if constexpr (EPI == Q2A_EPI_RESID)
+            hipLaunchKernelGGL(k_split_reduce<1>, dim3((unsigned) ((n4 + 255) / 256)), dim3(256), 0, s, a.part, a.ksplit,
+                               a.split_stride, a.M, a.N, a.bias, a.outF, a.ldo, a.resid, 0.0f);
+        else
+            hipLaunchKernelGGL(k_split_reduce<0>, dim3((unsigned) ((n4 + 255) / 256)), dim3(256), 0, s, a.part, a.ksplit,
+                               a.split_stride, a.M, a.N, a.store_bias ? a.bias : nullptr, a.outF, a.ldo, a.resid, a.out_scale);
     }
     return hipGetLastError();
 }
@@ -1000,7 +1021,7 @@ hipError_t q2a_launch_gemm(const q2a_gemm_args & a_in, int epi, int blk, hipStre
     q2a_gemm_args a = a_in;
     a.stagger_ns = st_ns; a.stagger_g = st_g;
     a.group_m = grp;
-    if (epi != Q2A_EPI_RESID || !a.part || a.ldo != a.N) a.ksplit = 0;
+    if (!(epi == Q2A_EPI_RESID || (epi == Q2A_EPI_STORE_F && a.split_store)) || !a.part || a.ldo != a.N) a.ksplit = 0;
     else a.ksplit = q2a_gemm_resid_ksplit(a.M, a.N, a.K, blk);
     if (a.N % 128 != 0 || a.K % BK != 0 || a.M <= 0) return hipErrorInvalidValue;
     if (blk > 1 && (a.K % blk != 0)) return hipErrorInvalidValue;

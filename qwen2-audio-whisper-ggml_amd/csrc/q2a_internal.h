@@ -73,6 +73,8 @@ struct q2a_gemm_args {
     // ggml-backend fusions (ggml-q2a.hip): MUL_MAT -> ADD(bias) [-> ADD(residual)] on the f32 epilogues
     const float * resid;              // Q2A_EPI_RESID: residual rows [M][ldo] (null = outF itself, in place)
     int store_bias;                   // Q2A_EPI_STORE_F: 1 = outF = acc + bias[n], 0 = raw accumulators
+    float out_scale;                  // Q2A_EPI_STORE_F: != 0 -> outF = (acc [+ bias]) * out_scale (ggml_scale after the add)
+    int split_store;                  // Q2A_EPI_STORE_F: 1 = allow the small-tile split-K (part/split_stride) like RESID
 };
 
 // the launcher's split factor for a small-tile Q2A_EPI_RESID GEMM (0 = none): a function of K only, so every batch

@@ -108,8 +108,9 @@ def test_backend_fusions_match_per_node(harness, make_model, make_clip, tmp_path
     assert info_p["fused"] == 0, info_p
     fused, info_f = run(harness, model, clip, tmp_path)
     L = 2
-    # per layer: Q and V bias, O bias + residual, fc1 bias + GELU, fc2 bias + residual, two LayerNorm affines;
+    # per layer: Q bias + scale, V bias, O bias + residual, fc1 bias + GELU, fc2 bias + residual, two LayerNorm affines,
+    # the attention output CONT;
     # plus the final LayerNorm affine
-    assert info_f["fused"] == 12 * L + 2, info_f
+    assert info_f["fused"] == 14 * L + 2, info_f
     assert info_f["other"] < info_p["other"], (info_f, info_p)
     assert np.array_equal(fused, plain)
