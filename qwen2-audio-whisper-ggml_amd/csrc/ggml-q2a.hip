@@ -234,7 +234,8 @@ __global__ __launch_bounds__(256) void k_norm(tview a, tview d, float eps) {
 // barriers. Mean and variance are double sums (ggml.c:11941-11990); y = (x - mean) * scale, then y * w, then + b,
 // each rounded to f32 (no contraction). V4: ne0 % 4 == 0 and 16-B aligned rows.
 template <bool AFF, bool V4>
-__global__ __launch_bounds__(256) void k_norm_row(tview a, tview d, float eps, const float * w, const float * bb, int nrows) {
+__global__ __launch_bounds__(256) void k_norm_row(tview a, tview d, float eps, const float * w, const float * bb, int nrows,
+                                                  _Float16 * yh) {
     const int r = (int) blockIdx.x * 4 + (int) (threadIdx.x >> 6);
     if (r >= nrows) return;
     const int lane = threadIdx.x & 63;
@@ -296,6 +297,10 @@ __global__ __launch_bounds__(256) void k_norm_row(tview a, tview d, float eps, c
         }
         if (V4) ((f4 *) y)[j] = f4{o[0], o[W > 1 ? 1 : 0], o[W > 2 ? 2 : 0], o[W > 3 ? 3 : 0]};
         else y[j] = o[0];
+        if (yh) {   // fp16 (RNE) copy of the row for the F16-weight GEMMs that consume it: ggml's vec_dot_type conversion
+#pragma unroll
+            for (int q = 0; q < W; ++q) yh[(int64_t) r * n + j * W + q] = (_Float16) o[q];
+        }
     }
 }
 
@@ -528,6 +533,12 @@ struct q2a_backend_ctx {
     void * scratch = nullptr;
     _Float16 * vt_buf = nullptr;       // V^T operand of the fused attention, written at the V CONT node
     size_t vt_bytes = 0;
+    // fp16 shadows of f32 activations written by their producer (LayerNorm, fc1 GELU epilogue) for F16-weight
+    // MUL_MATs that would otherwise convert them: two slots, a producer never writes the slot its own GEMM reads
+    _Float16 * a16[2] = {nullptr, nullptr};
+    size_t a16_bytes[2] = {0, 0};
+    const ggml_tensor * a16_src[2] = {nullptr, nullptr};
+    int a16_last = 1;
     size_t scratch_bytes = 0;
     ggml_backend_q2a_stats stats{};
     // HIP graphs of recent graph_computes: the sched hands the same cgraphs (same nodes, buffers, parameters) on
@@ -727,7 +738,8 @@ const packed_w * get_packed(q2a_backend_ctx * b, const ggml_tensor * w) {
 // epi: Q2A_EPI_STORE_F (bias optional), Q2A_EPI_GELU_F (bias, GELU), Q2A_EPI_RESID (bias, + resid rows); the result
 // goes to `out` (op itself, or the last node of a fused MUL_MAT -> ADD [-> GELU | ADD] chain)
 void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = nullptr, int epi = Q2A_EPI_STORE_F,
-                 const float * bias = nullptr, const float * resid = nullptr, float oscale = 0.0f) {
+                 const float * bias = nullptr, const float * resid = nullptr, float oscale = 0.0f,
+                 _Float16 * out16 = nullptr) {
     if (!out) out = op;
     const ggml_tensor * w = op->src[0];
     const ggml_tensor * x = op->src[1];
@@ -747,7 +759,12 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
     q2a_half * A = (q2a_half *) s;
     float * dy = (float *) (s + a_bytes);
     q2a_half * aext = (q2a_half *) (s + a_bytes + dy_bytes);
-    if (blk == 0) {
+    const _Float16 * shadow = nullptr;
+    if (blk == 0)
+        for (int k = 0; k < 2; ++k) if (b->a16_src[k] == x) shadow = b->a16[k];
+    if (shadow) {
+        A = (q2a_half *) shadow;   // the producer already wrote the fp16 operand
+    } else if (blk == 0) {
         const int64_t n = (int64_t) M * K;
         if (n % 8 == 0 && ((uintptr_t) x->data & 15) == 0 && ((uintptr_t) A & 15) == 0)
             hipLaunchKernelGGL(k_f32_to_f16_x8, grid1(n / 8), dim3(256), 0, b->stream, (const f4 *) x->data, (uint4 *) A, n / 8);
@@ -763,6 +780,7 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
     a.M = M; a.N = N; a.K = K; a.ldw = K;
     a.outF = (float *) out->data; a.ldo = N;
     a.bias = bias; a.store_bias = bias != nullptr; a.resid = resid; a.out_scale = oscale;
+    if (epi == Q2A_EPI_GELU_F) a.outH = (q2a_half *) out16;
     if (split) {
         a.part = (float *) (s + a_bytes + dy_bytes + ae_bytes);
         a.split_stride = (int64_t) M * N;
@@ -850,6 +868,22 @@ _Float16 * vt_buffer(q2a_backend_ctx * b, size_t bytes) {
         b->vt_bytes = bytes;
     }
     return b->vt_buf;
+}
+
+// a shadow slot for the fp16 copy of tensor t (the slot not written last)
+_Float16 * claim_a16(q2a_backend_ctx * b, const ggml_tensor * t) {
+    const int k = 1 - b->a16_last;
+    const size_t bytes = (size_t) ggml_nelements(t) * 2;
+    if (bytes > b->a16_bytes[k]) {
+        Q2A_HIP(hipStreamSynchronize(b->stream));
+        if (b->a16[k]) Q2A_HIP(hipFree(b->a16[k]));
+        b->a16[k] = nullptr;
+        Q2A_HIP(hipMalloc((void **) &b->a16[k], bytes));
+        b->a16_bytes[k] = bytes;
+    }
+    b->a16_last = k;
+    b->a16_src[k] = t;
+    return b->a16[k];
 }
 
 // vt_ready: V^T was already written into b->vt_buf at V's CONT node. merged: the CONT of permute(KQV, 0,2,1,3)
@@ -1009,7 +1043,14 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
     // V CONT nodes feeding a fused attention as its sole consumer: they produce the attention's V^T operand
     std::unordered_map<const ggml_tensor *, int> vprep;
     const ggml_tensor * vt_ready_for = nullptr;
+    // f32 activations some F16-weight MUL_MAT converts to fp16: their producer also writes the fp16 copy
+    std::unordered_map<const ggml_tensor *, int> want16;
+    b->a16_src[0] = b->a16_src[1] = nullptr;
     if (!no_fuse) {
+        for (int j = 0; j < nn; ++j) {
+            const ggml_tensor * t = ggml_graph_node(g, j);
+            if (t->op == GGML_OP_MUL_MAT && t->src[0]->type == GGML_TYPE_F16 && mm_fast_ok(t)) want16[t->src[1]] = j;
+        }
         for (int j = 0; j + 2 < nn; ++j) {
             ggml_tensor * kqv = match_attention(g, j);
             if (!kqv) continue;
@@ -1058,7 +1099,8 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                     const float * bias = (const float *) n1->src[1]->data;
                     if (n2 && n2->op == GGML_OP_UNARY && ggml_get_unary_op(n2) == GGML_UNARY_OP_GELU && n2->src[0] == n1 &&
                         sole(n1, n2) && same_shape_rows(n1, n2) && ((uintptr_t) n2->data & 15) == 0 && !mm_is_pipe8(op)) {
-                        run_mm_fast(b, op, n2, Q2A_EPI_GELU_F, bias);
+                        _Float16 * out16 = want16.count(n2) && ggml_is_contiguous(n2) ? claim_a16(b, n2) : nullptr;
+                        run_mm_fast(b, op, n2, Q2A_EPI_GELU_F, bias, nullptr, 0.0f, out16);
                         b->stats.n_fused += 2;
                         i += 2;
                     } else if (ggml_tensor * sc = scale_after(n1, i + 2)) {
@@ -1131,10 +1173,11 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                 const float * w = aff ? (const float *) n1->src[1]->data : nullptr;
                 const float * bb = aff ? (const float *) n2->src[1]->data : nullptr;
                 const dim3 grid((rows + 3) / 4);
-                if (aff && v4) hipLaunchKernelGGL((k_norm_row<true, true>), grid, dim3(256), 0, st, tv(s0), tv(out), eps, w, bb, (int) rows);
-                else if (aff) hipLaunchKernelGGL((k_norm_row<true, false>), grid, dim3(256), 0, st, tv(s0), tv(out), eps, w, bb, (int) rows);
-                else if (v4) hipLaunchKernelGGL((k_norm_row<false, true>), grid, dim3(256), 0, st, tv(s0), tv(out), eps, w, bb, (int) rows);
-                else hipLaunchKernelGGL((k_norm_row<false, false>), grid, dim3(256), 0, st, tv(s0), tv(out), eps, w, bb, (int) rows);
+                _Float16 * yh = want16.count(out) && ggml_is_contiguous(out) ? claim_a16(b, out) : nullptr;
+                if (aff && v4) hipLaunchKernelGGL((k_norm_row<true, true>), grid, dim3(256), 0, st, tv(s0), tv(out), eps, w, bb, (int) rows, yh);
+                else if (aff) hipLaunchKernelGGL((k_norm_row<true, false>), grid, dim3(256), 0, st, tv(s0), tv(out), eps, w, bb, (int) rows, yh);
+                else if (v4) hipLaunchKernelGGL((k_norm_row<false, true>), grid, dim3(256), 0, st, tv(s0), tv(out), eps, w, bb, (int) rows, yh);
+                else hipLaunchKernelGGL((k_norm_row<false, false>), grid, dim3(256), 0, st, tv(s0), tv(out), eps, w, bb, (int) rows, yh);
                 if (aff) {
                     b->stats.n_fused += 2;
                     i += 2;
@@ -1283,6 +1326,7 @@ void be_free(ggml_backend_t be) {
     (void) hipStreamSynchronize(b->stream);
     if (b->scratch) (void) hipFree(b->scratch);
     if (b->vt_buf) (void) hipFree(b->vt_buf);
+    for (int k = 0; k < 2; ++k) if (b->a16[k]) (void) hipFree(b->a16[k]);
     for (auto & e : b->graphs) if (e.exec) (void) hipGraphExecDestroy(e.exec);
     (void) hipStreamDestroy(b->stream);
     delete b;

@@ -891,6 +891,11 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
                     else if (EPI == Q2A_EPI_CONV2) v[r] = add[j][r] + v[r];   // pe + gelu(...)
                 }
                 if (Q2A_ST) q2a_st(v, (f4 *) (orow + 16 * j));
+                if (EPI == Q2A_EPI_GELU_F && p.outH) {   // fp16 copy (exact: GELU table values are fp16) for the next GEMM
+                    typedef _Float16 h4s __attribute__((ext_vector_type(4)));
+                    const h4s hv = {(_Float16) v[0], (_Float16) v[1], (_Float16) v[2], (_Float16) v[3]};
+                    *(h4s *) (p.outH + (int64_t) m * p.ldo + cbase + 4 * q + 16 * j) = hv;
+                }
             }
         }
     }

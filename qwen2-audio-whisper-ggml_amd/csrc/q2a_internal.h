@@ -40,7 +40,7 @@ struct q2a_gemm_args {
     const float * bias;
     float * outF;
     int64_t ldo;
-    q2a_half * outH;
+    q2a_half * outH;                  // (Q2A_EPI_GELU_F: optional fp16 copy of outF, same row stride)
     int o_rpg, o_gstride, o_off;      // output row remap for outH: (m / o_rpg) * o_gstride + (m % o_rpg) + o_off
     int o_dup;                        // Q2A_EPI_GELU_H: also store the row at column offset o_dup (0 = no copy)
     const float * pe;
