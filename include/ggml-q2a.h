@@ -47,6 +47,7 @@ typedef struct {
     int n_nodes, n_mul_mat_fast, n_mul_mat_f32, n_attn_fused, n_other;
     int n_graph_replayed;
     int n_fused;
+    int n_mm_grouped;   /* launches that ran two weight MUL_MATs of the same activation together */
 } ggml_backend_q2a_stats;
 GGML_API void ggml_backend_q2a_get_stats(ggml_backend_t backend, ggml_backend_q2a_stats * stats);
 

@@ -735,11 +735,27 @@ const packed_w * get_packed(q2a_backend_ctx * b, const ggml_tensor * w) {
     return &d->wcache.back();
 }
 
+struct mm_chain {          // a fast MUL_MAT and the nodes its epilogue absorbs
+    ggml_tensor * out;     // last node of the chain (where the result goes)
+    int epi;
+    const float * bias;
+    const float * resid;
+    float oscale;
+    int last;              // graph index of `out`
+    int nfused;            // nodes absorbed
+};
+struct mm_second {         // the second GEMM of a grouped launch (same activation, fp16 weight of the same shape)
+    const ggml_tensor * w;
+    ggml_tensor * out;
+    const float * bias;
+    float oscale;
+};
+
 // epi: Q2A_EPI_STORE_F (bias optional), Q2A_EPI_GELU_F (bias, GELU), Q2A_EPI_RESID (bias, + resid rows); the result
 // goes to `out` (op itself, or the last node of a fused MUL_MAT -> ADD [-> GELU | ADD] chain)
 void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = nullptr, int epi = Q2A_EPI_STORE_F,
                  const float * bias = nullptr, const float * resid = nullptr, float oscale = 0.0f,
-                 _Float16 * out16 = nullptr) {
+                 _Float16 * out16 = nullptr, const mm_second * sec = nullptr) {
     if (!out) out = op;
     const ggml_tensor * w = op->src[0];
     const ggml_tensor * x = op->src[1];
@@ -753,7 +769,8 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
     const size_t ae_bytes = blk == 256 ? (size_t) (K / 256) * MP * 32 : 0;
     // fp16 small-tile GEMMs (a single clip) split K like the engine's residual GEMMs (q2a_gemm_resid_ksplit: up to
     // 4 partial [M][N] f32 planes, reduced in split order with the bias / residual / scale of the epilogue)
-    const bool split = blk == 0 && (epi == Q2A_EPI_RESID || epi == Q2A_EPI_STORE_F) && q2a_gemm_resid_ksplit(M, N, K, 0) > 1;
+    const bool split = !sec && blk == 0 && (epi == Q2A_EPI_RESID || epi == Q2A_EPI_STORE_F) &&
+                       q2a_gemm_resid_ksplit(M, N, K, 0) > 1;
     const size_t part_bytes = split ? (size_t) 4 * M * N * 4 : 0;
     char * s = (char *) scratch(b, a_bytes + dy_bytes + ae_bytes + part_bytes);
     q2a_half * A = (q2a_half *) s;
@@ -781,6 +798,12 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
     a.outF = (float *) out->data; a.ldo = N;
     a.bias = bias; a.store_bias = bias != nullptr; a.resid = resid; a.out_scale = oscale;
     if (epi == Q2A_EPI_GELU_F) a.outH = (q2a_half *) out16;
+    if (sec) {
+        a.ngroup = 2;
+        a.W2 = (const q2a_half *) sec->w->data;
+        a.bias2 = sec->bias; a.store_bias2 = sec->bias != nullptr;
+        a.outF2 = (float *) sec->out->data; a.out_scale2 = sec->oscale;
+    }
     if (split) {
         a.part = (float *) (s + a_bytes + dy_bytes + ae_bytes);
         a.split_stride = (int64_t) M * N;
@@ -964,6 +987,11 @@ bool mm_is_pipe8(const ggml_tensor * op) {
     return q2a_gemm_wide_tiles((int) M, (int) op->src[0]->ne[1], 0);
 }
 
+bool is_view_op(const ggml_tensor * t) {
+    return t->op == GGML_OP_NONE || t->op == GGML_OP_RESHAPE || t->op == GGML_OP_VIEW || t->op == GGML_OP_PERMUTE ||
+           t->op == GGML_OP_TRANSPOSE || ggml_is_empty(t);
+}
+
 bool rows_f32(const ggml_tensor * t) { return t->type == GGML_TYPE_F32 && t->nb[0] == 4; }
 bool row_vec_f32(const ggml_tensor * t, int64_t n) {
     return rows_f32(t) && t->ne[0] == n && t->ne[1] == 1 && t->ne[2] == 1 && t->ne[3] == 1 && ((uintptr_t) t->data & 15) == 0;
@@ -1060,6 +1088,31 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                 vprep[V] = j;
         }
     }
+    // the epilogue chain that follows the fast MUL_MAT at node j (see the MUL_MAT case)
+    auto chain_of = [&](int j) -> mm_chain {
+        ggml_tensor * op = ggml_graph_node(g, j);
+        mm_chain c{op, Q2A_EPI_STORE_F, nullptr, nullptr, 0.0f, j, 0};
+        ggml_tensor * n1 = node(j + 1), * n2 = node(j + 2);
+        if (no_fuse || !n1 || n1->op != GGML_OP_ADD || n1->src[0] != op || !sole(op, n1) ||
+            !row_vec_f32(n1->src[1], op->ne[0]) || !same_shape_rows(op, n1) || ((uintptr_t) n1->data & 15) != 0)
+            return c;
+        c.bias = (const float *) n1->src[1]->data;
+        c.out = n1; c.last = j + 1; c.nfused = 1;
+        if (n2 && n2->op == GGML_OP_UNARY && ggml_get_unary_op(n2) == GGML_UNARY_OP_GELU && n2->src[0] == n1 &&
+            sole(n1, n2) && same_shape_rows(n1, n2) && ((uintptr_t) n2->data & 15) == 0 && !mm_is_pipe8(op)) {
+            c.epi = Q2A_EPI_GELU_F; c.out = n2; c.last = j + 2; c.nfused = 2;
+        } else if (ggml_tensor * sc = scale_after(n1, j + 2)) {
+            c.oscale = *(const float *) sc->op_params; c.out = sc; c.nfused = 2;
+            c.last = j + 2;
+            while (ggml_graph_node(g, c.last) != sc) ++c.last;
+        } else if (n2 && n2->op == GGML_OP_ADD && sole(n1, n2) && same_shape_rows(n1, n2) && ((uintptr_t) n2->data & 15) == 0) {
+            const ggml_tensor * r = n2->src[0] == n1 ? n2->src[1] : n2->src[0];
+            if (r != n1 && same_shape_rows(n1, r) && ((uintptr_t) r->data & 15) == 0) {
+                c.epi = Q2A_EPI_RESID; c.resid = (const float *) r->data; c.out = n2; c.last = j + 2; c.nfused = 2;
+            }
+        }
+        return c;
+    };
     for (int i = 0; i < nn; ++i) {
         ggml_tensor * op = ggml_graph_node(g, i);
         if (ggml_is_empty(op) || op->op == GGML_OP_NONE || op->op == GGML_OP_RESHAPE || op->op == GGML_OP_VIEW ||
@@ -1091,44 +1144,34 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                     break;
                 }
                 if (!mm_fast_ok(op)) { run_mm_f32(b, op); b->stats.n_mul_mat_f32++; break; }
-                // MUL_MAT -> ADD(bias row) [-> GELU | -> ADD(residual)] on the GEMM epilogue
-                // (qwen2-whisper.cpp:2029-2037, 2120-2154): same f32 operations, one kernel, no [N][M] round trips
-                ggml_tensor * n1 = node(i + 1), * n2 = node(i + 2);
-                if (n1 && n1->op == GGML_OP_ADD && n1->src[0] == op && sole(op, n1) && row_vec_f32(n1->src[1], op->ne[0]) &&
-                    same_shape_rows(op, n1) && ((uintptr_t) n1->data & 15) == 0) {
-                    const float * bias = (const float *) n1->src[1]->data;
-                    if (n2 && n2->op == GGML_OP_UNARY && ggml_get_unary_op(n2) == GGML_UNARY_OP_GELU && n2->src[0] == n1 &&
-                        sole(n1, n2) && same_shape_rows(n1, n2) && ((uintptr_t) n2->data & 15) == 0 && !mm_is_pipe8(op)) {
-                        _Float16 * out16 = want16.count(n2) && ggml_is_contiguous(n2) ? claim_a16(b, n2) : nullptr;
-                        run_mm_fast(b, op, n2, Q2A_EPI_GELU_F, bias, nullptr, 0.0f, out16);
-                        b->stats.n_fused += 2;
-                        i += 2;
-                    } else if (ggml_tensor * sc = scale_after(n1, i + 2)) {
-                        // Q: MUL_MAT -> ADD(bq) -> [RESHAPE] -> SCALE (qwen2-whisper.cpp:2029-2054)
-                        run_mm_fast(b, op, sc, Q2A_EPI_STORE_F, bias, nullptr, *(const float *) sc->op_params);
-                        b->stats.n_fused += 2;
-                        while (ggml_graph_node(g, i) != sc) ++i;
-                    } else if (n2 && n2->op == GGML_OP_ADD && sole(n1, n2) && same_shape_rows(n1, n2) &&
-                               ((uintptr_t) n2->data & 15) == 0) {
-                        const ggml_tensor * r = n2->src[0] == n1 ? n2->src[1] : n2->src[0];
-                        if (r != n1 && same_shape_rows(n1, r) && ((uintptr_t) r->data & 15) == 0) {
-                            run_mm_fast(b, op, n2, Q2A_EPI_RESID, bias, (const float *) r->data);
-                            b->stats.n_fused += 2;
-                            i += 2;
-                        } else {
-                            run_mm_fast(b, op, n1, Q2A_EPI_STORE_F, bias);
-                            b->stats.n_fused += 1;
-                            i += 1;
-                        }
-                    } else {
-                        run_mm_fast(b, op, n1, Q2A_EPI_STORE_F, bias);
-                        b->stats.n_fused += 1;
-                        i += 1;
+                // MUL_MAT -> ADD(bias row) [-> GELU | -> ADD(residual) | -> [RESHAPE] -> SCALE] on the GEMM epilogue
+                // (qwen2-whisper.cpp:2029-2054, 2120-2154): same f32 operations, one kernel, no [N][M] round trips
+                mm_chain c1 = chain_of(i);
+                // two consecutive projections of the same activation with plain / bias / bias+scale epilogues (the K
+                // and Q projections, :2029-2062) run as one grouped launch: twice the workgroups of either alone
+                int j2 = c1.last + 1;   // the next node that executes (views in between are free)
+                while (node(j2) && is_view_op(node(j2))) ++j2;
+                ggml_tensor * m2 = node(j2);
+                if (c1.epi == Q2A_EPI_STORE_F && !no_fuse && m2 && m2->op == GGML_OP_MUL_MAT && m2->src[1] == op->src[1] &&
+                    op->src[0]->type == GGML_TYPE_F16 && m2->src[0]->type == GGML_TYPE_F16 && mm_fast_ok(m2) &&
+                    !match_attention(g, j2) && ggml_are_same_shape(m2->src[0], op->src[0]) && !mm_is_pipe8(op)) {
+                    const mm_chain c2 = chain_of(j2);
+                    if (c2.epi == Q2A_EPI_STORE_F) {
+                        mm_second sec{m2->src[0], c2.out, c2.bias, c2.oscale};
+                        run_mm_fast(b, op, c1.out, Q2A_EPI_STORE_F, c1.bias, nullptr, c1.oscale, nullptr, &sec);
+                        b->stats.n_fused += c1.nfused + c2.nfused;
+                        b->stats.n_mul_mat_fast += 2;
+                        b->stats.n_mm_grouped++;
+                        i = c2.last;
+                        break;
                     }
-                } else {
-                    run_mm_fast(b, op);
                 }
+                _Float16 * out16 = c1.epi == Q2A_EPI_GELU_F && want16.count(c1.out) && ggml_is_contiguous(c1.out)
+                                       ? claim_a16(b, c1.out) : nullptr;
+                run_mm_fast(b, op, c1.out, c1.epi, c1.bias, c1.resid, c1.oscale, out16);
+                b->stats.n_fused += c1.nfused;
                 b->stats.n_mul_mat_fast++;
+                i = c1.last;
                 break;
             }
             case GGML_OP_ADD: case GGML_OP_MUL:

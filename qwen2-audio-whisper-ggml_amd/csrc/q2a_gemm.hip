@@ -412,7 +412,8 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 }
 
 template <int BM, int BN, int WM, int WN, int EPI, int BLK_, int PIPE>
-__global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p) {
+__global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_arg) {
+    q2a_gemm_args p = p_arg;   // (the grouped STORE_F launch swaps in its second GEMM's operands below)
     constexpr bool BF = BLK_ == Q2A_BLK_BF16;              // bf16 operands, no block scales
     constexpr int BLK = BF ? 0 : BLK_;
     constexpr int NW = WM * WN;
@@ -449,10 +450,19 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p)
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (__builtin_amdgcn_s_memrealtime() - t0 < dt) __builtin_amdgcn_s_sleep(8);
     }
-    const int ksplit = (!PIPE && BLK == 0 && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) && p.ksplit > 1) ? p.ksplit : 1;
-    const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, ntl = nbn * nbm, nwg = ntl * ksplit;
+    constexpr bool GROUPABLE = !PIPE && !BF && BLK == 0 && EPI == Q2A_EPI_STORE_F;
+    const int ngrp = (GROUPABLE && p.ngroup == 2) ? 2 : 1;
+    const int ksplit = (!PIPE && BLK == 0 && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) && p.ksplit > 1 && ngrp == 1)
+                           ? p.ksplit : 1;
+    const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, ntl = nbn * nbm, nwg = ntl * ksplit * ngrp;
     const int bid = blockIdx.x, xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
-    const int wgid_all = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+    int wgid_all = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
+    if constexpr (GROUPABLE) {
+        if (ngrp == 2 && wgid_all >= ntl) {
+            wgid_all -= ntl;
+            p.W = p.W2; p.bias = p.bias2; p.outF = p.outF2; p.out_scale = p.out_scale2; p.store_bias = p.store_bias2;
+        }
+    }
     const int ks = wgid_all / ntl, wgid = wgid_all - ks * ntl;   // K-split index, tile index
     const int GM = p.group_m > 0 ? p.group_m : GROUP_M;
     const int gsize = GM * nbn, g = wgid / gsize, gr = wgid % gsize;
@@ -939,9 +949,10 @@ __global__ void k_split_reduce(const float * __restrict__ part, int S, int64_t s
 
 template <int BM, int BN, int WM, int WN, int EPI, int BLK, int PIPE = 0>
 hipError_t launch_cfg(const q2a_gemm_args & a, hipStream_t s) {
+    const bool grouped = !PIPE && BLK == 0 && EPI == Q2A_EPI_STORE_F && a.ngroup == 2;
     const bool split = !PIPE && (BLK == 0 || BLK == Q2A_BLK_BF16) && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) &&
-                       a.ksplit > 1;
-    const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM) * (split ? a.ksplit : 1);
+                       a.ksplit > 1 && !grouped;
+    const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM) * (split ? a.ksplit : 1) * (grouped ? 2 : 1);
     hipLaunchKernelGGL((k_gemm<BM, BN, WM, WN, EPI, BLK, PIPE>), dim3(nwg), dim3(WM * WN * 64), 0, s, a);
     if (split) {
         const int64_t n4 = (int64_t) a.M * a.N / 4;
@@ -1026,7 +1037,9 @@ hipError_t q2a_launch_gemm(const q2a_gemm_args & a_in, int epi, int blk, hipStre
     q2a_gemm_args a = a_in;
     a.stagger_ns = st_ns; a.stagger_g = st_g;
     a.group_m = grp;
-    if (!(epi == Q2A_EPI_RESID || (epi == Q2A_EPI_STORE_F && a.split_store)) || !a.part || a.ldo != a.N) a.ksplit = 0;
+    if (a.ngroup == 2 && (epi != Q2A_EPI_STORE_F || blk != 0 || wide_tiles(a.M, a.N))) return hipErrorInvalidValue;
+    if (!(epi == Q2A_EPI_RESID || (epi == Q2A_EPI_STORE_F && a.split_store)) || !a.part || a.ldo != a.N || a.ngroup == 2)
+        a.ksplit = 0;
     else a.ksplit = q2a_gemm_resid_ksplit(a.M, a.N, a.K, blk);
     if (a.N % 128 != 0 || a.K % BK != 0 || a.M <= 0) return hipErrorInvalidValue;
     if (blk > 1 && (a.K % blk != 0)) return hipErrorInvalidValue;

@@ -75,6 +75,14 @@ struct q2a_gemm_args {
     int store_bias;                   // Q2A_EPI_STORE_F: 1 = outF = acc + bias[n], 0 = raw accumulators
     float out_scale;                  // Q2A_EPI_STORE_F: != 0 -> outF = (acc [+ bias]) * out_scale (ggml_scale after the add)
     int split_store;                  // Q2A_EPI_STORE_F: 1 = allow the small-tile split-K (part/split_stride) like RESID
+    // Q2A_EPI_STORE_F, small tiles, fp16 weights: ngroup = 2 runs a second GEMM with the same A, M, N, K in the same
+    // launch (its own W / bias / output / scale), e.g. the K and Q projections of one layer; no split-K then
+    int ngroup;
+    const q2a_half * W2;
+    const float * bias2;
+    float * outF2;
+    float out_scale2;
+    int store_bias2;
 };
 
 // the launcher's split factor for a small-tile Q2A_EPI_RESID GEMM (0 = none): a function of K only, so every batch

@@ -102,15 +102,19 @@ def test_backend_graph_replay_matches_direct(harness, make_model, make_clip, tmp
 def test_backend_fusions_match_per_node(harness, make_model, make_clip, tmp_path, wt):
     """Nodes folded into their producer's kernel (MUL_MAT -> ADD bias [-> GELU | ADD residual] on the GEMM epilogue,
     NORM -> MUL -> ADD in one row kernel) compute the same f32 operations as the per-node launches
-    (GGML_Q2A_NO_FUSE=1): embd_enc is bit-identical."""
+    (GGML_Q2A_NO_FUSE=1): embd_enc is bit-identical. Both runs without the single-clip split-K
+    (Q2A_GEMM_NO_SPLITK=1): the grouped K|Q launch never splits, so with it on the fp32 summation orders would differ
+    (its accuracy is what the golden tests above check)."""
     model, clip = make_model("tiny", wt), make_clip(1)
-    plain, info_p = run(harness, model, clip, tmp_path, {"GGML_Q2A_NO_FUSE": "1"})
-    assert info_p["fused"] == 0, info_p
-    fused, info_f = run(harness, model, clip, tmp_path)
+    plain, info_p = run(harness, model, clip, tmp_path, {"GGML_Q2A_NO_FUSE": "1", "Q2A_GEMM_NO_SPLITK": "1"})
+    assert info_p["fused"] == 0 and info_p["mm_grouped"] == 0, info_p
+    fused, info_f = run(harness, model, clip, tmp_path, {"Q2A_GEMM_NO_SPLITK": "1"})
     L = 2
     # per layer: Q bias + scale, V bias, O bias + residual, fc1 bias + GELU, fc2 bias + residual, two LayerNorm affines,
     # the attention output CONT;
     # plus the final LayerNorm affine
     assert info_f["fused"] == 14 * L + 2, info_f
+    # the K and Q projections of each layer run as one grouped launch (F16 weights)
+    assert info_f["mm_grouped"] == (L if wt == "f16" else 0), info_f
     assert info_f["other"] < info_p["other"], (info_f, info_p)
     assert np.array_equal(fused, plain)
