@@ -16,7 +16,9 @@ for m in f16 q4_k; do
   echo "$m nograph $(cat gpurun_out/gb_${m}_nograph.json)"
   cmp $W/out_$m.f32 $W/out_${m}_ng.f32 && echo "$m graph == nograph (bitwise)"
 done
-if [ -n "$GB_PROF" ]; then   # kernel trace of the F16 run: GPU time per whisper_full vs the wall clock
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/gb_prof -o gb --output-format csv -- \
-    oracle/_ref/ggml_harness encode $W/full-f16.bin $W/clip0.f32 $W/out_prof.f32 8 > gpurun_out/gb_prof.json
+if [ -n "$GB_PROF" ]; then   # kernel traces: GPU time per whisper_full vs the wall clock
+  for m in f16 q4_k; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/gb_prof_$m -o gb --output-format csv -- \
+      oracle/_ref/ggml_harness encode $W/full-$m.bin $W/clip0.f32 $W/out_prof.f32 8 > gpurun_out/gb_prof_$m.json
+  done
 fi

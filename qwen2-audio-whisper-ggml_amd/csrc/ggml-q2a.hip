@@ -539,6 +539,8 @@ struct q2a_backend_ctx {
     size_t a16_bytes[2] = {0, 0};
     const ggml_tensor * a16_src[2] = {nullptr, nullptr};
     int a16_last = 1;
+    const ggml_tensor * quant_src = nullptr;   // activation whose quantized image is in the scratch (see run_mm_fast)
+    int quant_blk = 0;
     size_t scratch_bytes = 0;
     ggml_backend_q2a_stats stats{};
     // HIP graphs of recent graph_computes: the sched hands the same cgraphs (same nodes, buffers, parameters) on
@@ -688,6 +690,7 @@ dim3 grid1(int64_t n) { return dim3((unsigned) ((n + 255) / 256)); }
 
 void * scratch(q2a_backend_ctx * b, size_t bytes) {
     if (bytes > b->scratch_bytes) {
+        b->quant_src = nullptr;
         Q2A_HIP(hipStreamSynchronize(b->stream));
         if (b->scratch) Q2A_HIP(hipFree(b->scratch));
         b->scratch = nullptr;
@@ -787,10 +790,14 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
             hipLaunchKernelGGL(k_f32_to_f16_x8, grid1(n / 8), dim3(256), 0, b->stream, (const f4 *) x->data, (uint4 *) A, n / 8);
         else
             hipLaunchKernelGGL(k_f32_to_f16, grid1(n), dim3(256), 0, b->stream, (const float *) x->data, A, n);
-    } else {
+    } else if (b->quant_src != x || b->quant_blk != blk) {
         q2a_quant_args qa{(const float *) x->data, nullptr, M, K, blk == 256 ? 1 : 2, A, dy, aext, MP};
         Q2A_HIP(q2a_launch_quant_act(qa, b->stream));
     }
+    // the scratch now holds x's quantized image (Q8_K / Q8_0 codes and scales): the next quantized-weight MUL_MAT of
+    // the same activation (the Q, K, V projections) reuses it; an fp16 conversion overwrote it
+    b->quant_src = blk ? x : nullptr;
+    b->quant_blk = blk;
     q2a_gemm_args a;
     memset(&a, 0, sizeof(a));
     a.A = A; a.lda = K; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
@@ -924,6 +931,7 @@ int run_fused_attention(q2a_backend_ctx * b, ggml_cgraph * g, int i, bool vt_rea
     const size_t hb = ((size_t) n * 2 + 255) & ~size_t(255);
     const size_t vb = ((size_t) H * 64 * TP * 2 + 255) & ~size_t(255);
     char * s = (char *) scratch(b, 4 * hb + vb + (size_t) n * 4);
+    b->quant_src = nullptr;   // the attention operands overwrite the scratch
     _Float16 *qh = (_Float16 *) s, *ql = (_Float16 *) (s + hb), *kh = (_Float16 *) (s + 2 * hb), *kl = (_Float16 *) (s + 3 * hb);
     _Float16 * vt = vt_ready ? b->vt_buf : (_Float16 *) (s + 4 * hb);
     float * o = merged ? (float *) merged->data : (float *) (s + 4 * hb + vb);
@@ -1074,6 +1082,7 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
     // f32 activations some F16-weight MUL_MAT converts to fp16: their producer also writes the fp16 copy
     std::unordered_map<const ggml_tensor *, int> want16;
     b->a16_src[0] = b->a16_src[1] = nullptr;
+    b->quant_src = nullptr;
     if (!no_fuse) {
         for (int j = 0; j < nn; ++j) {
             const ggml_tensor * t = ggml_graph_node(g, j);
