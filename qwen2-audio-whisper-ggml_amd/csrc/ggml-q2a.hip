@@ -772,9 +772,10 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
     const size_t ae_bytes = blk == 256 ? (size_t) (K / 256) * MP * 32 : 0;
     // fp16 small-tile GEMMs (a single clip) split K like the engine's residual GEMMs (q2a_gemm_resid_ksplit: up to
     // 4 partial [M][N] f32 planes, reduced in split order with the bias / residual / scale of the epilogue)
-    const bool split = !sec && blk == 0 && (epi == Q2A_EPI_RESID || epi == Q2A_EPI_STORE_F) &&
-                       q2a_gemm_resid_ksplit(M, N, K, 0) > 1;
-    const size_t part_bytes = split ? (size_t) 4 * M * N * 4 : 0;
+    const int nsplit = sec || !(epi == Q2A_EPI_RESID || epi == Q2A_EPI_STORE_F) ? 0
+                       : blk == 0 ? q2a_gemm_resid_ksplit(M, N, K, 0) : q2a_gemm_kq_ksplit(M, N, K, blk);
+    const bool split = nsplit > 1;
+    const size_t part_bytes = split ? (size_t) nsplit * M * N * 4 : 0;
     char * s = (char *) scratch(b, a_bytes + dy_bytes + ae_bytes + part_bytes);
     q2a_half * A = (q2a_half *) s;
     float * dy = (float *) (s + a_bytes);
@@ -815,6 +816,7 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
         a.part = (float *) (s + a_bytes + dy_bytes + ae_bytes);
         a.split_stride = (int64_t) M * N;
         a.split_store = 1;
+        a.split_kq = 1;
     }
     a.gelu_tab = gelu_table(b->device);
     if (blk == 0) {

@@ -452,8 +452,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     }
     constexpr bool GROUPABLE = !PIPE && !BF && BLK == 0 && EPI == Q2A_EPI_STORE_F;
     const int ngrp = (GROUPABLE && p.ngroup == 2) ? 2 : 1;
-    const int ksplit = (!PIPE && BLK == 0 && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) && p.ksplit > 1 && ngrp == 1)
-                           ? p.ksplit : 1;
+    const int ksplit = (!PIPE && (BLK == 0 || BLK == 256 || BLK == 32) && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) &&
+                        p.ksplit > 1 && ngrp == 1) ? p.ksplit : 1;
     const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, ntl = nbn * nbm, nwg = ntl * ksplit * ngrp;
     const int bid = blockIdx.x, xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
     int wgid_all = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
@@ -545,8 +545,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
 
         const int nk = p.K / BK / ksplit;                 // K-steps of this split
         const int kb0 = ks * nk * BK;                     // its first K element
+        const int gb0 = BLK == 256 ? kb0 / 256 : kb0 / BK;   // its first scale group (whole groups per split)
         stage(LDS_STAGE(0), kb0);
-        if (BLK == 32) scale_load(0);
+        if (BLK == 32) scale_load(gb0);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (BLK == 32) scale_store(0);
         __syncthreads();
@@ -557,7 +558,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
             // Q4_K: block kt/4's scales are fetched at its first K-step and land in LDS at its end (3 steps early);
             // Q8_0: the next K-step's two blocks are fetched one step ahead into the other buffer.
             const bool sload = BLK == 256 ? (kt % 4 == 0) : (BLK == 32 && kt + 1 < nk);
-            if (sload) scale_load(BLK == 256 ? kt / 4 : kt + 1);
+            if (sload) scale_load(gb0 + (BLK == 256 ? kt / 4 : kt + 1));
             const char * ia = LDS_STAGE(cur);
             const char * iw = LDS_STAGE(cur) + BM * ROWB;
     #pragma unroll
@@ -950,8 +951,8 @@ __global__ void k_split_reduce(const float * __restrict__ part, int S, int64_t s
 template <int BM, int BN, int WM, int WN, int EPI, int BLK, int PIPE = 0>
 hipError_t launch_cfg(const q2a_gemm_args & a, hipStream_t s) {
     const bool grouped = !PIPE && BLK == 0 && EPI == Q2A_EPI_STORE_F && a.ngroup == 2;
-    const bool split = !PIPE && (BLK == 0 || BLK == Q2A_BLK_BF16) && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) &&
-                       a.ksplit > 1 && !grouped;
+    const bool split = !PIPE && (BLK == 0 || BLK == Q2A_BLK_BF16 || BLK == 256 || BLK == 32) &&
+                       (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) && a.ksplit > 1 && !grouped;
     const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM) * (split ? a.ksplit : 1) * (grouped ? 2 : 1);
     hipLaunchKernelGGL((k_gemm<BM, BN, WM, WN, EPI, BLK, PIPE>), dim3(nwg), dim3(WM * WN * 64), 0, s, a);
     if (split) {
@@ -1030,6 +1031,16 @@ int q2a_gemm_resid_ksplit(int M, int N, int K, int blk) {
     return S && nk % S == 0 ? S : 0;
 }
 
+int q2a_gemm_kq_ksplit(int M, int N, int K, int blk) {
+    static const int off = [] { const char * v = getenv("Q2A_GEMM_NO_SPLITK"); return v ? atoi(v) : 0; }();
+    if (off || !(blk == 256 || blk == 32) || wide_tiles(M, N) || N % 128) return 0;
+    // whole scale groups per split: 4 K-steps per Q4_K block, 1 per Q8_0/Q4_0 pair of blocks
+    const int nk = K / BK, unit = blk == 256 ? 4 : 1;
+    for (int S : {4, 5, 2, 3})
+        if (nk % (S * unit) == 0 && nk / S >= 2 * unit) return S;
+    return 0;
+}
+
 hipError_t q2a_launch_gemm(const q2a_gemm_args & a_in, int epi, int blk, hipStream_t s) {
     static const int st_ns = [] { const char * v = getenv("Q2A_GEMM_STAGGER_NS"); return v ? atoi(v) : 0; }();
     static const int st_g = [] { const char * v = getenv("Q2A_GEMM_STAGGER_G"); return v ? std::max(1, atoi(v)) : 2; }();
@@ -1040,6 +1051,7 @@ hipError_t q2a_launch_gemm(const q2a_gemm_args & a_in, int epi, int blk, hipStre
     if (a.ngroup == 2 && (epi != Q2A_EPI_STORE_F || blk != 0 || wide_tiles(a.M, a.N))) return hipErrorInvalidValue;
     if (!(epi == Q2A_EPI_RESID || (epi == Q2A_EPI_STORE_F && a.split_store)) || !a.part || a.ldo != a.N || a.ngroup == 2)
         a.ksplit = 0;
+    else if (blk == 256 || blk == 32) a.ksplit = a.split_kq ? q2a_gemm_kq_ksplit(a.M, a.N, a.K, blk) : 0;
     else a.ksplit = q2a_gemm_resid_ksplit(a.M, a.N, a.K, blk);
     if (a.N % 128 != 0 || a.K % BK != 0 || a.M <= 0) return hipErrorInvalidValue;
     if (blk > 1 && (a.K % blk != 0)) return hipErrorInvalidValue;

@@ -83,11 +83,14 @@ struct q2a_gemm_args {
     float * outF2;
     float out_scale2;
     int store_bias2;
+    int split_kq;                     // allow the small-tile split-K for k-quant / Q8_0 / Q4_0 weights (q2a_gemm_kq_ksplit)
 };
 
 // the launcher's split factor for a small-tile Q2A_EPI_RESID GEMM (0 = none): a function of K only, so every batch
 // size on the small-tile path sums in the same order (batch and single-clip results stay bit-identical)
 int q2a_gemm_resid_ksplit(int M, int N, int K, int blk);
+// the same for the block-quantized weights (whole scale groups per split), used when a.split_kq is set
+int q2a_gemm_kq_ksplit(int M, int N, int K, int blk);
 // blk: 0 (plain fp16 GEMM), 256 (Q4_K x Q8_K), 32 (Q8_0/Q4_0 x Q8_0), Q2A_BLK_BF16 (bf16 x bf16 MFMA, no block
 // scales: the bf16-activation mode, whose fp16-typed operand and output pointers then hold bf16 bits)
 constexpr int Q2A_BLK_BF16 = 1;
