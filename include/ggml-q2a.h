@@ -48,6 +48,7 @@ typedef struct {
     int n_graph_replayed;
     int n_fused;
     int n_mm_grouped;   /* launches that ran two weight MUL_MATs of the same activation together */
+    int n_mul_mat_conv; /* MUL_MAT(F32 im2col, F16 kernel) on the fp16 MFMA GEMM with hi/lo-split activations */
 } ggml_backend_q2a_stats;
 GGML_API void ggml_backend_q2a_get_stats(ggml_backend_t backend, ggml_backend_q2a_stats * stats);
 

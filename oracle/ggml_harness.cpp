@@ -82,10 +82,10 @@ int cmd_encode(int argc, char ** argv) {
     fclose(f);
     printf("{\"ne0\": %lld, \"ne1\": %lld, \"reps\": %d, \"best_s\": %.6f, \"mean_s\": %.6f, \"backend\": \"%s\", "
            "\"embd_buffer\": \"%s\", \"n_splits_encode\": %d, \"nodes\": %d, \"mul_mat_fast\": %d, \"mul_mat_f32\": %d, "
-           "\"attn_fused\": %d, \"other\": %d, \"graph_replayed\": %d, \"fused\": %d, \"mm_grouped\": %d, \"best_mel_s\": %.6f, \"best_encode_s\": %.6f}\n",
+           "\"attn_fused\": %d, \"other\": %d, \"graph_replayed\": %d, \"fused\": %d, \"mm_grouped\": %d, \"mm_conv\": %d, \"best_mel_s\": %.6f, \"best_encode_s\": %.6f}\n",
            (long long) e->ne[0], (long long) e->ne[1], reps, best, total / reps, ggml_backend_name(be),
            ggml_backend_buffer_name(e->buffer), ggml_backend_sched_get_n_splits(ctx->state->sched_encode.sched),
-           st.n_nodes, st.n_mul_mat_fast, st.n_mul_mat_f32, st.n_attn_fused, st.n_other, st.n_graph_replayed, st.n_fused, st.n_mm_grouped, best_mel,
+           st.n_nodes, st.n_mul_mat_fast, st.n_mul_mat_f32, st.n_attn_fused, st.n_other, st.n_graph_replayed, st.n_fused, st.n_mm_grouped, st.n_mul_mat_conv, best_mel,
            best_enc);
     whisper_free(ctx);
     return 0;

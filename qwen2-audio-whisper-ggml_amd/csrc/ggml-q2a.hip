@@ -493,6 +493,41 @@ __global__ void k_attn_out(const float * o, tview d, int T, int H, int64_t n) {
     *(float *) (d.base + voff(d, dd, t, h, 0)) = o[(int64_t) t * H * 64 + h * 64 + dd];
 }
 
+// MUL_MAT(F32 im2col, F16 conv kernel) on the fp16 MFMA GEMM (the conv2 graph node, qwen2-whisper.cpp:1926-1931 via
+// ggml_conv_1d): every f32 activation x = hi + lo with hi = fp16(x), lo = fp16(x - hi) (22 significant bits; the
+// product with the fp16 weight and its f32 accumulation then sit at the f32 summation-order level), operand rows
+// [M][K] -> [M][2K] = hi | lo against weight rows duplicated [N][2K] = w | w
+__global__ void k_hilo_rows(const float * x, _Float16 * a, int K, int n) {
+    const int i = (int) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int m = i / K, k = i - m * K;
+    const float v = x[i];
+    const _Float16 h = (_Float16) v;
+    a[(int64_t) m * 2 * K + k] = h;
+    a[(int64_t) m * 2 * K + K + k] = (_Float16) (v - (float) h);
+}
+__global__ void k_dup_rows(const _Float16 * w, _Float16 * o, int K, int n) {
+    const int i = (int) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int r = i / K, k = i - r * K;
+    o[(int64_t) r * 2 * K + k] = w[i];
+    o[(int64_t) r * 2 * K + K + k] = w[i];
+}
+// t [R][C] -> o [C][R] (f32), 64x64 tiles through LDS
+__global__ __launch_bounds__(256) void k_transpose_f32(const float * t, float * o, int R, int C) {
+    __shared__ float tile[64][65];
+    const int r0 = (int) blockIdx.y * 64, c0 = (int) blockIdx.x * 64;
+    for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+        const int rr = idx >> 6, cc = idx & 63;
+        if (r0 + rr < R && c0 + cc < C) tile[rr][cc] = t[(int64_t) (r0 + rr) * C + c0 + cc];
+    }
+    __syncthreads();
+    for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
+        const int cc = idx >> 6, rr = idx & 63;
+        if (r0 + rr < R && c0 + cc < C) o[(int64_t) (c0 + cc) * R + r0 + rr] = tile[rr][cc];
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // devices, buffers, weight cache
 // ------------------------------------------------------------------------------------------------
@@ -839,6 +874,72 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
     Q2A_HIP(q2a_launch_gemm(a, epi, blk, b->stream));
 }
 
+// the conv kernel duplicated into [N][2K] (w | w), cached like the repacked weights (dropped when its bytes change)
+const packed_w * get_dup16(q2a_backend_ctx * b, const ggml_tensor * w, int N, int K) {
+    constexpr int DUP16 = -16;   // cache tag (not a ggml type)
+    q2a_device_ctx * d = dev_ctx(b->device);
+    {
+        std::lock_guard<std::mutex> lk(d->mu);
+        for (const packed_w & p : d->wcache)
+            if (p.raw == (const char *) w->data && p.type == DUP16 && p.N == N && p.K == K) return &p;
+    }
+    packed_w p{};
+    p.raw = (const char *) w->data; p.raw_bytes = ggml_nbytes(w); p.type = DUP16; p.N = N; p.K = K;
+    Q2A_HIP(hipStreamSynchronize(b->stream));
+    Q2A_HIP(hipMalloc(&p.dev, (size_t) N * 2 * K * 2));
+    const int n = N * K;
+    hipLaunchKernelGGL(k_dup_rows, grid1(n), dim3(256), 0, b->stream, (const _Float16 *) w->data, (_Float16 *) p.dev, K, n);
+    Q2A_HIP(hipStreamSynchronize(b->stream));
+    std::lock_guard<std::mutex> lk(d->mu);
+    d->wcache.push_back(p);
+    return &d->wcache.back();
+}
+
+bool conv_hilo_ok(const ggml_tensor * op) {
+    static const bool off = [] { const char * v = getenv("GGML_Q2A_NO_CONV_HILO"); return v && atoi(v); }();
+    const ggml_tensor * x = op->src[0];
+    const ggml_tensor * w = op->src[1];
+    if (off || x->type != GGML_TYPE_F32 || w->type != GGML_TYPE_F16 || op->type != GGML_TYPE_F32) return false;
+    if (!ggml_is_contiguous(x) || !ggml_is_contiguous(w) || !ggml_is_contiguous(op)) return false;
+    if (x->ne[2] != 1 || x->ne[3] != 1 || w->ne[2] != 1 || w->ne[3] != 1) return false;
+    const int64_t K = x->ne[0], M = x->ne[1], N = w->ne[1];
+    return K % 32 == 0 && N % 128 == 0 && 2 * K <= 16384 && M * K < (1ll << 30) && N * K < (1ll << 30);
+}
+
+// out[n][m] = sum_k x[m][k] * w[n][k] (ggml MUL_MAT with src0 = x F32, src1 = w F16): GEMM [M][N] into the scratch,
+// then one transpose into the node's [N][M] layout
+void run_mm_conv_hilo(q2a_backend_ctx * b, ggml_tensor * op) {
+    const ggml_tensor * x = op->src[0];
+    const ggml_tensor * w = op->src[1];
+    const int K = (int) x->ne[0], M = (int) x->ne[1], N = (int) w->ne[1];
+    const packed_w * wd = get_dup16(b, w, N, K);
+    const int S = q2a_gemm_resid_ksplit(M, N, 2 * K, 0);
+    const size_t a_bytes = ((size_t) M * 2 * K * 2 + 255) & ~size_t(255);
+    const size_t t_bytes = ((size_t) M * N * 4 + 255) & ~size_t(255);
+    const size_t p_bytes = S > 1 ? (size_t) S * M * N * 4 : 0;
+    char * s = (char *) scratch(b, a_bytes + t_bytes + p_bytes);
+    b->quant_src = nullptr;
+    _Float16 * A = (_Float16 *) s;
+    float * tmp = (float *) (s + a_bytes);
+    const int n = M * K;
+    hipLaunchKernelGGL(k_hilo_rows, grid1(n), dim3(256), 0, b->stream, (const float *) x->data, A, K, n);
+    q2a_gemm_args a;
+    memset(&a, 0, sizeof(a));
+    a.A = (const q2a_half *) A; a.lda = 2 * K; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
+    a.M = M; a.N = N; a.K = 2 * K; a.ldw = 2 * K;
+    a.W = (const q2a_half *) wd->dev;
+    a.outF = tmp; a.ldo = N;
+    a.gelu_tab = gelu_table(b->device);
+    if (S > 1) {
+        a.part = (float *) (s + a_bytes + t_bytes);
+        a.split_stride = (int64_t) M * N;
+        a.split_store = 1;
+    }
+    Q2A_HIP(q2a_launch_gemm(a, Q2A_EPI_STORE_F, 0, b->stream));
+    hipLaunchKernelGGL(k_transpose_f32, dim3((unsigned) ((N + 63) / 64), (unsigned) ((M + 63) / 64)), dim3(256), 0, b->stream,
+                       (const float *) tmp, (float *) op->data, M, N);
+}
+
 void run_mm_f32(q2a_backend_ctx * b, ggml_tensor * op) {
     const ggml_tensor * s0 = op->src[0];
     const ggml_tensor * s1 = op->src[1];
@@ -1154,6 +1255,7 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                     i += used - 1;
                     break;
                 }
+                if (!mm_fast_ok(op) && conv_hilo_ok(op)) { run_mm_conv_hilo(b, op); b->stats.n_mul_mat_conv++; break; }
                 if (!mm_fast_ok(op)) { run_mm_f32(b, op); b->stats.n_mul_mat_f32++; break; }
                 // MUL_MAT -> ADD(bias row) [-> GELU | -> ADD(residual) | -> [RESHAPE] -> SCALE] on the GEMM epilogue
                 // (qwen2-whisper.cpp:2029-2054, 2120-2154): same f32 operations, one kernel, no [N][M] round trips
