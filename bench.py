@@ -10,7 +10,9 @@ GPUs every rank runs its own 64 clips (weak scaling; N=8 is configs[3], batch=51
 synthetic (deterministic splitmix64 generator at the real Qwen2-Audio encoder shapes), generated and quantized
 on rank 0, packed into the device layout and broadcast to every rank with one RCCL broadcast.
 
-Prints ONE JSON line on rank 0. Multi-GPU: torchrun --nproc-per-node N bench.py --gpus N ...
+Prints ONE JSON line on rank 0. Multi-GPU: `python bench.py --gpus N` launches N ranks itself (torchrun as a child
+process, started before this process touches any GPU); the driver's own `torchrun --nproc-per-node N bench.py --gpus N`
+works the same way. A WORLD_SIZE that disagrees with --gpus is an error, never a silent 1-GPU run.
 """
 from __future__ import annotations
 
@@ -83,14 +85,8 @@ def synth_clips(first: int, n: int) -> np.ndarray:
     return out
 
 
-def cpu_baseline(model_path: str, workdir: str, threads: int, reps: int) -> dict | None:
-    """The reference ggml CPU path (oracle/_ref/ref_harness, compiled from /root/reference sources with
-    -O3 -march=x86-64-v3) on one synthetic 30 s clip per rep, on the host cores of this box."""
+def _ref_encode(model_path: str, clip: str, workdir: str, threads: int, reps: int) -> dict | None:
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
-    if not os.path.exists(harness):
-        return None
-    clip = os.path.join(workdir, "clip0.f32")
-    synth_clips(0, 1)[0].tofile(clip)
     outp = os.path.join(workdir, "ref_out.f32")
     try:
         r = subprocess.run([harness, "encode", model_path, clip, outp, str(threads), str(reps)], check=True,
@@ -98,11 +94,87 @@ def cpu_baseline(model_path: str, workdir: str, threads: int, reps: int) -> dict
     except Exception as ex:  # noqa: BLE001
         log("cpu baseline failed:", ex)
         return None
-    info = json.loads(r.stdout.strip().splitlines()[-1])
-    return {"value": round(T_MEL / info["mean_s"], 2), "unit": "audio-frames/s", "cores": threads,
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+def cpu_baseline(model_path: str, wt: str, workdir: str, reps: int) -> dict | None:
+    """The reference ggml CPU path itself (oracle/_ref/ref_harness: /root/reference's sources compiled -O3
+    -march=x86-64-v3, kind "reference") timed on this box's host cores, one synthetic 30 s clip per rep through
+    whisper_full, clips run sequentially on one context. Legs (~25 s of CPU work in all):
+      main     the workload's weight type, n_threads = the CPU share this process may use (affinity, capped by
+               OMP_NUM_THREADS: the box allots 16 host CPUs per GPU; lscpu / nproc are recorded beside it)
+      default  same weights, n_threads = min(4, hw) — examples/main/main.cpp:33's default
+      f16x1    configs[1] (fp16 weights, one clip) at the main thread count (when the workload is not F16)."""
+    if not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "ref_harness")):
+        return None
+    hw = host_cpu_info()
+    share = hw["affinity"] or 1
+    if hw["omp_num_threads"] and hw["omp_num_threads"].isdigit():
+        share = min(share, int(hw["omp_num_threads"]))
+    clip = os.path.join(workdir, "clip0.f32")
+    synth_clips(0, 1)[0].tofile(clip)
+    main = _ref_encode(model_path, clip, workdir, share, reps)
+    if main is None:
+        return None
+    legs = {}
+    dflt_threads = min(4, hw["os_cpu_count"] or 4)
+    d = _ref_encode(model_path, clip, workdir, dflt_threads, 1)
+    if d:
+        legs["default_threads"] = {"value": round(T_MEL / d["mean_s"], 2), "threads": dflt_threads, "weights": wt,
+                                   "s_per_clip": round(d["mean_s"], 3)}
+    if wt != "f16":
+        f16 = _ref_encode(os.path.join(workdir, "full-f16.bin"), clip, workdir, share, 1)
+        if f16:
+            legs["configs1_f16x1"] = {"value": round(T_MEL / f16["mean_s"], 2), "threads": share, "weights": "f16",
+                                      "s_per_clip": round(f16["mean_s"], 3)}
+    return {"value": round(T_MEL / main["mean_s"], 2), "unit": "audio-frames/s", "cores": share,
             "kind": "reference",
-            "sample": f"{reps} x one 30 s clip through whisper_full (ggml CPU backend, n_threads={threads}, "
-                      f"-O3 -march=x86-64-v3), mean {info['mean_s']:.2f} s/clip"}
+            "sample": f"{reps} x one 30 s clip ({wt} weights) through whisper_full (ggml CPU backend, n_threads={share}, "
+                      f"-O3 -march=x86-64-v3), mean {main['mean_s']:.2f} s/clip",
+            "gflops_per_s": round(FLOP_PER_CLIP / main["mean_s"] / 1e9, 1),
+            "legs": legs, "host": hw}
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n: int) -> int:
+    """`--gpus N` without a torchrun environment: run this script as N ranks (one process per GPU) under
+    torch.distributed.run as a CHILD process and return its exit code. Called before anything initialises the GPU
+    (only device_count, which does not, on this image): the parent never holds a GPU context."""
+    import torch
+    have = torch.cuda.device_count()
+    if have < n and os.environ.get("Q2A_BENCH_REHEARSE") != "1":
+        log(f"bench: --gpus {n} but only {have} visible device(s)")
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
+def host_cpu_info() -> dict:
+    """What the CPU baseline ran on: the box's CPUs (nproc / lscpu) and the share this process may use."""
+    info = {"os_cpu_count": os.cpu_count()}
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+    except AttributeError:
+        info["affinity"] = os.cpu_count()
+    info["omp_num_threads"] = os.environ.get("OMP_NUM_THREADS")
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        want = ("Model name", "Socket(s)", "Core(s) per socket", "Thread(s) per core", "CPU(s)")
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in want:
+                info["lscpu_" + k.strip().replace("(s)", "s").replace(" ", "_").lower()] = v.strip()
+    except Exception:  # noqa: BLE001
+        pass
+    return info
 
 
 def main():
@@ -113,11 +185,16 @@ def main():
     ap.add_argument("--config", default="q4k64", choices=sorted(CONFIGS))
     ap.add_argument("--clips", type=int, default=0, help="override clips per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-reps", type=int, default=4)   # ~13 s of reference CPU work on 16 threads
+    ap.add_argument("--cpu-reps", type=int, default=2)   # ~7 s of reference CPU work on 16 threads (+ legs)
     ap.add_argument("--workdir", default=os.environ.get("Q2A_BENCH_DIR", os.path.join(tempfile.gettempdir(), "q2a_bench")))
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     ws, rank, local = dist_env()
+    if ws != args.gpus:
+        log(f"bench: WORLD_SIZE={ws} but --gpus {args.gpus}: refusing to report a mislabelled run")
+        sys.exit(2)
     import torch
     # Q2A_BENCH_REHEARSE=1: rehearse the N>1 path on a 1-GPU box (every rank on device 0, gloo collectives on host
     # tensors); the numbers of such a run are not a scaling measurement
@@ -255,7 +332,7 @@ def main():
 
     cpu = None
     if ws == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(model_path, args.workdir, threads, args.cpu_reps)
+        cpu = cpu_baseline(model_path, wt, args.workdir, args.cpu_reps)
 
     res = {
         "metric": "encoder audio-frames/sec (30 s clips) at 1/2/4/8 MI355X; MFMA util %",

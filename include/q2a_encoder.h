@@ -134,6 +134,11 @@ int q2a_profile_read(q2a_engine * e, double * ms, int64_t * counts, int n, int r
 int q2a_test_linear(q2a_engine * e, int layer, int which, const float * x_dev, int M, float * y_dev, void * stream);
 /* One encoder block in place on X [n_clips*T][D] (f32, device). */
 int q2a_test_block(q2a_engine * e, int layer, float * x_dev, int n_clips, void * stream);
+/* Same, also copying the four GEMM A operands of the block as the MFMA consumed them into taps[0..3] (device,
+ * 2-byte elements, NULL entries skipped): LN1 -> QKV [M][D], attention -> O [M][D], LN2 -> fc1 [M][D], GELU -> fc2
+ * [M][F] (fp16 values for F16 files; Q8_K / Q8_0 integer codes held in fp16 for quantized files). Per-layer
+ * divergence trace against the reference's own intermediates (diag/layer_trace.py). */
+int q2a_test_block_taps(q2a_engine * e, int layer, float * x_dev, int n_clips, void * const * taps, void * stream);
 /* Attention only: q,k,v [n_clips*T][D] f32 (q already scaled), out [n_clips*T][D] f32. */
 int q2a_test_attention(q2a_engine * e, const float * q_dev, const float * k_dev, const float * v_dev, int n_clips,
                        float * out_dev, void * stream);

@@ -81,19 +81,32 @@ whisper_context * open_ctx(const char * model) {
 
 // Dump every node output of the encoder graph whose layer index is 0 (first n_dump nodes), through the
 // sched eval callback (ggml-backend.cpp:2306), which the reference itself uses for debugging (:2305).
+// ndump < 0 selects the per-layer mode: every layer's block input (node 3 + 33 l), its LN1 output (+3), the merged
+// attention output (+21), the post-attention residual (+24), the LN2 output (+27), the GELU output (+30), and the
+// encoder's last block output — the tensors ggml re-quantizes before the next weight GEMM, for the cross-build /
+// per-layer divergence trace (tests/golden/make_crossbuild.py). 33 nodes per layer: the graph of
+// whisper_build_graph_encoder (qwen2-whisper.cpp:1999-2154) as ggml orders it.
 struct dump_state {
     std::string dir;
     int idx = 0;
     int limit = 0;
+    bool layers = false;
     FILE * index = nullptr;
 };
+
+bool dump_wanted(const dump_state * ds, int idx) {
+    if (!ds->layers) return idx < ds->limit;
+    if (idx < 3) return false;
+    const int r = (idx - 3) % 33;
+    return r == 0 || r == 3 || r == 21 || r == 24 || r == 27 || r == 30;
+}
 
 bool dump_cb(struct ggml_tensor * t, bool ask, void * ud) {
     dump_state * ds = (dump_state *) ud;
     if (ask) {
-        return ds->idx < ds->limit;
+        return ds->layers || ds->idx < ds->limit;
     }
-    if (ds->idx >= ds->limit) return true;
+    if (!dump_wanted(ds, ds->idx)) { ds->idx++; return true; }
     if (t->type == GGML_TYPE_F32 && ggml_is_contiguous(t)) {
         std::vector<float> buf(ggml_nelements(t));
         ggml_backend_tensor_get(t, buf.data(), 0, ggml_nbytes(t));
@@ -133,6 +146,7 @@ int cmd_encode(int argc, char ** argv) {
     if (argc > 7) {
         ds.dir = argv[7];
         ds.limit = argc > 8 ? atoi(argv[8]) : 48;
+        ds.layers = ds.limit < 0;
         ds.index = fopen((ds.dir + "/index.txt").c_str(), "w");
         ggml_backend_sched_set_eval_callback(ctx->state->sched_encode.sched, dump_cb, &ds);
     }

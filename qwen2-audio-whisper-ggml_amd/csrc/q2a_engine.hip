@@ -543,6 +543,9 @@ struct q2a_engine {
     int fuse_q8k = [] { const char * v = getenv("Q2A_FUSE_Q8K"); return v ? atoi(v) : -1; }();
     // Q4_K fc1: GELU in the GEMM epilogue (1) or deferred to the Q8_K quantizer (0, default; A/B: Q2A_GELU_IN_EPI=1)
     int gelu_in_epi = [] { const char * v = getenv("Q2A_GELU_IN_EPI"); return v ? atoi(v) : 0; }();
+    // q2a_test_block_taps: device buffers receiving the GEMM A operands of one block (LN1 -> QKV, attention -> O,
+    // LN2 -> fc1, GELU -> fc2) as they were fed to the MFMA, for the per-layer divergence trace (NULL: off)
+    void * taps[4] = {nullptr, nullptr, nullptr, nullptr};
 
     // optional per-kernel-class timing with HIP events on the launch stream (q2a_profile_*)
     bool prof = false;
@@ -731,8 +734,13 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
     const dims & d = e->d;
     const int M = B * d.T;
     const int mode = ln_mode(e);
+    auto tap = [&](int i, const q2a_half * src, int K) -> hipError_t {
+        if (!e->taps[i]) return hipSuccess;
+        return hipMemcpyAsync(e->taps[i], src, (size_t) M * K * e->kx * 2, hipMemcpyDeviceToDevice, s);
+    };
     q2a_ln_args ln{e->X, M, d.D, e->lv<const float *>(l, L_LN1W), e->lv<const float *>(l, L_LN1B), mode, e->actD, e->dyD, e->aextD, e->dy_ld};
     PLAUNCH(e, s, Q2A_PROF_LN, q2a_launch_layernorm(ln, s));
+    LAUNCH(tap(0, e->actD, d.D));
     {
         q2a_gemm_args a = gemm_base(e, l, 0, e->actD, M);
         a.bias = e->lv<const float *>(l, L_BQKV);
@@ -752,6 +760,7 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
             PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_quant_act(qa, s));
         }
     }
+    LAUNCH(tap(1, e->actD, d.D));
     {
         q2a_gemm_args a = gemm_base(e, l, 1, e->actD, M);
         a.bias = e->lv<const float *>(l, L_BO);
@@ -761,6 +770,7 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
     }
     q2a_ln_args ln2{e->X, M, d.D, e->lv<const float *>(l, L_LN2W), e->lv<const float *>(l, L_LN2B), mode, e->actD, e->dyD, e->aextD, e->dy_ld};
     PLAUNCH(e, s, Q2A_PROF_LN, q2a_launch_layernorm(ln2, s));
+    LAUNCH(tap(2, e->actD, d.D));
     {
         q2a_gemm_args a = gemm_base(e, l, 2, e->actD, M);
         a.bias = e->lv<const float *>(l, L_B1);
@@ -792,6 +802,7 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
             PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_quant_act(qa, s));
         }
     }
+    LAUNCH(tap(3, e->actF, d.F));
     {
         q2a_gemm_args a = gemm_base(e, l, 3, e->actF, M);
         a.bias = e->lv<const float *>(l, L_B2);
@@ -1188,6 +1199,14 @@ int q2a_test_block(q2a_engine * e, int layer, float * x, int n_clips, void * str
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(x, e->X, bytes, hipMemcpyDeviceToDevice, s));
     return Q2A_OK;
+}
+
+int q2a_test_block_taps(q2a_engine * e, int layer, float * x, int n_clips, void * const * taps, void * stream) {
+    if (!e || !taps) return Q2A_ERR_ARG;
+    for (int i = 0; i < 4; ++i) e->taps[i] = taps[i];
+    const int rc = q2a_test_block(e, layer, x, n_clips, stream);
+    for (int i = 0; i < 4; ++i) e->taps[i] = nullptr;
+    return rc;
 }
 
 int q2a_test_attention(q2a_engine * e, const float * q, const float * k, const float * v, int n_clips, float * out,

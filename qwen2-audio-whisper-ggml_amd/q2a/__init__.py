@@ -18,7 +18,7 @@ TOOL_PATH = os.path.join(PKG_DIR, "bin", "q2a_tool")
 EXPORTS = (
     "q2a_last_error", "q2a_open", "q2a_pack_model", "q2a_free_host_blob", "q2a_open_device_blob", "q2a_close",
     "q2a_get_info", "q2a_reserve", "q2a_encode_device", "q2a_encode_host", "q2a_pcm_to_mel",
-    "q2a_test_linear", "q2a_test_block", "q2a_test_attention",
+    "q2a_test_linear", "q2a_test_block", "q2a_test_block_taps", "q2a_test_attention",
 )
 
 CLIP_ENCODED, CLIP_SKIPPED = 0, 1
@@ -71,6 +71,7 @@ def lib() -> C.CDLL:
         L.q2a_pcm_to_mel.argtypes = [vp, vp, C.c_int, vp, C.c_int64, i32p]
         L.q2a_test_linear.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int, vp, vp]
         L.q2a_test_block.argtypes = [vp, C.c_int, vp, C.c_int, vp]
+        L.q2a_test_block_taps.argtypes = [vp, C.c_int, vp, C.c_int, C.POINTER(vp), vp]
         L.q2a_test_attention.argtypes = [vp, vp, vp, vp, C.c_int, vp, vp]
         _lib = L
     return _lib
@@ -155,6 +156,11 @@ class Engine:
 
     def test_block(self, layer, x_ptr, n_clips, stream=None):
         _check(lib().q2a_test_block(self.h, layer, C.c_void_p(x_ptr), n_clips, C.c_void_p(stream) if stream else None))
+
+    def test_block_taps(self, layer, x_ptr, n_clips, tap_ptrs, stream=None):
+        arr = (C.c_void_p * 4)(*[C.c_void_p(t) if t else None for t in tap_ptrs])
+        _check(lib().q2a_test_block_taps(self.h, layer, C.c_void_p(x_ptr), n_clips, arr,
+                                         C.c_void_p(stream) if stream else None))
 
     def test_attention(self, q_ptr, k_ptr, v_ptr, n_clips, out_ptr, stream=None):
         _check(lib().q2a_test_attention(self.h, C.c_void_p(q_ptr), C.c_void_p(k_ptr), C.c_void_p(v_ptr), n_clips,

@@ -1,0 +1,168 @@
+"""Measure the reference's OWN cross-build disagreement on the full-size encoder (evidence for the parity bar).
+
+The reference CPU path (ggml) picks different SIMD kernels per x86 ISA level: scalar dot products at -march=x86-64,
+AVX2 at x86-64-v3 (the build oracle/_ref/ref_harness uses for every golden fixture), AVX-512 at x86-64-v4. Integer
+work is identical across them; only fp32 summation order (vector lanes, FMA) differs. This script runs the same
+full-size (L=32, D=1280) model bytes and the same clip through each build and records
+
+  * end-to-end max-rel / rel-L2 between every pair of builds (F16, Q4_K, Q8_0 model files);
+  * per layer l, between the AVX2 build and each other build: rel-L2 of the block output, and the number of
+    activation codes that differ at the four points where ggml re-quantizes before a weight GEMM (LN1 -> QKV,
+    attention -> O, LN2 -> fc1, GELU -> fc2): Q8_K codes for Q4_K files, Q8_0 codes for Q8_0, fp16 values for F16.
+
+Runs only in the build container (needs /root/reference compiled by `make -C oracle ref ref-isa`). Writes
+tests/golden/crossbuild.json (small, committed). Inputs come from bin/q2a_tool (same generator / quantizer / clip
+bytes as every other fixture; SHA-256 checked against golden.json).
+
+usage: python tests/golden/make_crossbuild.py [--workdir DIR] [--types q4_k,q8_0,f16] [--builds x86-64,avx512]
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import hashlib
+import json
+import os
+import shutil
+import subprocess
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+TOOL = os.path.join(ROOT, "qwen2-audio-whisper-ggml_amd", "bin", "q2a_tool")
+BUILDS = {"avx2": "_ref", "x86-64": "_ref_x86-64", "avx512": "_ref_avx512"}
+T, D, F, L = 1500, 1280, 5120, 32
+POINTS = {"ln1": 3, "attn": 21, "ln2": 27, "gelu": 30}   # node offsets within a layer (oracle/ref_harness.cpp)
+
+
+def sha(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 22), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+# ---- activation conversions, restated from ggml (numpy; used only to COUNT differing codes between two builds)
+def q8k_codes(x):
+    """quantize_row_q8_K_ref (ggml-quants.c:3785-3822): per 256, iscale = -127/max (max = signed value of the first
+    largest |x|), q = min(127, nearest_int(iscale * x)) with nearest_int = round-half-even (:1639-1644)."""
+    b = x.reshape(-1, 256).astype(np.float32)
+    i = np.abs(b).argmax(axis=1)
+    mx = b[np.arange(b.shape[0]), i]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        isc = np.where(mx != 0, np.float32(-127.0) / mx, np.float32(0)).astype(np.float32)
+    q = np.rint((isc[:, None] * b).astype(np.float32))
+    return np.minimum(q, 127).astype(np.int16)
+
+
+def q80_codes(x):
+    """quantize_row_q8_0, x86 AVX2 branch (ggml-quants.c:873-960): per 32, id = 127/amax, q = round-nearest(x*id)."""
+    b = x.reshape(-1, 32).astype(np.float32)
+    am = np.abs(b).max(axis=1)
+    with np.errstate(divide="ignore"):
+        idv = np.where(am != 0, np.float32(127.0) / am, np.float32(0)).astype(np.float32)
+    return np.rint((idv[:, None] * b).astype(np.float32)).astype(np.int16)
+
+
+def f16_codes(x):
+    return x.astype(np.float16).view(np.int16)
+
+
+CODES = {"q4_k": q8k_codes, "q8_0": q80_codes, "f16": f16_codes}
+
+
+def relerr(a, b):
+    d = a.astype(np.float64) - b.astype(np.float64)
+    return float(np.abs(d).max() / np.abs(b).max()), float(np.linalg.norm(d) / np.linalg.norm(b))
+
+
+def run_ref(build, model, clip, out, dump, nthreads):
+    exe = os.path.join(ROOT, "oracle", BUILDS[build], "ref_harness")
+    if os.path.exists(dump):
+        shutil.rmtree(dump)
+    os.makedirs(dump)
+    t0 = time.time()
+    res = subprocess.run([exe, "encode", model, clip, out, str(nthreads), "1", dump, "-1"], check=True,
+                         capture_output=True, text=True).stdout
+    info = json.loads(res.strip().splitlines()[-1])
+    info["wall_s"] = time.time() - t0
+    return np.fromfile(out, dtype=np.float32), info
+
+
+def node(dump, idx):
+    f = glob.glob(os.path.join(dump, f"node{idx:03d}_*.f32"))
+    assert len(f) == 1, (dump, idx)
+    return np.fromfile(f[0], dtype=np.float32)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--workdir", default="/tmp/q2a_crossbuild")
+    ap.add_argument("--types", default="q4_k,q8_0,f16")
+    ap.add_argument("--builds", default="x86-64,avx512")
+    ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
+    args = ap.parse_args()
+    os.makedirs(args.workdir, exist_ok=True)
+    with open(os.path.join(HERE, "golden.json")) as f:
+        gmeta = json.load(f)
+    outp = os.path.join(HERE, "crossbuild.json")
+    result = json.load(open(outp)) if os.path.exists(outp) else {}
+    result["about"] = ("reference CPU path (oracle/_ref* builds of /root/reference) vs itself across x86 ISA levels; "
+                       "full-size synthetic model (seed 0x51A2), clip 0 (30 s); tests/golden/make_crossbuild.py")
+    clip = os.path.join(args.workdir, "clip0.f32")
+    if not os.path.exists(clip):
+        subprocess.check_call([TOOL, "synth-clip", clip, "480000", "0"])
+    assert sha(clip) == gmeta["clips"]["0"]["sha256"]
+    base = os.path.join(args.workdir, "full-f16.bin")
+    if not os.path.exists(base):
+        subprocess.check_call([TOOL, "gen-model", base, "full", "f16", "0x51A2", str(args.threads)])
+    for wt in args.types.split(","):
+        model = base if wt == "f16" else os.path.join(args.workdir, f"full-{wt}.bin")
+        if not os.path.exists(model):
+            subprocess.check_call([TOOL, "quantize", base, model, wt, str(args.threads)])
+        assert sha(model) == gmeta["models"][f"full-{wt}"]["sha256"], wt
+        dref = os.path.join(args.workdir, f"dump-{wt}-avx2")
+        yref, iref = run_ref("avx2", model, clip, os.path.join(args.workdir, f"{wt}-avx2.out"), dref, args.threads)
+        g = gmeta["outputs"][f"full_{wt}_c0"]
+        ent = {"avx2_matches_golden_l2": abs(float(np.linalg.norm(yref.astype(np.float64))) - g["l2"]) < 1e-3 * g["l2"],
+               "seconds": {"avx2": iref["wall_s"]}, "pairs": {}, "layers": {}}
+        finals = {"avx2": yref}
+        for b in args.builds.split(","):
+            dother = os.path.join(args.workdir, f"dump-{wt}-{b}")
+            y, info = run_ref(b, model, clip, os.path.join(args.workdir, f"{wt}-{b}.out"), dother, args.threads)
+            finals[b] = y
+            ent["seconds"][b] = info["wall_s"]
+            codes = CODES[wt]
+            rows = []
+            for l in range(L):
+                b0 = 3 + 33 * l
+                out_idx = b0 + 33 if l + 1 < L else None
+                r = {"layer": l}
+                if out_idx is not None:
+                    r["out_max_rel"], r["out_rel_l2"] = relerr(node(dother, out_idx), node(dref, out_idx))
+                for nm, off in POINTS.items():
+                    ca, cb = codes(node(dother, b0 + off)), codes(node(dref, b0 + off))
+                    r[f"flips_{nm}"] = int((ca != cb).sum())
+                r["in_rel_l2"] = relerr(node(dother, b0), node(dref, b0))[1]
+                rows.append(r)
+                print(wt, b, r, flush=True)
+            ent["layers"][b] = rows
+            shutil.rmtree(dother)
+        shutil.rmtree(dref)
+        names = list(finals)
+        for i, a in enumerate(names):
+            for c in names[i + 1:]:
+                mx, l2 = relerr(finals[c], finals[a])
+                ent["pairs"][f"{a}_vs_{c}"] = {"max_rel": mx, "rel_l2": l2}
+        result[wt] = ent
+        print(wt, json.dumps(ent["pairs"]), flush=True)
+        with open(outp, "w") as f:
+            json.dump(result, f, indent=1, sort_keys=True)
+    print("wrote", outp)
+
+
+if __name__ == "__main__":
+    main()
