@@ -49,6 +49,9 @@ typedef struct {
     int n_fused;
     int n_mm_grouped;   /* launches that ran two weight MUL_MATs of the same activation together */
     int n_mul_mat_conv; /* MUL_MAT(F32 im2col, F16 kernel) on the fp16 MFMA GEMM with hi/lo-split activations */
+    int n_buffer_reallocs; /* backend lifetime: scratch / V^T / fp16-shadow reallocations (each drops every captured
+                              HIP graph, whose launches hold those buffers' addresses) */
+    int n_mul_mat_conv_total; /* backend lifetime: n_mul_mat_conv summed over every graph_compute that ran its nodes */
 } ggml_backend_q2a_stats;
 GGML_API void ggml_backend_q2a_get_stats(ggml_backend_t backend, ggml_backend_q2a_stats * stats);
 

@@ -10,6 +10,7 @@
 // runs on the backend as built.
 //
 //   ggml_harness encode MODEL PCM OUT [reps] [device]   -> embd_enc f32 [750][1280] to OUT, JSON line on stdout
+//   ggml_harness graphs [device]                        -> HIP-graph capture vs scratch growth check, JSON line
 
 #define GGML_USE_CUDA
 #define ggml_backend_cuda_init ggml_backend_q2a_init
@@ -82,13 +83,74 @@ int cmd_encode(int argc, char ** argv) {
     fclose(f);
     printf("{\"ne0\": %lld, \"ne1\": %lld, \"reps\": %d, \"best_s\": %.6f, \"mean_s\": %.6f, \"backend\": \"%s\", "
            "\"embd_buffer\": \"%s\", \"n_splits_encode\": %d, \"nodes\": %d, \"mul_mat_fast\": %d, \"mul_mat_f32\": %d, "
-           "\"attn_fused\": %d, \"other\": %d, \"graph_replayed\": %d, \"fused\": %d, \"mm_grouped\": %d, \"mm_conv\": %d, \"best_mel_s\": %.6f, \"best_encode_s\": %.6f}\n",
+           "\"attn_fused\": %d, \"other\": %d, \"graph_replayed\": %d, \"fused\": %d, \"mm_grouped\": %d, \"mm_conv\": %d, \"mm_conv_total\": %d, \"best_mel_s\": %.6f, \"best_encode_s\": %.6f}\n",
            (long long) e->ne[0], (long long) e->ne[1], reps, best, total / reps, ggml_backend_name(be),
            ggml_backend_buffer_name(e->buffer), ggml_backend_sched_get_n_splits(ctx->state->sched_encode.sched),
-           st.n_nodes, st.n_mul_mat_fast, st.n_mul_mat_f32, st.n_attn_fused, st.n_other, st.n_graph_replayed, st.n_fused, st.n_mm_grouped, st.n_mul_mat_conv, best_mel,
+           st.n_nodes, st.n_mul_mat_fast, st.n_mul_mat_f32, st.n_attn_fused, st.n_other, st.n_graph_replayed, st.n_fused, st.n_mm_grouped, st.n_mul_mat_conv, st.n_mul_mat_conv_total, best_mel,
            best_enc);
     whisper_free(ctx);
     return 0;
+}
+
+// A captured graph must never replay against a reallocated scratch: capture a small MUL_MAT graph (third compute =
+// replay), grow the scratch with a larger graph on the same backend, then compute the small graph again — it must be
+// re-run (not replayed from the stale capture) and give the same bytes.
+int cmd_graphs(int argc, char ** argv) {
+    const int device = argc > 2 ? atoi(argv[2]) : 0;
+    ggml_backend_t be = ggml_backend_q2a_init(device);
+    if (!be) { fprintf(stderr, "no Q2A backend\n"); return 3; }
+    const int K = 256, N = 256;
+    ggml_init_params ip = { 8 * ggml_tensor_overhead(), nullptr, true };
+    ggml_context * cw = ggml_init(ip);
+    ggml_tensor * w = ggml_new_tensor_2d(cw, GGML_TYPE_F16, K, N);
+    ggml_backend_buffer_t bw = ggml_backend_alloc_ctx_tensors(cw, be);
+    ggml_backend_buffer_set_usage(bw, GGML_BACKEND_BUFFER_USAGE_WEIGHTS);
+    std::vector<ggml_fp16_t> wh((size_t) K * N);
+    uint32_t st = 12345;
+    auto rnd = [&]() { st = st * 1664525u + 1013904223u; return (float) ((st >> 8) & 0xFFFF) / 65536.0f - 0.5f; };
+    for (auto & v : wh) v = ggml_fp32_to_fp16(rnd());
+    ggml_backend_tensor_set(w, wh.data(), 0, wh.size() * 2);
+    struct G { ggml_context * c; ggml_cgraph * g; ggml_tensor * x, * y; ggml_backend_buffer_t buf; };
+    auto make = [&](int M) {
+        ggml_init_params gp = { 16 * ggml_tensor_overhead() + ggml_graph_overhead(), nullptr, true };
+        G r;
+        r.c = ggml_init(gp);
+        r.x = ggml_new_tensor_2d(r.c, GGML_TYPE_F32, K, M);
+        r.y = ggml_mul_mat(r.c, w, r.x);
+        r.g = ggml_new_graph(r.c);
+        ggml_build_forward_expand(r.g, r.y);
+        r.buf = ggml_backend_alloc_ctx_tensors(r.c, be);
+        std::vector<float> xh((size_t) K * M);
+        for (auto & v : xh) v = rnd();
+        ggml_backend_tensor_set(r.x, xh.data(), 0, xh.size() * 4);
+        return r;
+    };
+    auto run = [&](G & g, std::vector<float> * out) {
+        if (ggml_backend_graph_compute(be, g.g) != GGML_STATUS_SUCCESS) { fprintf(stderr, "compute failed\n"); exit(5); }
+        ggml_backend_q2a_stats s;
+        memset(&s, 0, sizeof(s));
+        ggml_backend_q2a_get_stats(be, &s);
+        if (out) { out->resize((size_t) ggml_nelements(g.y)); ggml_backend_tensor_get(g.y, out->data(), 0, ggml_nbytes(g.y)); }
+        return s;
+    };
+    G small = make(64), big = make(8192);
+    std::vector<float> y0, y1, y2;
+    run(small, &y0);
+    run(small, nullptr);
+    const ggml_backend_q2a_stats s3 = run(small, &y1);   // third sighting: replayed from the capture
+    const ggml_backend_q2a_stats sb = run(big, nullptr);  // grows the scratch (drops the captures)
+    const ggml_backend_q2a_stats s4 = run(small, &y2);    // must NOT replay the stale capture
+    const ggml_backend_q2a_stats s5 = run(small, nullptr);
+    const ggml_backend_q2a_stats s6 = run(small, &y2);    // captured again against the new scratch, replayed
+    const bool eq = y0 == y1 && y1 == y2;
+    printf("{\"replayed_third\": %d, \"reallocs_before_big\": %d, \"reallocs_after_big\": %d, \"replayed_after_grow\": %d, "
+           "\"recaptured\": %d, \"replayed_again\": %d, \"equal\": %s}\n", s3.n_graph_replayed, s3.n_buffer_reallocs,
+           sb.n_buffer_reallocs, s4.n_graph_replayed, s5.n_graph_replayed, s6.n_graph_replayed, eq ? "true" : "false");
+    for (G * g : {&small, &big}) { ggml_backend_buffer_free(g->buf); ggml_free(g->c); }
+    ggml_backend_buffer_free(bw);
+    ggml_free(cw);
+    ggml_backend_free(be);
+    return eq ? 0 : 6;
 }
 
 }  // namespace
@@ -97,6 +159,7 @@ int main(int argc, char ** argv) {
     if (argc < 2) { fprintf(stderr, "usage: ggml_harness encode ...\n"); return 1; }
     whisper_log_set([](ggml_log_level lvl, const char * text, void *) { if (lvl == GGML_LOG_LEVEL_ERROR) fputs(text, stderr); }, nullptr);
     if (std::string(argv[1]) == "encode") return cmd_encode(argc, argv);
+    if (std::string(argv[1]) == "graphs") return cmd_graphs(argc, argv);
     fprintf(stderr, "unknown command %s\n", argv[1]);
     return 1;
 }

@@ -584,6 +584,8 @@ struct q2a_backend_ctx {
     struct captured { uint64_t sig; int seen; hipGraphExec_t exec; ggml_backend_q2a_stats stats; uint64_t used; };
     std::vector<captured> graphs;
     uint64_t graph_clock = 0;
+    int n_buffer_reallocs = 0;         // scratch / V^T / shadow reallocations (each drops the captured graphs)
+    int n_mul_mat_conv_total = 0;      // conv MUL_MATs run on the hi/lo path over the backend's lifetime
 };
 
 q2a_reg_ctx * reg_ctx();
@@ -723,6 +725,18 @@ tview tv(const ggml_tensor * t) {
 
 dim3 grid1(int64_t n) { return dim3((unsigned) ((n + 255) / 256)); }
 
+// Captured HIP graphs bake in the addresses of the scratch, V^T and fp16-shadow buffers: whenever one of them is
+// reallocated, every captured exec is destroyed (its cgraph is re-captured on its next sightings against the new
+// buffers), so no replay can touch freed memory.
+void drop_graphs(q2a_backend_ctx * b) {
+    for (auto & e : b->graphs) {
+        if (e.exec) (void) hipGraphExecDestroy(e.exec);
+        e.exec = nullptr;
+        e.seen = 1;
+    }
+    ++b->n_buffer_reallocs;
+}
+
 void * scratch(q2a_backend_ctx * b, size_t bytes) {
     if (bytes > b->scratch_bytes) {
         b->quant_src = nullptr;
@@ -731,6 +745,7 @@ void * scratch(q2a_backend_ctx * b, size_t bytes) {
         b->scratch = nullptr;
         Q2A_HIP(hipMalloc(&b->scratch, bytes));
         b->scratch_bytes = bytes;
+        drop_graphs(b);
     }
     return b->scratch;
 }
@@ -750,12 +765,13 @@ bool mm_fast_ok(const ggml_tensor * op) {
     return N % 128 == 0 && K % 256 == 0 && K <= 8192 && N <= (1 << 30);
 }
 
-const packed_w * get_packed(q2a_backend_ctx * b, const ggml_tensor * w) {
+// (returned by value: the cache vector may grow or swap-remove entries under another backend's lock)
+packed_w get_packed(q2a_backend_ctx * b, const ggml_tensor * w) {
     q2a_device_ctx * d = dev_ctx(b->device);
     {
         std::lock_guard<std::mutex> lk(d->mu);
         for (const packed_w & p : d->wcache)
-            if (p.raw == (const char *) w->data && p.type == w->type && p.N == w->ne[1] && p.K == w->ne[0]) return &p;
+            if (p.raw == (const char *) w->data && p.type == w->type && p.N == w->ne[1] && p.K == w->ne[0]) return p;
     }
     // first use: repack on the host from the device bytes (one-time, per weight tensor)
     const size_t nb = ggml_nbytes(w);
@@ -770,7 +786,7 @@ const packed_w * get_packed(q2a_backend_ctx * b, const ggml_tensor * w) {
     Q2A_HIP(hipMemcpy(p.dev, out.data(), out.size(), hipMemcpyHostToDevice));
     std::lock_guard<std::mutex> lk(d->mu);
     d->wcache.push_back(p);
-    return &d->wcache.back();
+    return p;
 }
 
 struct mm_chain {          // a fast MUL_MAT and the nodes its epilogue absorbs
@@ -857,31 +873,38 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
     if (blk == 0) {
         a.W = (const q2a_half *) w->data;
     } else {
-        const packed_w * p = get_packed(b, w);
-        const char * base = (const char *) p->dev;
-        a.W = (const q2a_half *) (base + p->off[0]);
+        const packed_w p = get_packed(b, w);
+        const char * base = (const char *) p.dev;
+        a.W = (const q2a_half *) (base + p.off[0]);
         a.nblk = K / blk;
-        a.dx = (const float *) (base + p->off[1]);
+        a.dx = (const float *) (base + p.off[1]);
         a.dy = dy; a.dy_ld = MP;
         if (blk == 256) {
-            a.dmin = (const float *) (base + p->off[2]);
-            a.wext = (const q2a_half *) (base + p->off[3]);
-            a.beta = (const float *) (base + p->off[4]);
-            a.gamma = (const float *) (base + p->off[5]);
+            a.dmin = (const float *) (base + p.off[2]);
+            a.wext = (const q2a_half *) (base + p.off[3]);
+            a.beta = (const float *) (base + p.off[4]);
+            a.gamma = (const float *) (base + p.off[5]);
             a.aext = aext;
         }
     }
     Q2A_HIP(q2a_launch_gemm(a, epi, blk, b->stream));
 }
 
-// the conv kernel duplicated into [N][2K] (w | w), cached like the repacked weights (dropped when its bytes change)
-const packed_w * get_dup16(q2a_backend_ctx * b, const ggml_tensor * w, int N, int K) {
+// the conv kernel duplicated into [N][2K] (w | w), cached like the repacked weights (dropped when its bytes change);
+// only for tensors in a WEIGHTS buffer (the model's, qwen2-whisper.cpp:1867): any other F16 tensor may be rewritten
+// by a kernel at the same address, so run_mm_conv_hilo duplicates it into the scratch on every call instead
+bool is_weight_buffer(const ggml_tensor * w) {
+    const ggml_tensor * t = w->view_src ? w->view_src : w;
+    return t->buffer && ggml_backend_buffer_get_usage(t->buffer) == GGML_BACKEND_BUFFER_USAGE_WEIGHTS;
+}
+
+packed_w get_dup16(q2a_backend_ctx * b, const ggml_tensor * w, int N, int K) {
     constexpr int DUP16 = -16;   // cache tag (not a ggml type)
     q2a_device_ctx * d = dev_ctx(b->device);
     {
         std::lock_guard<std::mutex> lk(d->mu);
         for (const packed_w & p : d->wcache)
-            if (p.raw == (const char *) w->data && p.type == DUP16 && p.N == N && p.K == K) return &p;
+            if (p.raw == (const char *) w->data && p.type == DUP16 && p.N == N && p.K == K) return p;
     }
     packed_w p{};
     p.raw = (const char *) w->data; p.raw_bytes = ggml_nbytes(w); p.type = DUP16; p.N = N; p.K = K;
@@ -892,9 +915,15 @@ const packed_w * get_dup16(q2a_backend_ctx * b, const ggml_tensor * w, int N, in
     Q2A_HIP(hipStreamSynchronize(b->stream));
     std::lock_guard<std::mutex> lk(d->mu);
     d->wcache.push_back(p);
-    return &d->wcache.back();
+    return p;
 }
 
+// The hi/lo split writes each f32 activation x as fp16 hi = fp16(x) plus fp16 lo = fp16(x - hi) (22 significant
+// bits). It assumes |x| < 65504 and |x| above the fp16 normal range (6.1e-5) for the full precision: the conv inputs
+// are the normalised log-mel ((x + 4) / 4 after the clamp: [-0.75, 1.5], qwen2-whisper.cpp:2633-2649) and conv1's
+// GELU output (|x| of order 1-10 for trained and synthetic weights); smaller values lose relative precision in lo only
+// (absolute error < 2^-25, far below the f32 rounding of the 384/3840-term dot products). Outside that range
+// (GGML_Q2A_NO_CONV_HILO=1) the exact-f32 MFMA GEMM (run_mm_f32) computes the node.
 bool conv_hilo_ok(const ggml_tensor * op) {
     static const bool off = [] { const char * v = getenv("GGML_Q2A_NO_CONV_HILO"); return v && atoi(v); }();
     const ggml_tensor * x = op->src[0];
@@ -912,13 +941,21 @@ void run_mm_conv_hilo(q2a_backend_ctx * b, ggml_tensor * op) {
     const ggml_tensor * x = op->src[0];
     const ggml_tensor * w = op->src[1];
     const int K = (int) x->ne[0], M = (int) x->ne[1], N = (int) w->ne[1];
-    const packed_w * wd = get_dup16(b, w, N, K);
+    const bool cached = is_weight_buffer(w);
+    const packed_w wd = cached ? get_dup16(b, w, N, K) : packed_w{};
     const int S = q2a_gemm_resid_ksplit(M, N, 2 * K, 0);
     const size_t a_bytes = ((size_t) M * 2 * K * 2 + 255) & ~size_t(255);
     const size_t t_bytes = ((size_t) M * N * 4 + 255) & ~size_t(255);
-    const size_t p_bytes = S > 1 ? (size_t) S * M * N * 4 : 0;
-    char * s = (char *) scratch(b, a_bytes + t_bytes + p_bytes);
+    const size_t p_bytes = S > 1 ? ((size_t) S * M * N * 4 + 255) & ~size_t(255) : 0;
+    const size_t d_bytes = cached ? 0 : (size_t) N * 2 * K * 2;
+    char * s = (char *) scratch(b, a_bytes + t_bytes + p_bytes + d_bytes);
     b->quant_src = nullptr;
+    const _Float16 * wdup = (const _Float16 *) wd.dev;
+    if (!cached) {   // not a model weight: duplicate this call's bytes into the scratch
+        _Float16 * dst = (_Float16 *) (s + a_bytes + t_bytes + p_bytes);
+        hipLaunchKernelGGL(k_dup_rows, grid1((int64_t) N * K), dim3(256), 0, b->stream, (const _Float16 *) w->data, dst, K, N * K);
+        wdup = dst;
+    }
     _Float16 * A = (_Float16 *) s;
     float * tmp = (float *) (s + a_bytes);
     const int n = M * K;
@@ -927,7 +964,7 @@ void run_mm_conv_hilo(q2a_backend_ctx * b, ggml_tensor * op) {
     memset(&a, 0, sizeof(a));
     a.A = (const q2a_half *) A; a.lda = 2 * K; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
     a.M = M; a.N = N; a.K = 2 * K; a.ldw = 2 * K;
-    a.W = (const q2a_half *) wd->dev;
+    a.W = (const q2a_half *) wdup;
     a.outF = tmp; a.ldo = N;
     a.gelu_tab = gelu_table(b->device);
     if (S > 1) {
@@ -999,6 +1036,7 @@ _Float16 * vt_buffer(q2a_backend_ctx * b, size_t bytes) {
         b->vt_buf = nullptr;
         Q2A_HIP(hipMalloc((void **) &b->vt_buf, bytes));
         b->vt_bytes = bytes;
+        drop_graphs(b);
     }
     return b->vt_buf;
 }
@@ -1013,6 +1051,7 @@ _Float16 * claim_a16(q2a_backend_ctx * b, const ggml_tensor * t) {
         b->a16[k] = nullptr;
         Q2A_HIP(hipMalloc((void **) &b->a16[k], bytes));
         b->a16_bytes[k] = bytes;
+        drop_graphs(b);
     }
     b->a16_last = k;
     b->a16_src[k] = t;
@@ -1255,7 +1294,12 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                     i += used - 1;
                     break;
                 }
-                if (!mm_fast_ok(op) && conv_hilo_ok(op)) { run_mm_conv_hilo(b, op); b->stats.n_mul_mat_conv++; break; }
+                if (!mm_fast_ok(op) && conv_hilo_ok(op)) {
+                    run_mm_conv_hilo(b, op);
+                    b->stats.n_mul_mat_conv++;
+                    b->n_mul_mat_conv_total++;
+                    break;
+                }
                 if (!mm_fast_ok(op)) { run_mm_f32(b, op); b->stats.n_mul_mat_f32++; break; }
                 // MUL_MAT -> ADD(bias row) [-> GELU | -> ADD(residual) | -> [RESHAPE] -> SCALE] on the GEMM epilogue
                 // (qwen2-whisper.cpp:2029-2054, 2120-2154): same f32 operations, one kernel, no [N][M] round trips
@@ -1670,7 +1714,12 @@ ggml_backend_reg_t ggml_backend_q2a_reg(void) {
 }
 
 void ggml_backend_q2a_get_stats(ggml_backend_t backend, ggml_backend_q2a_stats * stats) {
-    if (ggml_backend_is_q2a(backend) && stats) *stats = ((q2a_backend_ctx *) backend->context)->stats;
+    if (ggml_backend_is_q2a(backend) && stats) {
+        const q2a_backend_ctx * b = (const q2a_backend_ctx *) backend->context;
+        *stats = b->stats;
+        stats->n_buffer_reallocs = b->n_buffer_reallocs;
+        stats->n_mul_mat_conv_total = b->n_mul_mat_conv_total;
+    }
 }
 
 }  // extern "C"

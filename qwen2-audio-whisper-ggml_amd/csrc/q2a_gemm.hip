@@ -98,6 +98,24 @@ __device__ __forceinline__ float gelu_lut_c(float x, const uint16_t * lut) {
     return (float) gh;
 }
 
+// Q4_K block-ratio accumulation (every Q4_K kernel, 8-phase and small-tile, runs exactly these float operations in
+// the same order, so a clip's outputs do not depend on the tile regime its batch size selects):
+//   block start  acc <- fma(acc, alpha[m] * beta[n], -(gamma[n] * S2[m][n]))
+//   block body   acc += the block's MFMAs (exact integer products, K order fixed by the 64-deep K-steps)
+//   after last   acc * (dy_last[m] * dx_last[n])
+__device__ __forceinline__ float kq_rescale(float a, float al, float be, float ga, float s2) {
+#pragma clang fp contract(off)
+    const float t = al * be;
+    const float u = ga * s2;
+    return __builtin_fmaf(a, t, -u);
+}
+__device__ __forceinline__ float kq_final(float a, float yc, float dx) {
+#pragma clang fp contract(off)
+    const float t = yc * dx;
+    return a * t;
+}
+__device__ __forceinline__ float kq_alpha(float yp, float yc) { return yp * __builtin_amdgcn_rcpf(yc); }
+
 __device__ __forceinline__ int64_t a_row_off(const q2a_gemm_args & p, int m) {
     return ((int64_t) (m / p.a_rpg) * p.a_gstride + (int64_t) (m % p.a_rpg) * p.a_step) * p.lda;
 }
@@ -233,7 +251,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
         asm volatile("ds_read_b32 %0, %1" : "=v"(yp) : "v"(sb0 + row * 4));
         asm volatile("ds_read_b32 %0, %1 offset:1024" : "=v"(yc) : "v"(sb0 + row * 4));
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(yp), "+v"(yc));
-        const float al = yp * __builtin_amdgcn_rcpf(yc);
+        const float al = kq_alpha(yp, yc);
         asm volatile("ds_write_b32 %0, %1" :: "v"(sb0 + ALPHA_OFF + row * 4), "v"(al) : "memory");
     };
     auto block_start = [&]() {
@@ -272,20 +290,9 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #pragma unroll
             for (int j = 0; j < 4; ++j) s2v[j] = __builtin_amdgcn_mfma_f32_16x16x16f16(we[j], ae[c], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const f4 s2 = s2v[j];
-                // packed fp32 (v_pk_mul/v_pk_fma): two columns per instruction
-                const f2 al2 = {al[c], al[c]};
+            for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int r = 0; r < 4; r += 2) {
-                    const f2 a2 = {acc[i][j][r], acc[i][j][r + 1]};
-                    const f2 bj = {bet[j][r], bet[j][r + 1]}, gj = {gam[j][r], gam[j][r + 1]};
-                    const f2 s22 = {s2[r], s2[r + 1]};
-                    const f2 res = a2 * (al2 * bj) - gj * s22;
-                    acc[i][j][r] = res[0];
-                    acc[i][j][r + 1] = res[1];
-                }
-            }
+                for (int r = 0; r < 4; ++r) acc[i][j][r] = kq_rescale(acc[i][j][r], al[c], bet[j][r], gam[j][r], s2v[j][r]);
             if (i + 1 < 8) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(al[n]), "+v"(ae[n]));
             __builtin_amdgcn_sched_barrier(0);   // one row block at a time: bounds the live min-term results
         }
@@ -405,7 +412,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             for (int i = 0; i < 8; ++i) {
                 const float yc = *(lds_fp) (uintptr_t) (sb0 + 1024 + (wm * 128 + i * 16 + (lane & 15)) * 4);
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc[i][j][r] *= yc * dx4[r];
+                for (int r = 0; r < 4; ++r) acc[i][j][r] = kq_final(acc[i][j][r], yc, dx4[r]);
             }
         }
     }
@@ -421,10 +428,11 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     constexpr int LA = BM / 8 / NW, LB = BN / 8 / NW;     // glds instructions per wave per stage
     static_assert(LA >= 1 && LB >= 1, "tile too small for the wave count");
     // k-quant block scales of the tile, staged through LDS (block-major global layout => contiguous per block):
-    //   BLK=256: dy[BM] f32 | aext[BM][16] f16 | dx[BN] f32 | dmin[BN] f32 | wext[BN][16] f16   (one buffer)
+    //   BLK=256: dy_{b-1}[BM] | dy_b[BM] f32 | aext[BM][16] f16 | beta[BN] | gamma[BN] | dx[BN] f32 | wext[BN][16] f16
+    //            (two buffers by block parity: block b+1's scales land while block b computes)
     //   BLK=32 : dy[2][BM] f32 | dx[2][BN] f32 for the two 32-blocks of a K-step            (two buffers)
-    constexpr int SB = BLK == 256 ? (BM * 4 + BM * 32 + BN * 8 + BN * 32) : BLK == 32 ? 2 * (BM * 4 + BN * 4) : 0;
-    constexpr int NSB = BLK == 32 ? 2 : 1;
+    constexpr int SB = BLK == 256 ? (BM * 8 + BM * 32 + BN * 12 + BN * 32) : BLK == 32 ? 2 * (BM * 4 + BN * 4) : 0;
+    constexpr int NSB = BLK ? 2 : 1;
     constexpr int NT = NW * 64;
     constexpr int SCH = (SB / 16 + NT - 1) / NT;          // 16-B scale chunks per thread
     constexpr int OPB = (BM + BN) * ROWB;                 // one operand stage (A image | W image)
@@ -434,12 +442,26 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                                       EPI == Q2A_EPI_GELU_Q8K);
     constexpr int EPI_OFF = LUT_EPI ? Q2A_GELU_C_BYTES : 0;
     constexpr int EPI_WREG = 2 * 32 * (BN / WN + 8) * 2;
-    constexpr int LDS_MAIN = PIPE ? (BLK ? SBUF_OFF + SBUF_BYTES : 2 * OPB) : 2 * OPB + (BLK ? NSB * SB : 0);
+    // small-tile kernels: NS operand stages (NS - 1 K-steps of loads in flight, counted vmcnt, raw barriers) within
+    // ~150 KiB of LDS. Q4_K: block b+1's scales arrive by glds in 1 KiB pieces (SBP per block, one per wave on the
+    // first SP K-steps of block b) into the other of two buffers, plus one pad piece per wave for the dummy pieces
+    // that keep every step's glds count uniform (so the vmcnt counts are compile-time); a piece issued at step s has
+    // landed by the end of step s + NS - 2, so SP + NS <= 6 puts it in place before block b+1 starts at step 4b + 4.
+    // The Q8_0 path drains its per-step register-staged scale loads every step and keeps 2 stages.
+    constexpr int SBP = BLK == 256 ? (SB + 1023) / 1024 : 0;          // 1 KiB pieces per Q4_K block
+    constexpr int SP = BLK == 256 ? (SBP + NW - 1) / NW : 0;          // K-steps per block that issue a piece
+    static_assert(BLK != 256 || SP <= 4, "Q4_K scale pieces must fit the block's 4 K-steps");
+    constexpr int SCALE_LDS = BLK == 256 ? (2 * SBP + NW) * 1024 : BLK ? NSB * SB : 0;
+    constexpr int NS_FIT = (150 * 1024 - SCALE_LDS) / OPB;
+    constexpr int NS_MAX = BLK == 256 ? 6 - SP : 5;
+    constexpr int NS = PIPE ? 2 : (BLK == 32 ? 2 : (NS_FIT >= NS_MAX ? NS_MAX : NS_FIT >= 2 ? NS_FIT : 2));
+    static_assert(PIPE || BLK != 256 || SP + NS <= 6, "Q4_K scale prefetch distance");
+    constexpr int LDS_MAIN = PIPE ? (BLK ? SBUF_OFF + SBUF_BYTES : 2 * OPB) : NS * OPB + SCALE_LDS;
     constexpr int LDS_BYTES = LDS_MAIN > EPI_OFF + NW * EPI_WREG ? LDS_MAIN : EPI_OFF + NW * EPI_WREG;
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
     __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES];
 #define LDS_STAGE(b_) (lds_raw + (b_) * OPB)
-    char * sbuf = lds_raw + 2 * OPB;                      // scale staging (only when BLK)
+    char * sbuf = lds_raw + NS * OPB;                     // scale staging (only when BLK)
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
 
@@ -452,7 +474,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     }
     constexpr bool GROUPABLE = !PIPE && !BF && BLK == 0 && EPI == Q2A_EPI_STORE_F;
     const int ngrp = (GROUPABLE && p.ngroup == 2) ? 2 : 1;
-    const int ksplit = (!PIPE && (BLK == 0 || BLK == 256 || BLK == 32) && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) &&
+    const int ksplit = (!PIPE && (BLK == 0 || BLK == 32) && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) &&
                         p.ksplit > 1 && ngrp == 1) ? p.ksplit : 1;
     const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, ntl = nbn * nbm, nwg = ntl * ksplit * ngrp;
     const int bid = blockIdx.x, xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
@@ -504,13 +526,17 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
         // scale chunk c of K-block group g (BLK=256: block g; BLK=32: blocks 2g, 2g+1) -> global source
         auto scale_src = [&](int c, int g) -> const uint4 * {
             if (BLK == 256) {
+                if (c < BM / 4) return (const uint4 *) (p.dy + (int64_t) max(g - 1, 0) * p.dy_ld + m0) + c;
+                c -= BM / 4;
                 if (c < BM / 4) return (const uint4 *) (p.dy + (int64_t) g * p.dy_ld + m0) + c;
                 c -= BM / 4;
                 if (c < BM * 2) return (const uint4 *) (p.aext + ((int64_t) g * p.dy_ld + m0) * 16) + c;
                 c -= BM * 2;
-                if (c < BN / 4) return (const uint4 *) (p.dx + (int64_t) g * p.N + n0) + c;
+                if (c < BN / 4) return (const uint4 *) (p.beta + (int64_t) g * p.N + n0) + c;
                 c -= BN / 4;
-                if (c < BN / 4) return (const uint4 *) (p.dmin + (int64_t) g * p.N + n0) + c;
+                if (c < BN / 4) return (const uint4 *) (p.gamma + (int64_t) g * p.N + n0) + c;
+                c -= BN / 4;
+                if (c < BN / 4) return (const uint4 *) (p.dx + (int64_t) g * p.N + n0) + c;
                 c -= BN / 4;
                 return (const uint4 *) (p.wext + ((int64_t) g * p.N + n0) * 16) + c;
             } else {
@@ -519,7 +545,19 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                 return (const uint4 *) (p.dx + (int64_t) (2 * g + c / (BN / 4)) * p.N + n0) + c % (BN / 4);
             }
         };
-        uint4 sreg[BLK ? SCH : 1];
+        // Q4_K: piece q (0 <= q < SP * NW) of block g: chunk q * 64 + lane of the SB layout (16 B per lane), or a
+        // dummy re-load into this wave's pad piece when q >= SBP or the block does not exist
+        uint32_t l16s = lane * 16;
+        auto scale_piece = [&](int q, int g) {
+            asm volatile("" : "+v"(l16s));
+            const int c = q * 64 + lane;
+            const bool real = q < SBP && g < p.K / 256 && c < SB / 16;
+            const uint4 * src = real ? scale_src(c, g) : (const uint4 *) p.dy + lane;
+            char * dst = real ? sbuf + (g & 1) * SBP * 1024 + q * 1024 : sbuf + 2 * SBP * 1024 + wave * 1024;
+            if (q >= SBP || g >= p.K / 256) dst = sbuf + 2 * SBP * 1024 + wave * 1024;
+            __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) dst, 16, 0, 0);
+        };
+        uint4 sreg[BLK == 32 ? SCH : 1];
         auto scale_load = [&](int g) {
     #pragma unroll
             for (int u = 0; u < SCH; ++u) {
@@ -535,30 +573,79 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
             }
         };
 
-        f4 blk[BLK ? MI : 1][BLK ? NJ : 1];
-        if (BLK) {
+        // Q8_0 / Q4_0 (BLK = 32): a fresh accumulator per 32-block, combined acc += (dx*dy)*blk after each
+        f4 blk[BLK == 32 ? MI : 1][BLK == 32 ? NJ : 1];
+        if (BLK == 32) {
     #pragma unroll
-            for (int i = 0; i < (BLK ? MI : 1); ++i)
+            for (int i = 0; i < (BLK == 32 ? MI : 1); ++i)
     #pragma unroll
-                for (int j = 0; j < (BLK ? NJ : 1); ++j) blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+                for (int j = 0; j < (BLK == 32 ? NJ : 1); ++j) blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
         }
+        // Q4_K (BLK = 256): the block-ratio recurrence of the 8-phase kernel (kq_rescale), op for op
+        auto kq_block_start = [&](const char * sb) {
+            const float * s_dyp = (const float *) sb;
+            const float * s_dy = s_dyp + BM;
+            const q2a_half * s_ae = (const q2a_half *) (sb + BM * 8);
+            const float * s_be = (const float *) (sb + BM * 40);
+            const float * s_ga = s_be + BN;
+            const q2a_half * s_we = (const q2a_half *) (sb + BM * 40 + BN * 12);
+            f4 be[NJ], ga[NJ];
+            half4 we[NJ];
+    #pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const int n4 = wn * (BN / WN) + j * 16 + (lane >> 4) * 4;
+                be[j] = *(const f4 *) (s_be + n4);
+                ga[j] = *(const f4 *) (s_ga + n4);
+                we[j] = *(const half4 *) (s_we + (wn * (BN / WN) + j * 16 + (lane & 15)) * 16 + (lane >> 4) * 4);
+            }
+    #pragma unroll
+            for (int i = 0; i < MI; ++i) {
+                const int row = wm * (BM / WM) + i * 16 + (lane & 15);
+                const float al = kq_alpha(s_dyp[row], s_dy[row]);
+                const half4 ae = *(const half4 *) (s_ae + row * 16 + (lane >> 4) * 4);
+    #pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const f4 s2 = __builtin_amdgcn_mfma_f32_16x16x16f16(we[j], ae, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    #pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[i][j][r] = kq_rescale(acc[i][j][r], al, be[j][r], ga[j][r], s2[r]);
+                }
+            }
+        };
 
         const int nk = p.K / BK / ksplit;                 // K-steps of this split
         const int kb0 = ks * nk * BK;                     // its first K element
         const int gb0 = BLK == 256 ? kb0 / 256 : kb0 / BK;   // its first scale group (whole groups per split)
-        stage(LDS_STAGE(0), kb0);
+        const int nkb = p.K / 256;                        // Q4_K blocks
+        // prologue: block 0's scales, then stages 0 .. NS-2; K-step kt reads stage kt % NS and, before its MFMAs,
+        // issues stage kt + NS - 1 into the slot K-step kt - 1 read (behind the barrier that ended kt - 1)
+        constexpr int GL = LA + LB;                       // glds instructions per stage per thread
         if (BLK == 32) scale_load(gb0);
+        if (BLK == 256) {                                 // block 0's scales, every piece
+    #pragma unroll
+            for (int u = 0; u < SP; ++u) scale_piece(u * NW + wave, 0);
+        }
+    #pragma unroll
+        for (int q = 0; q < NS - 1; ++q)
+            if (q < nk) stage(LDS_STAGE(q), kb0 + q * BK);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (BLK == 32) scale_store(0);
         __syncthreads();
 
         for (int kt = 0; kt < nk; ++kt) {
-            const int cur = kt & 1;
-            if (kt + 1 < nk) stage(LDS_STAGE(cur ^ 1), kb0 + (kt + 1) * BK);
-            // Q4_K: block kt/4's scales are fetched at its first K-step and land in LDS at its end (3 steps early);
+            const int cur = kt % NS;
+            const bool issue = kt + NS - 1 < nk;
+            if (issue) stage(LDS_STAGE((kt + NS - 1) % NS), kb0 + (kt + NS - 1) * BK);
+            // Q4_K: block b starts at K-step 4b with its scales resident (buffer b&1), and block b+1's scales are
+            // fetched then and land in the other buffer at the end of that K-step;
             // Q8_0: the next K-step's two blocks are fetched one step ahead into the other buffer.
-            const bool sload = BLK == 256 ? (kt % 4 == 0) : (BLK == 32 && kt + 1 < nk);
-            if (sload) scale_load(gb0 + (BLK == 256 ? kt / 4 : kt + 1));
+            bool sload = false;
+            if (BLK == 256) {
+                if (kt % 4 == 0) kq_block_start(sbuf + ((kt / 4) & 1) * SBP * 1024);
+                if (kt % 4 < SP) scale_piece((kt % 4) * NW + wave, kt / 4 + 1);   // uniform: one per wave
+            } else if (BLK == 32 && kt + 1 < nk) {
+                sload = true;
+                scale_load(gb0 + kt + 1);
+            }
             const char * ia = LDS_STAGE(cur);
             const char * iw = LDS_STAGE(cur) + BM * ROWB;
     #pragma unroll
@@ -573,62 +660,77 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     #pragma unroll
                     for (int j = 0; j < NJ; ++j) {
                         // W as the A operand: C^T tiles (lane = 4 consecutive columns of one row, see the epilogue)
-                        if (BLK == 0) acc[i][j] = mma16<BF>(b[j], a, acc[i][j]);
+                        if (BLK != 32) acc[i][j] = mma16<BF>(b[j], a, acc[i][j]);
                         else blk[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], a, blk[i][j], 0, 0, 0);
                     }
                 }
-                if (BLK) {
-                    const int kpos = kt * BK + (s + 1) * 32;   // K consumed so far
-                    if (kpos % BLK == 0) {
-                        const char * sb = BLK == 256 ? sbuf : sbuf + cur * SB;
-                        const int sub = BLK == 256 ? 0 : s;                    // which of the K-step's two 32-blocks
-                        const float * s_dy = (const float *) sb + (BLK == 256 ? 0 : sub * BM);
-                        const q2a_half * s_ae = (const q2a_half *) (sb + BM * 4);
-                        const float * s_dx = (const float *) (sb + (BLK == 256 ? BM * 36 : 2 * BM * 4)) + (BLK == 256 ? 0 : sub * BN);
-                        const float * s_dm = (const float *) (sb + BM * 36 + BN * 4);
-                        const q2a_half * s_we = (const q2a_half *) (sb + BM * 36 + BN * 8);
-                        // C^T tiles: per-column scales as float4 (columns 16j + 4(lane>>4) + r), per-row as a scalar
-                        f4 dx[NJ], dm[NJ];
-                        half4 we[NJ];
+                if (BLK == 32) {
+                    const char * sb = sbuf + (kt & 1) * SB;
+                    const float * s_dy = (const float *) sb + s * BM;
+                    const float * s_dx = (const float *) (sb + 2 * BM * 4) + s * BN;
+                    // C^T tiles: per-column scales as float4 (columns 16j + 4(lane>>4) + r), per-row as a scalar
+                    f4 dx[NJ];
+    #pragma unroll
+                    for (int j = 0; j < NJ; ++j) dx[j] = *(const f4 *) (s_dx + wn * (BN / WN) + j * 16 + (lane >> 4) * 4);
+    #pragma unroll
+                    for (int i = 0; i < MI; ++i) {
+                        const float dyi = s_dy[wm * (BM / WM) + i * 16 + (lane & 15)];
     #pragma unroll
                         for (int j = 0; j < NJ; ++j) {
-                            const int n4 = wn * (BN / WN) + j * 16 + (lane >> 4) * 4;
-                            dx[j] = *(const f4 *) (s_dx + n4);
-                            if (BLK == 256) {
-                                dm[j] = *(const f4 *) (s_dm + n4);
-                                we[j] = *(const half4 *) (s_we + (wn * (BN / WN) + j * 16 + (lane & 15)) * 16 + (lane >> 4) * 4);
-                            }
-                        }
     #pragma unroll
-                        for (int i = 0; i < MI; ++i) {
-                            const float dyi = s_dy[wm * (BM / WM) + i * 16 + (lane & 15)];
-                            half4 ae;
-                            if (BLK == 256) {
-                                // min term S2 = sum_j m_j * bsum32_j: one 16x16x16 MFMA per tile on (hi,lo)-split bsums
-                                ae = *(const half4 *) (s_ae + (wm * (BM / WM) + i * 16 + (lane & 15)) * 16 + (lane >> 4) * 4);
-                            }
-    #pragma unroll
-                            for (int j = 0; j < NJ; ++j) {
-                                if (BLK == 256) {
-                                    const f4 s2 = __builtin_amdgcn_mfma_f32_16x16x16f16(we[j], ae, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-    #pragma unroll
-                                    for (int r = 0; r < 4; ++r) {
-                                        acc[i][j][r] += (dyi * dx[j][r]) * blk[i][j][r];
-                                        acc[i][j][r] -= (dyi * dm[j][r]) * s2[r];
-                                    }
-                                } else {
-    #pragma unroll
-                                    for (int r = 0; r < 4; ++r) acc[i][j][r] += (dx[j][r] * dyi) * blk[i][j][r];
-                                }
-                                blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-                            }
+                            for (int r = 0; r < 4; ++r) acc[i][j][r] += (dx[j][r] * dyi) * blk[i][j][r];
+                            blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
                         }
                     }
                 }
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            if (sload) scale_store(BLK == 256 ? 0 : cur ^ 1);
-            __syncthreads();
+            // stage kt + 1 must have landed before the barrier; the NS - 2 younger stages stay in flight (raw
+            // s_barrier: __syncthreads would drain them). Steps that fetched scales into registers drain fully.
+            if (sload) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                scale_store((kt & 1) ^ 1);
+            } else if (issue && NS > 2) {
+                if constexpr (BLK == 256) {
+                    // younger than stage kt+1: the NS-2 stages of steps kt+3-NS .. kt and the scale pieces of those
+                    // steps (steps with s % 4 < SP)
+                    constexpr int W0 = GL * (NS - 2);
+                    auto npc = [](int r) {   // pieces issued in the NS-2 steps ending at a step with kt % 4 == r
+                        int n = 0;
+                        for (int d = 0; d < NS - 2; ++d) n += (((r - d) % 4 + 4) % 4) < SP;
+                        return n;
+                    };
+                    switch (kt & 3) {
+                        case 0: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(W0 + npc(0)) : "memory"); break;
+                        case 1: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(W0 + npc(1)) : "memory"); break;
+                        case 2: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(W0 + npc(2)) : "memory"); break;
+                        default: asm volatile("s_waitcnt vmcnt(%0)" :: "n"(W0 + npc(3)) : "memory"); break;
+                    }
+                } else {
+                    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(GL * (NS - 2)) : "memory");
+                }
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            asm volatile("" ::: "memory");
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if constexpr (BLK == 256) {
+            // acc is in units of the last block's scale: multiply by dy_last[m] * dx_last[n]
+            const char * sb = sbuf + ((nkb - 1) & 1) * SBP * 1024;
+            const float * s_dy = (const float *) sb + BM;
+            const float * s_dx = (const float *) (sb + BM * 40 + BN * 8);
+    #pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                const f4 dx4 = *(const f4 *) (s_dx + wn * (BN / WN) + j * 16 + (lane >> 4) * 4);
+    #pragma unroll
+                for (int i = 0; i < MI; ++i) {
+                    const float yc = s_dy[wm * (BM / WM) + i * 16 + (lane & 15)];
+    #pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[i][j][r] = kq_final(acc[i][j][r], yc, dx4[r]);
+                }
+            }
         }
     }
 
@@ -951,7 +1053,7 @@ __global__ void k_split_reduce(const float * __restrict__ part, int S, int64_t s
 template <int BM, int BN, int WM, int WN, int EPI, int BLK, int PIPE = 0>
 hipError_t launch_cfg(const q2a_gemm_args & a, hipStream_t s) {
     const bool grouped = !PIPE && BLK == 0 && EPI == Q2A_EPI_STORE_F && a.ngroup == 2;
-    const bool split = !PIPE && (BLK == 0 || BLK == Q2A_BLK_BF16 || BLK == 256 || BLK == 32) &&
+    const bool split = !PIPE && (BLK == 0 || BLK == Q2A_BLK_BF16 || BLK == 32) &&
                        (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) && a.ksplit > 1 && !grouped;
     const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM) * (split ? a.ksplit : 1) * (grouped ? 2 : 1);
     hipLaunchKernelGGL((k_gemm<BM, BN, WM, WN, EPI, BLK, PIPE>), dim3(nwg), dim3(WM * WN * 64), 0, s, a);
@@ -965,6 +1067,12 @@ hipError_t launch_cfg(const q2a_gemm_args & a, hipStream_t s) {
                                a.split_stride, a.M, a.N, a.store_bias ? a.bias : nullptr, a.outF, a.ldo, a.resid, a.out_scale);
     }
     return hipGetLastError();
+}
+
+// small M (one or a few clips): 64-row tiles when 128x128 tiles would leave CUs idle
+bool narrow_tiles(int M, int N) {
+    static const int off = [] { const char * v = getenv("Q2A_GEMM_NO_NARROW"); return v ? atoi(v) : 0; }();
+    return !off && (int64_t) ((M + 127) / 128) * (N / 128) < 256;
 }
 
 bool wide_tiles(int M, int N) {
@@ -1001,19 +1109,29 @@ hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
         if (p8) return launch_cfg<256, 256, 2, 4, EPI, 256, 1>(a, s);
         return launch_cfg<128, 256, 2, 4, EPI, 256>(a, s);
     } else {
+        // every configuration sums K in the same order (64-deep K-steps, two 32-deep MFMAs each; Q4_K with the
+        // same block recurrence): a clip's outputs are bit-identical whichever tile regime its batch size selects
+        const bool narrow = !big && narrow_tiles(a.M, a.N) && a.ksplit <= 1 && a.ngroup != 2;
         if (blk == 0) {
             if (p8) return launch_cfg<256, 256, 2, 4, EPI, 0, 1>(a, s);
+            if (narrow) return launch_cfg<64, 128, 2, 2, EPI, 0>(a, s);
             return big ? launch_cfg<256, 256, 2, 4, EPI, 0>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 0>(a, s);
         }
         if (blk == 256) {
+            if (!a.beta || !a.gamma) return hipErrorInvalidValue;   // the block recurrence needs beta / gamma
             if (p8) return launch_cfg<256, 256, 2, 4, EPI, 256, 1>(a, s);
+            if (narrow) return launch_cfg<64, 128, 2, 2, EPI, 256>(a, s);
             return big ? launch_cfg<128, 256, 2, 4, EPI, 256>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 256>(a, s);
         }
-        if (blk == 32) return big ? launch_cfg<128, 256, 2, 4, EPI, 32>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 32>(a, s);
+        if (blk == 32) {
+            if (narrow) return launch_cfg<64, 128, 2, 2, EPI, 32>(a, s);
+            return big ? launch_cfg<128, 256, 2, 4, EPI, 32>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 32>(a, s);
+        }
         if constexpr (EPI == Q2A_EPI_QKV || EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_STORE_F) {
             if (blk == Q2A_BLK_BF16) {
                 constexpr int B16 = Q2A_BLK_BF16;
                 if (p8) return launch_cfg<256, 256, 2, 4, EPI, B16, 1>(a, s);
+                if (narrow) return launch_cfg<64, 128, 2, 2, EPI, B16>(a, s);
                 return big ? launch_cfg<256, 256, 2, 4, EPI, B16>(a, s) : launch_cfg<128, 128, 2, 2, EPI, B16>(a, s);
             }
         }
@@ -1023,17 +1141,24 @@ hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
 
 }  // namespace
 
+// Split-K of the small-tile residual GEMMs: OFF by default (opt-in Q2A_GEMM_SPLITK=1). Partial sums combined
+// across splits change the fp32 summation order, so a clip's output would depend on whether its batch took the
+// small-tile or the 8-phase regime; without it every regime sums K identically (batch invariance).
+static bool splitk_on() {
+    static const int on = [] { const char * v = getenv("Q2A_GEMM_SPLITK"); return v ? atoi(v) : 0; }();
+    return on != 0;
+}
+
 int q2a_gemm_resid_ksplit(int M, int N, int K, int blk) {
-    static const int off = [] { const char * v = getenv("Q2A_GEMM_NO_SPLITK"); return v ? atoi(v) : 0; }();
-    if (off || !(blk == 0 || blk == Q2A_BLK_BF16) || wide_tiles(M, N) || N % 128) return 0;
+    if (!splitk_on() || !(blk == 0 || blk == Q2A_BLK_BF16) || wide_tiles(M, N) || N % 128) return 0;
     const int nk = K / BK;
     const int S = K >= 4096 ? 4 : K >= 1024 ? 2 : 0;
     return S && nk % S == 0 ? S : 0;
 }
 
 int q2a_gemm_kq_ksplit(int M, int N, int K, int blk) {
-    static const int off = [] { const char * v = getenv("Q2A_GEMM_NO_SPLITK"); return v ? atoi(v) : 0; }();
-    if (off || !(blk == 256 || blk == 32) || wide_tiles(M, N) || N % 128) return 0;
+    // Q8_0 / Q4_0 only (opt-in); Q4_K never splits (its block recurrence runs through every K-block in order)
+    if (!splitk_on() || blk != 32 || wide_tiles(M, N) || N % 128) return 0;
     // whole scale groups per split: 4 K-steps per Q4_K block, 1 per Q8_0/Q4_0 pair of blocks
     const int nk = K / BK, unit = blk == 256 ? 4 : 1;
     for (int S : {4, 5, 2, 3})

@@ -79,6 +79,17 @@ def relerr(a, b):
     return float(np.abs(d).max() / np.abs(b).max()), float(np.linalg.norm(d) / np.linalg.norm(b))
 
 
+def pair_stats(y, ref, idx):
+    """The statistics the GPU parity tests compute (tests/test_gpu_parity.py), for one pair of outputs: on the full
+    [750][1280] output, on the golden's 8192 sampled indices, and the max row-norm error."""
+    mx, l2 = relerr(y, ref)
+    smx, sl2 = relerr(y.reshape(-1)[idx], ref.reshape(-1)[idx])
+    rn = np.linalg.norm(y.reshape(750, -1).astype(np.float64), axis=1)
+    rr = np.linalg.norm(ref.reshape(750, -1).astype(np.float64), axis=1)
+    return {"max_rel": mx, "rel_l2": l2, "sampled_max_rel": smx, "sampled_rel_l2": sl2,
+            "rownorm_rel": float(np.abs(rn - rr).max() / rr.max())}
+
+
 def run_ref(build, model, clip, out, dump, nthreads):
     exe = os.path.join(ROOT, "oracle", BUILDS[build], "ref_harness")
     if os.path.exists(dump):
@@ -104,6 +115,7 @@ def main():
     ap.add_argument("--types", default="q4_k,q8_0,f16")
     ap.add_argument("--builds", default="x86-64,avx512")
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
+    ap.add_argument("--summarize-only", action="store_true", help="recompute pair statistics from existing outputs")
     args = ap.parse_args()
     os.makedirs(args.workdir, exist_ok=True)
     with open(os.path.join(HERE, "golden.json")) as f:
@@ -119,6 +131,18 @@ def main():
     base = os.path.join(args.workdir, "full-f16.bin")
     if not os.path.exists(base):
         subprocess.check_call([TOOL, "gen-model", base, "full", "f16", "0x51A2", str(args.threads)])
+    gold = dict(np.load(os.path.join(HERE, "golden.npz"), allow_pickle=False))
+    if args.summarize_only:
+        for wt in args.types.split(","):
+            finals = {b: np.fromfile(os.path.join(args.workdir, f"{wt}-{b}.out"), dtype=np.float32)
+                      for b in ["avx2"] + args.builds.split(",")}
+            names = list(finals)
+            result[wt]["pairs"] = {f"{a}_vs_{c}": pair_stats(finals[c], finals[a], gold[f"full_{wt}_c0_idx"])
+                                   for i, a in enumerate(names) for c in names[i + 1:]}
+        with open(outp, "w") as f:
+            json.dump(result, f, indent=1, sort_keys=True)
+        print("wrote", outp)
+        return
     for wt in args.types.split(","):
         model = base if wt == "f16" else os.path.join(args.workdir, f"full-{wt}.bin")
         if not os.path.exists(model):
@@ -155,8 +179,7 @@ def main():
         names = list(finals)
         for i, a in enumerate(names):
             for c in names[i + 1:]:
-                mx, l2 = relerr(finals[c], finals[a])
-                ent["pairs"][f"{a}_vs_{c}"] = {"max_rel": mx, "rel_l2": l2}
+                ent["pairs"][f"{a}_vs_{c}"] = pair_stats(finals[c], finals[a], gold[f"full_{wt}_c0_idx"])
         result[wt] = ent
         print(wt, json.dumps(ent["pairs"]), flush=True)
         with open(outp, "w") as f:

@@ -69,7 +69,7 @@ def test_backend_unfused_attention_path(harness, make_model, make_clip, golden, 
 
 
 @pytest.mark.parametrize("wt", ["f16", "q4_k"])
-def test_reference_whisper_full_on_backend_full_size(harness, make_model, make_clip, golden, wt, tmp_path):
+def test_reference_whisper_full_on_backend_full_size(harness, make_model, make_clip, golden, xbuild_bar, wt, tmp_path):
     _, g = golden
     emb, info = run(harness, make_model("full", wt), make_clip(0), tmp_path)
     assert info["mul_mat_fast"] == 6 * 32 and info["attn_fused"] == 32, info
@@ -77,10 +77,10 @@ def test_reference_whisper_full_on_backend_full_size(harness, make_model, make_c
     mxs, l2s = rel_errors(o[g[f"full_{wt}_c0_idx"]], g[f"full_{wt}_c0_val"])
     rn = np.linalg.norm(emb.astype(np.float64), axis=1)
     rnerr = np.abs(rn - g[f"full_{wt}_c0_rownorm"]).max() / g[f"full_{wt}_c0_rownorm"].max()
+    bar = xbuild_bar(wt)   # the reference's own cross-build spread
+    assert mxs < bar["max_rel"] and l2s < bar["rel_l2"] and rnerr < 20 * bar["rownorm_rel"], (mxs, l2s, rnerr, bar)
     if wt == "f16":
-        assert mxs < 1e-3 and l2s < 1e-3 and rnerr < 1e-4, (mxs, l2s, rnerr)
-    else:   # inherent activation re-quantization flips, as for the engine
-        assert l2s < 2e-2 and rnerr < 2e-3, (mxs, l2s, rnerr)
+        assert mxs < 1e-3 and l2s < 1e-3
 
 
 @pytest.mark.parametrize("wt", ["f16", "q4_k"])
@@ -102,13 +102,12 @@ def test_backend_graph_replay_matches_direct(harness, make_model, make_clip, tmp
 def test_backend_fusions_match_per_node(harness, make_model, make_clip, tmp_path, wt):
     """Nodes folded into their producer's kernel (MUL_MAT -> ADD bias [-> GELU | ADD residual] on the GEMM epilogue,
     NORM -> MUL -> ADD in one row kernel) compute the same f32 operations as the per-node launches
-    (GGML_Q2A_NO_FUSE=1): embd_enc is bit-identical. Both runs without the single-clip split-K
-    (Q2A_GEMM_NO_SPLITK=1): the grouped K|Q launch never splits, so with it on the fp32 summation orders would differ
-    (its accuracy is what the golden tests above check)."""
+    (GGML_Q2A_NO_FUSE=1): embd_enc is bit-identical (no GEMM configuration splits K by default, so the grouped K|Q
+    launch and the per-node launches sum in the same order)."""
     model, clip = make_model("tiny", wt), make_clip(1)
-    plain, info_p = run(harness, model, clip, tmp_path, {"GGML_Q2A_NO_FUSE": "1", "Q2A_GEMM_NO_SPLITK": "1"})
+    plain, info_p = run(harness, model, clip, tmp_path, {"GGML_Q2A_NO_FUSE": "1"})
     assert info_p["fused"] == 0 and info_p["mm_grouped"] == 0, info_p
-    fused, info_f = run(harness, model, clip, tmp_path, {"Q2A_GEMM_NO_SPLITK": "1"})
+    fused, info_f = run(harness, model, clip, tmp_path, {})
     L = 2
     # per layer: Q bias + scale, V bias, O bias + residual, fc1 bias + GELU, fc2 bias + residual, two LayerNorm affines,
     # the attention output CONT;
@@ -118,3 +117,34 @@ def test_backend_fusions_match_per_node(harness, make_model, make_clip, tmp_path
     assert info_f["mm_grouped"] == (L if wt == "f16" else 0), info_f
     assert info_f["other"] < info_p["other"], (info_f, info_p)
     assert np.array_equal(fused, plain)
+
+
+def test_graph_capture_dropped_when_scratch_grows(harness):
+    """a captured HIP graph holds the scratch's address. A small MUL_MAT graph is captured and replayed,
+    a larger graph on the same backend then grows the scratch: the small graph must be re-run and re-captured (never
+    replayed against the freed buffer) and give the same bytes (oracle/ggml_harness.cpp cmd_graphs)."""
+    r = subprocess.run([harness, "graphs"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:] + r.stdout[-2000:]
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    assert info["replayed_third"] == 1, info
+    assert info["reallocs_after_big"] > info["reallocs_before_big"], info
+    assert info["replayed_after_grow"] == 0 and info["recaptured"] == 1 and info["replayed_again"] == 1, info
+    assert info["equal"] is True
+
+
+@pytest.mark.parametrize("cfg", ["tiny", "full"])
+def test_conv_hilo_path_runs_and_matches_exact_f32(harness, make_model, make_clip, golden, xbuild_bar, cfg, tmp_path):
+    """the conv MUL_MAT(F32 im2col, F16 kernel) runs on the fp16 MFMA GEMM with hi/lo-split activations
+    (both convs of the conv graph), and agrees with the exact-f32 MFMA GEMM path (GGML_Q2A_NO_CONV_HILO=1)."""
+    _, g = golden
+    model = make_model(cfg, "f16")
+    hilo, info_h = run(harness, model, make_clip(0), tmp_path)
+    assert info_h["mm_conv_total"] == 2, info_h
+    exact, info_e = run(harness, model, make_clip(0), tmp_path, {"GGML_Q2A_NO_CONV_HILO": "1"})
+    assert info_e["mm_conv_total"] == 0, info_e
+    mx, l2 = rel_errors(hilo, exact)
+    if cfg == "tiny":   # the two conv outputs differ by f32 rounding only; the F16 blocks' fp16 roundings amplify it
+        assert mx < 1e-3 and l2 < 1e-4, (mx, l2)
+    else:   # through 32 layers both sit within the reference's own F16 cross-build spread of each other
+        bar = xbuild_bar("f16")
+        assert mx < bar["max_rel"] and l2 < bar["rel_l2"], (mx, l2, bar)
