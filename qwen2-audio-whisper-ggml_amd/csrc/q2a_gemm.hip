@@ -454,7 +454,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     constexpr int SCALE_LDS = BLK == 256 ? (2 * SBP + NW) * 1024 : BLK ? NSB * SB : 0;
     constexpr int NS_FIT = (150 * 1024 - SCALE_LDS) / OPB;
     constexpr int NS_MAX = BLK == 256 ? 6 - SP : 5;
-    constexpr int NS = PIPE ? 2 : (BLK == 32 ? 2 : (NS_FIT >= NS_MAX ? NS_MAX : NS_FIT >= 2 ? NS_FIT : 2));
+    // deep pipelines only on the narrow 64-row tiles (grids under one workgroup per CU); the 128-row tiles keep two
+    // stages so two workgroups share a CU (their grids have several tiles per CU)
+    constexpr int NS = PIPE || BLK == 32 || BM > 64 ? 2 : (NS_FIT >= NS_MAX ? NS_MAX : NS_FIT >= 2 ? NS_FIT : 2);
     static_assert(PIPE || BLK != 256 || SP + NS <= 6, "Q4_K scale prefetch distance");
     constexpr int LDS_MAIN = PIPE ? (BLK ? SBUF_OFF + SBUF_BYTES : 2 * OPB) : NS * OPB + SCALE_LDS;
     constexpr int LDS_BYTES = LDS_MAIN > EPI_OFF + NW * EPI_WREG ? LDS_MAIN : EPI_OFF + NW * EPI_WREG;
