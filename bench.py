@@ -330,6 +330,17 @@ def main():
         if "hbm_bytes_per_launch_corrected" in k:
             traffic, traffic_src = k["hbm_bytes_per_launch_corrected"], "profiles/" + pmc_files[-1]
 
+    # MFMA busy fraction of the same kernel from the committed SQ counter pass (profiles/collect_sq.sh +
+    # sq_summary.py): SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs), rocprof's MfmaUtil
+    mfma_busy, mfma_src = None, None
+    sq_files = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith(f"_{args.config}_sq_mfma.json")) \
+        if os.path.isdir(os.path.join(ROOT, "profiles")) else []
+    if sq_files:
+        with open(os.path.join(ROOT, "profiles", sq_files[-1])) as f:
+            for e in json.load(f)["kernels"].values():
+                if e.get("class") == "gemm_fc1" and "mfma_busy_frac" in e:
+                    mfma_busy, mfma_src = round(e["mfma_busy_frac"], 4), "profiles/" + sq_files[-1]
+
     cpu = None
     if ws == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(model_path, wt, args.workdir, args.cpu_reps)
@@ -361,7 +372,8 @@ def main():
                      "frac": round(achieved / PEAK_FP16_MFMA_TFLOPS, 4), "traffic": traffic,
                      "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
                      "flop_per_launch": fc1_flop, "avg_launch_ms": round(fc1_avg_s * 1e3, 4),
-                     "all_weight_gemms_tflops": round(gemm_tf, 1)},
+                     "all_weight_gemms_tflops": round(gemm_tf, 1),
+                     "mfma_busy_frac": mfma_busy, "mfma_busy_source": mfma_src},
         "cpu_baseline": cpu,
         "pcie_inclusive_frames_per_s": round(pcie_rate, 1),
         "per_kernel": per_kernel,

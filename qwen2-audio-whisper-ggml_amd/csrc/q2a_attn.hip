@@ -16,6 +16,8 @@
 // its B operand with no data movement (cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand").
 #include "q2a_internal.h"
 
+#include <cstdlib>
+
 namespace {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
@@ -58,7 +60,9 @@ template <> struct attn_lds<true> {
 constexpr float L2E = 1.4426950408889634f;   // exp(x) = exp2(x * log2 e)
 
 // BF: bf16-activation mode (Q, K, V^T, P and the output in bf16; S = K.Q^T is one MFMA per 16-deep step)
-template <bool BF>
+// QT: fp16 terms of S in the reference contract (3: Kh.Qh + Kl.Qh + Kh.Ql, the default; 2 / 1: precision experiments,
+// Q2A_ATTN_TERMS, diag only)
+template <bool BF, int QT = 3>
 __global__ __launch_bounds__(256, BF ? 3 : Q2A_ATTN_F32_OCC) void k_attn(const q2a_attn_args p) {
     typedef attn_lds<BF> LY;
     constexpr int KROW = LY::KROW, VROW = LY::VROW;
@@ -158,9 +162,11 @@ __global__ __launch_bounds__(256, BF ? 3 : Q2A_ATTN_F32_OCC) void k_attn(const q
                 const half8 ah = *(const half8 *) (kh_img + off);
                 sc[kb] = mma32<BF>(ah, qh[st], sc[kb]);
                 if (!BF) {
-                    const half8 al = *(const half8 *) (kl_img + off);
-                    sc[kb] = mma32<BF>(al, qh[st], sc[kb]);
-                    sc[kb] = mma32<BF>(ah, ql[st], sc[kb]);
+                    if (QT >= 3) {
+                        const half8 al = *(const half8 *) (kl_img + off);
+                        sc[kb] = mma32<BF>(al, qh[st], sc[kb]);
+                    }
+                    if (QT >= 2) sc[kb] = mma32<BF>(ah, ql[st], sc[kb]);
                 }
             }
         }
@@ -250,7 +256,10 @@ hipError_t q2a_launch_attention(const q2a_attn_args & a, hipStream_t s) {
         if (!a.outH) return hipErrorInvalidValue;
         hipLaunchKernelGGL(k_attn<true>, grid, dim3(256), 0, s, a);
     } else {
-        hipLaunchKernelGGL(k_attn<false>, grid, dim3(256), 0, s, a);
+        static const int terms = [] { const char * v = getenv("Q2A_ATTN_TERMS"); return v ? atoi(v) : 3; }();
+        if (terms == 2) hipLaunchKernelGGL((k_attn<false, 2>), grid, dim3(256), 0, s, a);
+        else if (terms == 1) hipLaunchKernelGGL((k_attn<false, 1>), grid, dim3(256), 0, s, a);
+        else hipLaunchKernelGGL(k_attn<false>, grid, dim3(256), 0, s, a);
     }
     return hipGetLastError();
 }
