@@ -247,16 +247,267 @@ __global__ __launch_bounds__(256, BF ? 3 : Q2A_ATTN_F32_OCC) void k_attn(const q
     }
 }
 
+// ---- ping-pong variant (default): one 512-thread workgroup = 8 waves x 32 queries (256 queries of one (clip, head)),
+// the two waves that share a SIMD (w and w + 4) run the same loop one segment apart: while group A (waves 0-3) is in
+// its MFMA segment (P.V of the previous tile + QK^T of this one, 32 MFMAs) group B (waves 4-7) is in its VALU segment
+// (the online-softmax update of its scores), and the other way round after the next workgroup barrier — the matrix
+// pipe and the VALU of each SIMD busy at once (MI355X_MICROARCH.md "Two waves per SIMD"). K/V tiles of 64 keys in
+// three LDS stages: tile t is read from segment 2t (A's QK^T) to 2t+3 (B's P.V); tile t+3 is written into tile t's
+// stage by A in its VALU segment 2t+5 and by B in its VALU segment 2t+4 (one half each), from registers loaded two
+// segments earlier. Per element the arithmetic of k_attn: S = Kh.Qh + Kl.Qh + Kh.Ql in the same MFMA order, one
+// online-softmax update per 64 keys, P and V fp16 (bf16 in the bf16-activation mode) into the P.V MFMA.
+template <bool BF>
+__global__ __launch_bounds__(512, 2) void k_attn_pp(const q2a_attn_args p) {
+    typedef attn_lds<false> LY;
+    constexpr int KROW = LY::KROW, VROW = LY::VROW;
+    constexpr int KIMG = KT * KROW, VIMG = 64 * VROW;
+    constexpr int NK = BF ? 1 : 2;                 // K images per stage (hi, lo)
+    constexpr int STAGE = NK * KIMG + VIMG;
+    constexpr int NST = 3;
+    constexpr int CH = (NK + 1) * 512;             // 16-B chunks per tile: K images then V^T
+    constexpr int CPT = CH / 512;                  // chunks per thread of one group's half tile (CH / 2 / 256)
+    __shared__ __attribute__((aligned(16))) char lds[NST * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int grp = wave >> 2, gt = tid & 255;     // group A (0) / B (1), thread index within the group
+    const int T = p.T, D = p.D;
+    const int nq = (T + 255) / 256, total = (int) gridDim.x;
+    const int L = (int) blockIdx.x;
+    const int w = (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);
+    const int qt = w % nq, h = (w / nq) % p.H, clip = w / (nq * p.H);
+    const int q0 = qt * 256 + wave * 32;
+    const int64_t rowbase = (int64_t) clip * T;
+    const int hi = lane >> 5, col = lane & 31;
+
+    half8 qh[4], ql[4];
+    {
+        const int q = min(q0 + col, T - 1);
+        const q2a_half * sh = p.qh + (rowbase + q) * D + h * 64 + 8 * hi;
+        const q2a_half * sl = p.ql + (rowbase + q) * D + h * 64 + 8 * hi;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            qh[s] = *(const half8 *) (sh + 16 * s);
+            ql[s] = BF ? qh[s] : *(const half8 *) (sl + 16 * s);
+        }
+    }
+    const q2a_half * vt_base = p.vt + ((int64_t) clip * p.H + h) * 64 * p.TP;
+    // staging: this group's half of a tile, CPT 16-B chunks per thread. Chunk c of the tile (0 .. CH-1): image
+    // c / 512 (Kh, [Kl,] V^T), row (c % 512) / 8, 16-B piece c % 8.
+    uint4 rg[CPT];
+    auto chunk_of = [&](int u) __attribute__((always_inline)) { return grp * (CH / 2) + u * 256 + gt; };
+    auto load_half = [&](int t) __attribute__((always_inline)) {
+        const int kb0 = t * KT;
+#pragma unroll
+        for (int u = 0; u < CPT; ++u) {
+            const int c = chunk_of(u), img = c >> 9, r = (c >> 3) & 63, pc = c & 7;
+            if (img < NK) {
+                const q2a_half * src = img == 0 ? p.kh : p.kl;
+                rg[u] = *(const uint4 *) (src + (rowbase + min(kb0 + r, T - 1)) * D + h * 64 + pc * 8);
+            } else {
+                rg[u] = *(const uint4 *) (vt_base + (int64_t) r * p.TP + kb0 + pc * 8);
+            }
+        }
+    };
+    auto store_half = [&](int t) __attribute__((always_inline)) {
+        char * st = lds + (t % NST) * STAGE;
+#pragma unroll
+        for (int u = 0; u < CPT; ++u) {
+            const int c = chunk_of(u), img = c >> 9, r = (c >> 3) & 63, pc = c & 7;
+            if (img < NK) {
+                *(uint4 *) (st + img * KIMG + r * KROW + LY::k(r, pc)) = rg[u];
+            } else {
+                char * vr = st + NK * KIMG + r * VROW;
+                *(uint2 *) (vr + LY::v(r, 2 * pc)) = make_uint2(rg[u].x, rg[u].y);
+                *(uint2 *) (vr + LY::v(r, 2 * pc + 1)) = make_uint2(rg[u].z, rg[u].w);
+            }
+        }
+    };
+    auto barrier = [&]() __attribute__((always_inline)) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // LDS writes done; global prefetch stays in flight
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+
+    f16v o[2], sc[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+    float m_run = -1e30f, l_run = 0.f, alpha = 1.f;
+    half8 pf[2][2];
+
+    // MFMA segment M(t): P.V(t-1) (t > 0) then S^T = K_t . Q^T
+    auto mfma_seg = [&](int t, int ntiles) __attribute__((always_inline)) {
+        if (t > 0) {
+            if (__any(alpha != 1.0f)) {
+#pragma unroll
+                for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+            }
+            const char * vt_img = lds + ((t - 1) % NST) * STAGE + NK * KIMG;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int dt = 0; dt < 2; ++dt) {
+                    const int vr = dt * 32 + col;
+                    const char * vrow = vt_img + vr * VROW;
+#pragma unroll
+                    for (int sp = 0; sp < 2; ++sp) {
+                        const int c8 = 8 * kb + 4 * sp + hi;
+                        const half4 v0 = *(const half4 *) (vrow + LY::v(vr, c8));
+                        const half4 v1 = *(const half4 *) (vrow + LY::v(vr, c8 + 2));
+                        const half8 va = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+                        o[dt] = mma32<BF>(va, pf[kb][sp], o[dt]);
+                    }
+                }
+        }
+        if (t < ntiles) {
+            const char * kh_img = lds + (t % NST) * STAGE;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                const int krow = kb * 32 + col;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sc[kb][r] = 0.f;
+#pragma unroll
+                for (int st = 0; st < 4; ++st) {
+                    const int off = krow * KROW + LY::k(krow, 2 * st + hi);
+                    const half8 ah = *(const half8 *) (kh_img + off);
+                    sc[kb] = mma32<BF>(ah, qh[st], sc[kb]);
+                    if (!BF) {
+                        const half8 al = *(const half8 *) (kh_img + KIMG + off);
+                        sc[kb] = mma32<BF>(al, qh[st], sc[kb]);
+                        sc[kb] = mma32<BF>(ah, ql[st], sc[kb]);
+                    }
+                }
+            }
+        }
+    };
+    // VALU segment V(t): online-softmax update of tile t's scores -> pf, alpha (applied at the next P.V)
+    auto valu_seg = [&](int t, int ntiles) __attribute__((always_inline)) {
+        if (t == ntiles - 1) {   // keys >= T exist only in the last tile (row of reg r = (r&3) + 8(r>>2) + 4hi)
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (t * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi >= T) sc[kb][r] = -1e30f;
+        }
+        float mx0 = sc[0][0], mx1 = sc[1][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) { mx0 = fmaxf(mx0, sc[0][r]); mx1 = fmaxf(mx1, sc[1][r]); }
+        float mx = fmaxf(mx0, mx1);
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float m_new = fmaxf(m_run, mx);
+        const float nm = -m_new * L2E;
+        alpha = __builtin_amdgcn_exp2f(fmaf(m_run, L2E, nm));
+        float ls0 = 0.f, ls1 = 0.f;
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float pv = __builtin_amdgcn_exp2f(fmaf(sc[kb][r], L2E, nm));
+                if (r & 1) ls1 += pv; else ls0 += pv;
+                pf[kb][r >> 3][r & 7] = to16<BF>(pv);
+            }
+        l_run = l_run * alpha + (ls0 + ls1);
+        m_run = m_new;
+    };
+
+    const int ntiles = (T + KT - 1) / KT;
+    // prologue: tiles 0, 1, 2 into the three stages, every thread a share of each
+    {
+        // prologue staging by every thread: tile t's 2 halves = all CH chunks, 512 threads
+#pragma unroll
+        for (int t = 0; t < NST; ++t) {
+            if (t >= ntiles) break;
+            const int kb0 = t * KT;
+            char * st = lds + t * STAGE;
+#pragma unroll
+            for (int u = 0; u < CH / 512; ++u) {
+                const int c = u * 512 + tid, img = c >> 9, r = (c >> 3) & 63, pc = c & 7;
+                if (img < NK) {
+                    const q2a_half * src = img == 0 ? p.kh : p.kl;
+                    *(uint4 *) (st + img * KIMG + r * KROW + LY::k(r, pc)) =
+                        *(const uint4 *) (src + (rowbase + min(kb0 + r, T - 1)) * D + h * 64 + pc * 8);
+                } else {
+                    const uint4 v = *(const uint4 *) (vt_base + (int64_t) r * p.TP + kb0 + pc * 8);
+                    char * vr = st + NK * KIMG + r * VROW;
+                    *(uint2 *) (vr + LY::v(r, 2 * pc)) = make_uint2(v.x, v.y);
+                    *(uint2 *) (vr + LY::v(r, 2 * pc + 1)) = make_uint2(v.z, v.w);
+                }
+            }
+        }
+    }
+    asm volatile("" :: "v"(qh[0]), "v"(qh[1]), "v"(qh[2]), "v"(qh[3]), "v"(ql[0]), "v"(ql[1]), "v"(ql[2]), "v"(ql[3]));
+    __syncthreads();
+    // group B starts one segment late; A ends with one extra barrier: every wave passes 2 * ntiles + 1 barriers
+    if (grp == 0 && ntiles > 3) load_half(3);   // A stores its half of tile 3 in V(2)
+    if (grp == 1) {
+        if (ntiles > 3) load_half(3);           // B stores its half of tile 3 in V(1)
+        barrier();
+    }
+    for (int t = 0; t < ntiles; ++t) {
+        mfma_seg(t, ntiles);
+        barrier();
+        valu_seg(t, ntiles);
+        // staging: tile t+1 (A) / t+2 (B) goes into the stage of tile t-2 / t-1, whose last reader (B's P.V) has
+        // passed the previous barrier; then the registers load the group's half of the next tile it will store
+        const int ts = grp == 0 ? t + 1 : t + 2;
+        if (t >= (grp == 0 ? 2 : 1) && ts < ntiles && ts >= NST) {
+            store_half(ts);
+            if (ts + 1 < ntiles) load_half(ts + 1);
+        }
+        barrier();
+    }
+    mfma_seg(ntiles, ntiles);   // the last P.V
+    if (grp == 0) barrier();
+
+    const float l_tot = l_run + __shfl_xor(l_run, 32);
+    const float inv = 1.0f / l_tot;
+    const int q = q0 + col;
+    if (q < T) {
+        const int64_t orow = (rowbase + q) * D + h * 64;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d = dt * 32 + 8 * g + 4 * hi;
+                const float v0 = o[dt][4 * g + 0] * inv, v1 = o[dt][4 * g + 1] * inv;
+                const float v2 = o[dt][4 * g + 2] * inv, v3 = o[dt][4 * g + 3] * inv;
+                if (p.outH) {
+                    const half4 hv = {to16<BF>(v0), to16<BF>(v1), to16<BF>(v2), to16<BF>(v3)};
+                    *(half4 *) (p.outH + orow + d) = hv;
+                } else {
+                    *(float4 *) (p.outF + orow + d) = make_float4(v0, v1, v2, v3);
+                }
+            }
+    }
+}
+
 }  // namespace
 
 hipError_t q2a_launch_attention(const q2a_attn_args & a, hipStream_t s) {
     if (a.D != a.H * 64 || a.TP < ((a.T + KT - 1) / KT) * KT) return hipErrorInvalidValue;
     dim3 grid(((a.T + 127) / 128) * a.H * a.n_clips);
+    // bf16 contract: the 8-wave ping-pong kernel (measured 33 -> 30 ms/step at 64 clips; Q2A_ATTN_V1=1 for the 4-wave
+    // one). F32-class contract: the 4-wave kernel — the ping-pong form of its 3-term QK^T ran slower (61 vs 49 ms/step:
+    // one 81 KiB workgroup per CU, barrier waits 46 % of wave cycles; Q2A_ATTN_PP=1 runs it, A/B only)
+    static const bool v1 = [] { const char * v = getenv("Q2A_ATTN_V1"); return v && atoi(v); }();
+    static const bool pp32 = [] { const char * v = getenv("Q2A_ATTN_PP"); return v && atoi(v); }();
+    static const int terms = [] { const char * v = getenv("Q2A_ATTN_TERMS"); return v ? atoi(v) : 3; }();
+    if (!v1 && (a.bf16 || (pp32 && terms == 3))) {
+        const dim3 grid2(((a.T + 255) / 256) * a.H * a.n_clips);
+        if (a.bf16) {
+            if (!a.outH) return hipErrorInvalidValue;
+            hipLaunchKernelGGL(k_attn_pp<true>, grid2, dim3(512), 0, s, a);
+        } else {
+            hipLaunchKernelGGL(k_attn_pp<false>, grid2, dim3(512), 0, s, a);
+        }
+        return hipGetLastError();
+    }
     if (a.bf16) {
         if (!a.outH) return hipErrorInvalidValue;
         hipLaunchKernelGGL(k_attn<true>, grid, dim3(256), 0, s, a);
     } else {
-        static const int terms = [] { const char * v = getenv("Q2A_ATTN_TERMS"); return v ? atoi(v) : 3; }();
         if (terms == 2) hipLaunchKernelGGL((k_attn<false, 2>), grid, dim3(256), 0, s, a);
         else if (terms == 1) hipLaunchKernelGGL((k_attn<false, 1>), grid, dim3(256), 0, s, a);
         else hipLaunchKernelGGL(k_attn<false>, grid, dim3(256), 0, s, a);
