@@ -143,6 +143,19 @@ int q2a_test_block_taps(q2a_engine * e, int layer, float * x_dev, int n_clips, v
 int q2a_test_attention(q2a_engine * e, const float * q_dev, const float * k_dev, const float * v_dev, int n_clips,
                        float * out_dev, void * stream);
 
+/* ---- downstream consumer: the Qwen2-Audio multi-modal projector ------------------------
+ * audio_features = Linear(d_model -> text hidden size, bias)(embd_enc) — transformers' Qwen2AudioMultiModalProjector
+ * (modeling_qwen2_audio.py), the step after the reference's path ends at embd_enc (qwen2-whisper.cpp:2185; the
+ * reference has no projector). Weights: a projector file in the ggml container (multi_modal_projector.linear.weight
+ * [d_out][d_in] F16 / Q4_K / Q8_0 / Q4_0, .bias [d_out] F32; bin/q2a_tool gen-projector + quantize). Numerics: a ggml
+ * MUL_MAT of that weight type (activations per vec_dot_type, exact products, fp32 accumulation) + bias in f32. */
+typedef struct q2a_projector q2a_projector;
+q2a_projector * q2a_projector_open(const char * path, int device);
+void q2a_projector_close(q2a_projector * p);
+int q2a_projector_get_dims(const q2a_projector * p, int * d_in, int * d_out, int * wtype);
+/* y_dev [rows][d_out] f32 = x_dev [rows][d_in] f32 (device) projected; asynchronous on `stream` (NULL = own stream). */
+int q2a_projector_apply(q2a_projector * p, const float * x_dev, int64_t rows, float * y_dev, void * stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1228,4 +1228,137 @@ int q2a_test_attention(q2a_engine * e, const float * q, const float * k, const f
     return Q2A_OK;
 }
 
+// ---- downstream consumer: the Qwen2-Audio multi-modal projector ---------------------------
+// audio_features = Linear(d_model -> text hidden, bias)(embd_enc) (transformers modeling_qwen2_audio.py,
+// Qwen2AudioMultiModalProjector; the reference path ends at embd_enc, qwen2-whisper.cpp:2185). Weights from a projector
+// file in the ggml container (q2a_write_synthetic_projector layout), run with the encoder's numerics contract for a
+// ggml MUL_MAT of that weight type: activations converted per vec_dot_type (fp16 RNE for F16, Q8_K for Q4_K, Q8_0 for
+// Q8_0 / Q4_0), exact products, fp32 accumulation in the canonical K order, then + bias in f32 — on the same GEMM.
+struct q2a_projector {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int d_in = 0, d_out = 0, wtype = 0, blk = 0;
+    void * wdev = nullptr;          // q2a_pack_linear layout
+    uint64_t off[A_COUNT] = {};
+    float * bias = nullptr;
+    void * ws = nullptr;            // A operand [rows][d_in] fp16 | dy [d_in/blk][MP] | aext [d_in/256][MP][16]
+    size_t ws_bytes = 0;
+    const uint16_t * gelu = nullptr;   // the GEMM's table argument (unused by STORE_F, kept valid)
+};
+
+q2a_projector * q2a_projector_open(const char * path, int device) {
+    char err[256] = {0};
+    q2a_model_file * mf = q2a_model_file_read(path, err, sizeof(err));
+    if (!mf) { set_err("projector %s: %s", path ? path : "(null)", err); return nullptr; }
+    const q2a_tensor_desc * wt = q2a_model_file_find(mf, "multi_modal_projector.linear.weight");
+    const q2a_tensor_desc * bt = q2a_model_file_find(mf, "multi_modal_projector.linear.bias");
+    auto fail = [&](int code, const char * msg) -> q2a_projector * {
+        set_err("projector %s: %s", path, msg);
+        q2a_model_file_free(mf);
+        (void) code;
+        return nullptr;
+    };
+    if (!wt || !bt || wt->n_dims != 2 || bt->type != Q2A_TYPE_F32 || bt->ne[0] != wt->ne[1]) return fail(Q2A_ERR_FORMAT, "missing or malformed tensors");
+    const int K = (int) wt->ne[0], N = (int) wt->ne[1];
+    if (N % 128 != 0 || K % 256 != 0) return fail(Q2A_ERR_UNSUPPORTED, "d_out must be a multiple of 128, d_in of 256");
+    std::vector<uint8_t> packed;
+    uint64_t off[A_COUNT];
+    if (q2a_pack_linear(mf->data + wt->offset, wt->type, N, K, packed, off) != Q2A_OK)
+        return fail(Q2A_ERR_UNSUPPORTED, "weight type not supported (F16, Q4_K, Q8_0, Q4_0)");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) { (void) hipGetLastError(); return fail(Q2A_ERR_HIP, "no such HIP device"); }
+    q2a_projector * p = new q2a_projector();
+    p->device = device; p->d_in = K; p->d_out = N; p->wtype = wt->type; p->blk = blk_of(wt->type);
+    for (int i = 0; i < A_COUNT; ++i) p->off[i] = off[i];
+    std::vector<uint16_t> gtab(65536);
+    q2a_make_gelu_table(gtab.data());
+    bool ok = hipSetDevice(device) == hipSuccess && hipStreamCreateWithFlags(&p->stream, hipStreamNonBlocking) == hipSuccess &&
+              hipMalloc(&p->wdev, packed.size()) == hipSuccess && hipMalloc((void **) &p->bias, (size_t) N * 4) == hipSuccess &&
+              hipMalloc((void **) &p->gelu, 65536 * 2) == hipSuccess;
+    ok = ok && hipMemcpy(p->wdev, packed.data(), packed.size(), hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy(p->bias, mf->data + bt->offset, (size_t) N * 4, hipMemcpyHostToDevice) == hipSuccess &&
+         hipMemcpy((void *) p->gelu, gtab.data(), 65536 * 2, hipMemcpyHostToDevice) == hipSuccess;
+    q2a_model_file_free(mf);
+    if (!ok) {
+        (void) hipGetLastError();
+        set_err("projector %s: device allocation / upload failed", path);
+        q2a_projector_close(p);
+        return nullptr;
+    }
+    return p;
+}
+
+void q2a_projector_close(q2a_projector * p) {
+    if (!p) return;
+    (void) hipSetDevice(p->device);
+    if (p->stream) (void) hipStreamSynchronize(p->stream);
+    if (p->wdev) (void) hipFree(p->wdev);
+    if (p->bias) (void) hipFree(p->bias);
+    if (p->gelu) (void) hipFree((void *) p->gelu);
+    if (p->ws) (void) hipFree(p->ws);
+    if (p->stream) (void) hipStreamDestroy(p->stream);
+    delete p;
+}
+
+int q2a_projector_get_dims(const q2a_projector * p, int * d_in, int * d_out, int * wtype) {
+    if (!p) return Q2A_ERR_ARG;
+    if (d_in) *d_in = p->d_in;
+    if (d_out) *d_out = p->d_out;
+    if (wtype) *wtype = p->wtype;
+    return Q2A_OK;
+}
+
+int q2a_projector_apply(q2a_projector * p, const float * x, int64_t rows, float * y, void * stream) {
+    if (!p || !x || !y || rows <= 0 || rows > (1 << 30) / 4) return Q2A_ERR_ARG;
+    HIP_TRY(hipSetDevice(p->device));
+    hipStream_t s = stream ? (hipStream_t) stream : p->stream;
+    const int M = (int) rows, K = p->d_in, N = p->d_out, blk = p->blk;
+    const int64_t MP = (rows + 255) / 256 * 256;
+    const size_t a_bytes = ((size_t) M * K * 2 + 255) & ~size_t(255);
+    const size_t dy_bytes = blk ? ((size_t) (K / blk) * MP * 4 + 255) & ~size_t(255) : 0;
+    const size_t ae_bytes = blk == 256 ? (size_t) (K / 256 + 1) * MP * 32 : 0;
+    const size_t need = a_bytes + dy_bytes + ae_bytes;
+    if (need > p->ws_bytes) {
+        HIP_TRY(hipStreamSynchronize(s));
+        if (p->ws) (void) hipFree(p->ws);
+        p->ws = nullptr; p->ws_bytes = 0;
+        if (hipMalloc(&p->ws, need) != hipSuccess) { (void) hipGetLastError(); set_err("projector workspace of %zu bytes", need); return Q2A_ERR_OOM; }
+        p->ws_bytes = need;
+    }
+    q2a_half * A = (q2a_half *) p->ws;
+    float * dy = (float *) ((char *) p->ws + a_bytes);
+    q2a_half * aext = (q2a_half *) ((char *) p->ws + a_bytes + dy_bytes);
+    if (blk == 0) {
+        const int64_t n = (int64_t) M * K;
+        hipLaunchKernelGGL(k_to_half, dim3((unsigned) ((n + 255) / 256)), dim3(256), 0, s, x, A, n);
+        LAUNCH(hipGetLastError());
+    } else {
+        q2a_quant_args qa{x, nullptr, M, K, blk == 256 ? 1 : 2, A, dy, aext, (int) MP};
+        LAUNCH(q2a_launch_quant_act(qa, s));
+    }
+    q2a_gemm_args a;
+    memset(&a, 0, sizeof(a));
+    const char * w = (const char *) p->wdev;
+    a.A = A; a.lda = K; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
+    a.W = (const q2a_half *) (w + p->off[A_W]); a.ldw = K;
+    a.M = M; a.N = N; a.K = K;
+    a.outF = y; a.ldo = N;
+    a.bias = p->bias; a.store_bias = 1;
+    a.gelu_tab = p->gelu;
+    if (blk) {
+        a.nblk = K / blk;
+        a.dx = (const float *) (w + p->off[A_DX]);
+        a.dy = dy; a.dy_ld = (int) MP;
+        if (blk == 256) {
+            a.dmin = (const float *) (w + p->off[A_DMIN]);
+            a.wext = (const q2a_half *) (w + p->off[A_WEXT]);
+            a.beta = (const float *) (w + p->off[A_BETA]);
+            a.gamma = (const float *) (w + p->off[A_GAMMA]);
+            a.aext = aext;
+        }
+    }
+    LAUNCH(q2a_launch_gemm(a, Q2A_EPI_STORE_F, blk, s));
+    return Q2A_OK;
+}
+
 }  // extern "C"

@@ -442,6 +442,34 @@ extern "C" int q2a_write_synthetic_model(const char * path, const q2a_hparams * 
     return ok ? 0 : -2;
 }
 
+// The Qwen2-Audio multi-modal projector (transformers modeling_qwen2_audio.py Qwen2AudioMultiModalProjector: one
+// nn.Linear(audio d_model, text hidden_size, bias=True) over the encoder's last_hidden_state) in the same ggml container:
+// hparams with n_audio_state = d_in, n_text_state = d_out (every other field 0 but ftype), no filters, no vocab,
+// tensors multi_modal_projector.linear.weight [d_out][d_in] (F16 or F32 by ftype, quantizable by q2a_quantize_model)
+// and multi_modal_projector.linear.bias [d_out] F32. The reference's converter stops at the encoder
+// (qwen2-whisper.cpp:2185 ends the path at embd_enc), so this is the layout a converter of the projector would emit.
+extern "C" int q2a_write_synthetic_projector(const char * path, int d_in, int d_out, int ftype, uint64_t seed) {
+    if (d_in <= 0 || d_out <= 0 || (ftype != 0 && ftype != 1)) return -3;
+    out_file o;
+    o.f = fopen(path, "wb");
+    if (!o.f) return -1;
+    q2a_hparams hp;
+    memset(&hp, 0, sizeof(hp));
+    hp.n_audio_state = d_in;
+    hp.n_text_state = d_out;
+    hp.ftype = ftype;
+    o.i32((int32_t) Q2A_FILE_MAGIC);
+    o.w(&hp, sizeof(hp));
+    o.i32(0);   // n_mel
+    o.i32(0);   // n_fft
+    o.i32(0);   // vocab
+    emit(o, "multi_modal_projector.linear.weight", {d_out, d_in}, true, ftype, seed, 1000, 0.f, 0.02f, 8);
+    emit(o, "multi_modal_projector.linear.bias", {d_out}, false, ftype, seed, 1001, 0.f, 0.02f, 8);
+    const bool ok = o.ok;
+    fclose(o.f);
+    return ok ? 0 : -2;
+}
+
 // ------------------------------------------------------------------------------------------------
 // reader
 // ------------------------------------------------------------------------------------------------

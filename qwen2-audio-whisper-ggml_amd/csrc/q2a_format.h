@@ -68,6 +68,10 @@ void q2a_mel_filters_slaney(float * out, int n_mel, int n_fft, int sample_rate);
 // convert-pt-to-ggml.py:309-321). Returns 0 on success.
 int q2a_write_synthetic_model(const char * path, const q2a_hparams * hp, uint64_t seed, int n_threads);
 
+// Write a synthetic Qwen2-Audio multi-modal projector file (one Linear d_in -> d_out with bias) in the same ggml
+// container (see q2a_format.cpp). ftype 0 = F32 weight, 1 = F16. Returns 0 on success.
+int q2a_write_synthetic_projector(const char * path, int d_in, int d_out, int ftype, uint64_t seed);
+
 // Re-quantize a F16/F32 model file the way whisper.cpp's quantize flow does (examples/common-ggml.cpp:41-244
 // with to_quant {".*"} and skip {"embed_positions.weight","conv1.bias","conv2.bias"}; only 2-D tensors).
 // qtype: Q2A_TYPE_Q4_K / Q2A_TYPE_Q8_0 / Q2A_TYPE_Q4_0. Byte-identical to ggml_quantize_chunk. 0 on success.

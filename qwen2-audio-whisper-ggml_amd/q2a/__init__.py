@@ -19,6 +19,7 @@ EXPORTS = (
     "q2a_last_error", "q2a_open", "q2a_pack_model", "q2a_free_host_blob", "q2a_open_device_blob", "q2a_close",
     "q2a_get_info", "q2a_reserve", "q2a_encode_device", "q2a_encode_host", "q2a_pcm_to_mel",
     "q2a_test_linear", "q2a_test_block", "q2a_test_block_taps", "q2a_test_attention",
+    "q2a_projector_open", "q2a_projector_close", "q2a_projector_get_dims", "q2a_projector_apply",
 )
 
 CLIP_ENCODED, CLIP_SKIPPED = 0, 1
@@ -73,6 +74,11 @@ def lib() -> C.CDLL:
         L.q2a_test_block.argtypes = [vp, C.c_int, vp, C.c_int, vp]
         L.q2a_test_block_taps.argtypes = [vp, C.c_int, vp, C.c_int, C.POINTER(vp), vp]
         L.q2a_test_attention.argtypes = [vp, vp, vp, vp, C.c_int, vp, vp]
+        L.q2a_projector_open.restype = vp
+        L.q2a_projector_open.argtypes = [C.c_char_p, C.c_int]
+        L.q2a_projector_close.argtypes = [vp]
+        L.q2a_projector_get_dims.argtypes = [vp, i32p, i32p, i32p]
+        L.q2a_projector_apply.argtypes = [vp, vp, C.c_int64, vp, vp]
         _lib = L
     return _lib
 
@@ -165,6 +171,34 @@ class Engine:
     def test_attention(self, q_ptr, k_ptr, v_ptr, n_clips, out_ptr, stream=None):
         _check(lib().q2a_test_attention(self.h, C.c_void_p(q_ptr), C.c_void_p(k_ptr), C.c_void_p(v_ptr), n_clips,
                                         C.c_void_p(out_ptr), C.c_void_p(stream) if stream else None))
+
+
+class Projector:
+    """The Qwen2-Audio multi-modal projector (Linear d_model -> text hidden, bias) on the GPU: the consumer of embd_enc
+    (include/q2a_encoder.h, q2a_projector_*). No CPU fallback."""
+
+    def __init__(self, path: str, device: int = 0):
+        self.h = lib().q2a_projector_open(path.encode(), device)
+        if not self.h:
+            raise Q2AError(lib().q2a_last_error().decode())
+        a, b, w = C.c_int32(), C.c_int32(), C.c_int32()
+        _check(lib().q2a_projector_get_dims(self.h, C.byref(a), C.byref(b), C.byref(w)))
+        self.d_in, self.d_out, self.wtype = a.value, b.value, w.value
+
+    def apply(self, x_ptr: int, rows: int, y_ptr: int, stream=None):
+        _check(lib().q2a_projector_apply(self.h, C.c_void_p(x_ptr), rows, C.c_void_p(y_ptr),
+                                         C.c_void_p(stream) if stream else None))
+
+    def close(self):
+        if self.h:
+            lib().q2a_projector_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
 
 
 def pack_model(path: str, act: int = ACT_REFERENCE) -> bytes:

@@ -4,6 +4,7 @@
 //   q2a_tool gen-model OUT {tiny|full|L,D,H,M} {f32|f16} [seed] [threads]
 //   q2a_tool quantize IN OUT {q4_k|q8_0|q4_0} [threads]
 //   q2a_tool synth-clip OUT.f32 N_SAMPLES CLIP_INDEX
+//   q2a_tool gen-projector OUT D_IN D_OUT {f32|f16} [seed]   (Qwen2-Audio multi-modal projector, q2a_format.cpp)
 #include "../csrc/q2a_format.h"
 
 #include <cstdio>
@@ -16,7 +17,8 @@ static int usage() {
     fprintf(stderr,
             "usage:\n  q2a_tool gen-model OUT {tiny|full|L,D,H,M} {f32|f16} [seed] [threads]\n"
             "  q2a_tool quantize IN OUT {q4_k|q8_0|q4_0} [threads]\n"
-            "  q2a_tool synth-clip OUT.f32 N_SAMPLES CLIP_INDEX\n");
+            "  q2a_tool synth-clip OUT.f32 N_SAMPLES CLIP_INDEX\n"
+            "  q2a_tool gen-projector OUT D_IN D_OUT {f32|f16} [seed]\n");
     return 1;
 }
 
@@ -53,6 +55,10 @@ int main(int argc, char ** argv) {
         fwrite(v.data(), 4, v.size(), f);
         fclose(f);
         return 0;
+    }
+    if (cmd == "gen-projector" && argc >= 6) {
+        const uint64_t seed = argc > 6 ? strtoull(argv[6], nullptr, 0) : 0x51A2;
+        return q2a_write_synthetic_projector(argv[2], atoi(argv[3]), atoi(argv[4]), std::string(argv[5]) == "f32" ? 0 : 1, seed);
     }
     return usage();
 }
