@@ -791,7 +791,7 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
             q2a_half * hH = (q2a_half *) e->hF;
             a.outH = hH; a.ldo = d.F; a.o_rpg = M; a.o_gstride = 0; a.o_off = 0;
             PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_PRE_H, e->blk, s));
-            PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_gelu_quant_q8k(hH, M, d.F, e->g<const uint16_t *>(G_GELU_C), e->actF,
+            PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_gelu_quant_q8k(hH, M, d.F, e->g<const uint16_t *>(G_GELU), e->actF,
                                                                    e->dyF, e->aextF, e->dy_ld, s));
         } else {
             // GELU output is exactly fp16-valued (LUT): keep it as fp16, then quantize for fc2

@@ -314,42 +314,115 @@ __global__ __launch_bounds__(256) void k_quant_q8k_h16(const q2a_half * __restri
     quant_q8k_row16(v, sub, outH + blk * 256 + sub * 16, dy + (int64_t) bf * ld + m, aext + ((int64_t) bf * ld + m) * 16);
 }
 
-// GELU + Q8_K of the fc1 pre-activation (Q2A_EPI_PRE_H output): persistent workgroups of 16 waves each stage the
-// 80 KiB compact GELU table into LDS once, then quantize 4 blocks per wave per iteration like k_quant_q8k_h16.
-// Per element: -inf (x <= -10) -> 0; h >= 10 -> h; else lut[h] (the table's own value at 10.0 is 10.0), which is
-// gelu_lut_c16(x) of the fused epilogue for every x.
-constexpr int GQ_THREADS = 1024;
-__global__ __launch_bounds__(GQ_THREADS) void k_gelu_quant_q8k_h16(const q2a_half * __restrict__ X, int64_t nblocks, int bpr,
-                                                                   const uint16_t * __restrict__ gelu_c, q2a_half * outH,
+// GELU + Q8_K of the fc1 pre-activation (Q2A_EPI_PRE_H output; fp16, x <= -10 marked -inf). Persistent workgroups
+// of 8 waves stage ggml's whole 64 Ki-entry fp16 GELU table (128 KiB) into LDS once, so an element is one lookup at
+// its own bits: entries for h >= 10 are h itself (ggml_vec_gelu_f32's x >= 10 branch: tanhf saturates to 1), and the
+// -inf marker's entry is patched to ggml's +0 for x <= -10. The kernel is VALU-bound once its stores are whole
+// sectors (~19 -> ~13 VALU per element with the direct index).
+//
+// Work unit = one block column bf of 16 consecutive rows, four wave-iterations of 4 rows (16 lanes per 256-block,
+// 16 values per lane): every side store is whole sectors — the bsum operand 128 B (4 rows x 32 B) per iteration, d
+// 64 B (16 rows) per unit. Scattered 4-B d / 32-B bsum stores (one block per lane group) went to HBM as single
+// partial writes: 25 % of the kernel (diag/bwbench.hip). Input: the 2 KiB of an iteration arrive by LDS-DMA one
+// iteration ahead (register prefetch cannot run ahead: vmcnt retires in order and counts the stores, and with loads
+// and stores pending the compiler waits vmcnt(0), i.e. for the previous iteration's stores). Per iteration 2 DMA +
+// 3 stores (+1 for d on the unit's last iteration).
+constexpr int GQ_THREADS = 512;
+constexpr int GQ_WAVES = GQ_THREADS / 64;
+typedef __attribute__((address_space(3))) void * lds_vptr_t;
+__global__ __launch_bounds__(GQ_THREADS) void k_gelu_quant_q8k_h16(const q2a_half * __restrict__ X, int M, int bpr,
+                                                                   const uint16_t * __restrict__ gelu_tab, q2a_half * outH,
                                                                    float * dy, q2a_half * aext, int ld) {
-    __shared__ __attribute__((aligned(16))) uint16_t lut[Q2A_GELU_C_BYTES / 2];
-    for (int i = threadIdx.x; i < Q2A_GELU_C_BYTES / 16; i += GQ_THREADS)
-        ((uint4 *) lut)[i] = ((const uint4 *) gelu_c)[i];
+    __shared__ __attribute__((aligned(16))) uint16_t lut[65536];
+    __shared__ __attribute__((aligned(16))) char stage[GQ_WAVES][2048];
+    for (int i = threadIdx.x; i < 65536 / 8; i += GQ_THREADS) ((uint4 *) lut)[i] = ((const uint4 *) gelu_tab)[i];
     __syncthreads();
-    const int lane = threadIdx.x & 63, sub = lane & 15;
-    const int64_t waves = (int64_t) gridDim.x * (GQ_THREADS / 64);
+    if (threadIdx.x == 0) lut[0xFC00] = 0;   // -inf marker (x <= -10) -> +0
+    __syncthreads();
+    const int lane = threadIdx.x & 63, sub = lane & 15, grp = lane >> 4;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t K = (int64_t) bpr * 256;
+    const int64_t nunits = (int64_t) ((M + 15) / 16) * bpr;
+    const int64_t stride = (int64_t) gridDim.x * GQ_WAVES;
+    auto unit_of = [&](int64_t t) -> int64_t { return (int64_t) blockIdx.x * GQ_WAVES + wave + (t >> 2) * stride; };
+    // rows r0 .. r0 + 3 of block column bf for iteration t (wave-uniform)
+    auto place = [&](int64_t t, int & r0, int & bf) {
+        const int64_t U = min(unit_of(t), nunits - 1);
+        const int c = (int) (U / bpr);
+        bf = (int) (U - (int64_t) c * bpr);
+        r0 = c * 16 + (int) (t & 3) * 4;
+    };
+    char * st = &stage[wave][0];
+    // 2 x 1 KiB pieces: piece i = rows r0 + 2i (lanes 0-31) and r0 + 2i + 1 (lanes 32-63), 16 B per lane
+    auto dma = [&](int64_t t) {
+        int r0, bf;
+        place(t, r0, bf);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int row = min(r0 + 2 * i + (lane >> 5), M - 1);   // past the end: harmless re-loads keep the counts
+            __builtin_amdgcn_global_load_lds((const void *) (X + row * K + bf * 256 + (lane & 31) * 8), (lds_vptr_t) (st + i * 1024),
+                                             16, 0, 0);
+        }
+    };
+    const uint32_t st0 = (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) char *) st;
+    const uint32_t lut0 = (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) char *) lut;
     typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
-    for (int64_t wg4 = (int64_t) blockIdx.x * (GQ_THREADS / 64) + (threadIdx.x >> 6); wg4 * 4 < nblocks; wg4 += waves) {
-        const int64_t blk = wg4 * 4 + (lane >> 4);
-        if (blk >= nblocks) continue;
-        const int64_t m = blk / bpr;
-        const int bf = (int) (blk - m * bpr);
-        const h8_t * src = (const h8_t *) (X + blk * 256 + sub * 16);
-        const h8_t h0 = __builtin_nontemporal_load(src), h1 = __builtin_nontemporal_load(src + 1);
+    typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+    if (unit_of(0) < nunits) dma(0);
+    bool wait_all = true;
+    float dd = 0.f;   // lane L (0..15): d of row 16c + L, filled over the unit's four iterations
+    for (int64_t t = 0; unit_of(t) < nunits; ++t) {
+        // this iteration's DMA; the previous iteration's 3 or 4 stores may still be out (all of them after a ragged one)
+        if (wait_all) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        // lane (grp, sub): values 16 sub .. 16 sub + 15 of row r0 + grp
+        h8_t h0, h1;
+        const uint32_t a = st0 + (uint32_t) (grp * 512 + sub * 32);
+        asm volatile("ds_read_b128 %0, %1" : "=v"(h0) : "v"(a));
+        asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(h1) : "v"(a));
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(h0), "+v"(h1) :: "memory");
+        dma(t + 1);                                          // the buffer's next fill (its data is in registers)
+        int r0, bf;
+        place(t, r0, bf);
+        wait_all = r0 + 4 > M;
+        // 16 table reads back to back behind one wait (a compiler-visible lookup is placed per element with its own
+        // wait); the index is the element's own bits
+        uint32_t g[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            const _Float16 he = e < 8 ? h0[e] : h1[e - 8];
+            uint16_t u;
+            __builtin_memcpy(&u, &he, 2);
+            asm volatile("ds_read_u16 %0, %1" : "=v"(g[e]) : "v"(lut0 + (uint32_t) u * 2));
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(g[0]), "+v"(g[1]), "+v"(g[2]), "+v"(g[3]), "+v"(g[4]), "+v"(g[5]), "+v"(g[6]),
+                     "+v"(g[7]), "+v"(g[8]), "+v"(g[9]), "+v"(g[10]), "+v"(g[11]), "+v"(g[12]), "+v"(g[13]), "+v"(g[14]), "+v"(g[15]));
         float v[16];
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
-            const _Float16 h = e < 8 ? h0[e] : h1[e - 8];
-            uint16_t u;
-            __builtin_memcpy(&u, &h, 2);
-            const uint16_t g = lut[(u & 0x7FFF) + ((u & 0x8000) ? Q2A_GELU_C_HALF : 0)];
+            const uint16_t gg = (uint16_t) g[e];
             _Float16 gh;
-            __builtin_memcpy(&gh, &g, 2);
-            const float x = (float) h;
-            v[e] = u == 0xFC00 ? 0.0f : x >= 10.0f ? x : (float) gh;
+            __builtin_memcpy(&gh, &gg, 2);
+            v[e] = (float) gh;
         }
-        quant_q8k_row16(v, sub, outH + blk * 256 + sub * 16, dy + (int64_t) bf * ld + m, aext + ((int64_t) bf * ld + m) * 16);
+        const int row = r0 + grp;
+        float d;
+        int sb;
+        quant_q8k_row16c(v, sub, outH + row * K + bf * 256 + sub * 16, row < M, d, sb);
+        if ((sub & 1) == 0 && row < M) {   // bsum32 of sub-block sub / 2 as (hi, lo): rows r0 .. r0 + 3 = 128 B
+            const int hi = (sb >= 0) ? (sb >> 6) : -((-sb + 63) >> 6);   // floor(s / 64)
+            const int lo = sb - 64 * hi;
+            *(h2_t *) (aext + ((int64_t) bf * ld + row) * 16 + sub) = h2_t{(_Float16) (float) hi, (_Float16) (float) lo};
+        }
+        const int q = (int) (t & 3);
+        const float dq = __shfl(d, (lane & 3) * 16);         // d of row r0 + (lane & 3)
+        if ((lane >> 2) == q) dd = dq;
+        if (q == 3) {   // d of the unit's 16 rows: one 64-B store
+            const int r = r0 - 12 + lane;
+            if (lane < 16 && r < M) dy[(int64_t) bf * ld + r] = dd;
+        }
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the trailing re-load lands before the workgroup's LDS is freed
 }
 
 // AvgPool1d(k=2,s=2) over time (ggml.c:15077-15125: drow = 0; += a; += b; /= 2) + final LayerNorm -> f32
@@ -448,16 +521,15 @@ hipError_t q2a_launch_layernorm(const q2a_ln_args & a, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t q2a_launch_gelu_quant_q8k(const q2a_half * XH, int M, int K, const uint16_t * gelu_c, q2a_half * outH,
+hipError_t q2a_launch_gelu_quant_q8k(const q2a_half * XH, int M, int K, const uint16_t * gelu_tab, q2a_half * outH,
                                      float * dy, q2a_half * aext, int dy_ld, hipStream_t s) {
-    if (K % 256 != 0 || M <= 0) return hipErrorInvalidValue;
+    if (K % 256 != 0 || M <= 0 || (int64_t) M * K >= ((int64_t) 1 << 31)) return hipErrorInvalidValue;
     int dev = 0, ncu = 256;
     (void) hipGetDevice(&dev);
     (void) hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    const int64_t nb = (int64_t) M * (K / 256);
-    const int64_t need = (nb + 4 * (GQ_THREADS / 64) - 1) / (4 * (GQ_THREADS / 64));
-    const unsigned grid = (unsigned) std::min<int64_t>(need, 2 * (int64_t) ncu);   // two 80 KiB tables per CU
-    hipLaunchKernelGGL(k_gelu_quant_q8k_h16, dim3(grid), dim3(GQ_THREADS), 0, s, XH, nb, K / 256, gelu_c, outH, dy, aext, dy_ld);
+    const int64_t units = (int64_t) ((M + 15) / 16) * (K / 256);
+    const unsigned grid = (unsigned) std::min<int64_t>((units + GQ_WAVES - 1) / GQ_WAVES, (int64_t) ncu);   // 144 KiB each
+    hipLaunchKernelGGL(k_gelu_quant_q8k_h16, dim3(grid), dim3(GQ_THREADS), 0, s, XH, M, K / 256, gelu_tab, outH, dy, aext, dy_ld);
     return hipGetLastError();
 }
 

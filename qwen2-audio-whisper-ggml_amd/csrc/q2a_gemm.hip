@@ -86,6 +86,32 @@ __device__ __forceinline__ _Float16 gelu_lut_c16(float x, const uint16_t * lut) 
     return x <= -10.0f ? (_Float16) 0.0f : x >= 10.0f ? h : gh;
 }
 
+// 8 lookups of gelu_lut_c16 issued back to back behind ONE wait. A compiler-visible lookup is sunk into the branch of
+// the |x| >= 10 select, each followed by its own lgkmcnt(0): 8 dependent LDS round trips instead of one. The index is
+// clamped into the table so the read is unconditional (the select discards it outside |x| < 10).
+__device__ __forceinline__ void gelu_c16_x8(const float (&x)[8], _Float16 (&y)[8], const uint16_t * lut) {
+    const uint32_t lut0 = (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) uint16_t *) lut;
+    uint32_t g[8];
+    _Float16 h[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        h[e] = (_Float16) x[e];
+        uint16_t u;
+        __builtin_memcpy(&u, &h[e], 2);
+        const uint32_t idx = min((uint32_t) (u & 0x7FFF), (uint32_t) (Q2A_GELU_C_HALF - 1)) + ((u & 0x8000) ? Q2A_GELU_C_HALF : 0);
+        asm volatile("ds_read_u16 %0, %1" : "=v"(g[e]) : "v"(lut0 + idx * 2) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(g[0]), "+v"(g[1]), "+v"(g[2]), "+v"(g[3]), "+v"(g[4]), "+v"(g[5]), "+v"(g[6]),
+                 "+v"(g[7]) :: "memory");
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const uint16_t gg = (uint16_t) g[e];
+        _Float16 gh;
+        __builtin_memcpy(&gh, &gg, 2);
+        y[e] = x[e] <= -10.0f ? (_Float16) 0.0f : x[e] >= 10.0f ? h[e] : gh;
+    }
+}
+
 __device__ __forceinline__ float gelu_lut_c(float x, const uint16_t * lut) {
     if (x <= -10.0f) return 0.0f;
     if (x >= 10.0f) return x;
@@ -758,11 +784,20 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
 #pragma unroll
                 for (int i = 0; i < MI; ++i)
 #pragma unroll
-                    for (int j = 0; j < NJ; ++j) {
-                        h4_t hv;
+                    for (int j = 0; j < NJ; j += 2) {
+                        float xs[8];
+                        _Float16 ys[8];
 #pragma unroll
-                        for (int r = 0; r < 4; ++r) hv[r] = gelu_lut_c16(acc[i][j][r] + bias4[j][r], lut);
-                        *(h4_t *) (tl + (i * 16 + (lane & 15)) * RSH + wn * 64 + j * 16 + (lane >> 4) * 4) = hv;
+                        for (int r = 0; r < 4; ++r) {
+                            xs[r] = acc[i][j][r] + bias4[j][r];
+                            xs[4 + r] = acc[i][j + 1][r] + bias4[j + 1][r];
+                        }
+                        gelu_c16_x8(xs, ys, lut);
+#pragma unroll
+                        for (int jj = 0; jj < 2; ++jj) {
+                            const h4_t hv = {ys[4 * jj], ys[4 * jj + 1], ys[4 * jj + 2], ys[4 * jj + 3]};
+                            *(h4_t *) (tl + (i * 16 + (lane & 15)) * RSH + wn * 64 + (j + jj) * 16 + (lane >> 4) * 4) = hv;
+                        }
                     }
             }
             __syncthreads();
@@ -925,15 +960,28 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
 #pragma unroll
             for (int jp = 0; jp < NJ / 2; ++jp) {
                 h4v ha, hb, la, lb;
+                if constexpr (EPI == Q2A_EPI_GELU_H && LUT_EPI) {
+                    float xs[8];
+                    _Float16 ys[8];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    if (EPI == Q2A_EPI_GELU_H && LUT_EPI) {
-                        ha[r] = gelu_lut_c16(acc[i][2 * jp][r] + bias4[2 * jp][r], lut);
-                        hb[r] = gelu_lut_c16(acc[i][2 * jp + 1][r] + bias4[2 * jp + 1][r], lut);
+                    for (int r = 0; r < 4; ++r) {
+                        xs[r] = acc[i][2 * jp][r] + bias4[2 * jp][r];
+                        xs[4 + r] = acc[i][2 * jp + 1][r] + bias4[2 * jp + 1][r];
+                    }
+                    gelu_c16_x8(xs, ys, lut);
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        ha[r] = ys[r];
+                        hb[r] = ys[4 + r];
                         if (BF) {   // the fp16 GELU value handed on as bf16
                             ha[r] = to16<true>((float) ha[r]);
                             hb[r] = to16<true>((float) hb[r]);
                         }
+                    }
+                }
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    if (EPI == Q2A_EPI_GELU_H && LUT_EPI) {
                     } else if (EPI == Q2A_EPI_PRE_H) {   // pre-activation; x <= -10 marked -inf (GELU = 0)
                         const float va = val(i, 2 * jp, r), vb = val(i, 2 * jp + 1, r);
                         ha[r] = va <= -10.0f ? (_Float16) -INFINITY : (_Float16) va;
@@ -975,6 +1023,83 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
             if (m >= p.M) continue;
 #pragma unroll
             for (int j = 0; j < NJ; ++j) *(f4 *) (pb + (int64_t) m * p.N + cbase + j * 16 + 4 * q) = acc[i][j];
+        }
+    } else if constexpr (EPI == Q2A_EPI_RESID && PIPE) {
+        static_assert(MI == 8 && NJ == 4 && NW == 8, "8-phase residual epilogue layout");
+        // residual add, 8-phase tile: every load is consumed before the first store. vmcnt retires in order and
+        // counts stores, and with loads and stores both pending the compiler waits vmcnt(0): a residual load between
+        // the stores of two row blocks waits for the earlier stores to land, eight store round trips per wave.
+        //   1. rows 0..63 of the wave's 128 by glds into the idle operand images (16 KiB per wave, 16-B granules
+        //      XOR-swizzled by row: the column-chunk reads are conflict-free); one wait
+        //   2. their results (acc + bias) + x back into the same LDS slots: acc rows 0..63 are dead
+        //   3. rows 64..127 by register loads into the freed registers; one wait
+        //   4. stores: rows 64..127 from registers, then rows 0..63 from LDS (integer-address LDS reads, opaque to the
+        //      compiler: no vmcnt guard for the glds target behind the stores)
+        const float * rsrc = p.resid ? p.resid : p.outF;
+        char * rl = lds_raw + wave * (64 * 256);
+#pragma unroll
+        for (int t = 0; t < 16; ++t) {
+            const int lr = 4 * t + (lane >> 4), ch = (lane & 15) ^ (lr & 15);
+            const int m = min(rbase + lr, p.M - 1);
+            __builtin_amdgcn_global_load_lds((const void *) (rsrc + (int64_t) m * p.ldo + cbase + ch * 4),
+                                             (lds_ptr_t) (rl + t * 1024), 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("" : "+v"(bias4[0]), "+v"(bias4[1]), "+v"(bias4[2]), "+v"(bias4[3]));
+        const uint32_t rl0 = (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) char *) rl;
+        auto slot = [&](int i, int j) -> uint32_t {
+            return rl0 + (uint32_t) (i * 16 + l16) * 256 + ((uint32_t) ((4 * j + q) ^ l16) << 4);
+        };
+#pragma unroll
+        for (int i = 0; i < MI / 2; ++i) {
+            f4 add[NJ];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) asm volatile("ds_read_b128 %0, %1" : "=v"(add[j]) : "v"(slot(i, j)));
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(add[0]), "+v"(add[1]), "+v"(add[2]), "+v"(add[3]));
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                f4 v;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = val(i, j, r) + add[j][r];   // (acc + bias) + x
+                asm volatile("ds_write_b128 %0, %1" :: "v"(slot(i, j)), "v"(v) : "memory");
+            }
+        }
+        f4 add_hi[MI / 2][NJ];
+#pragma unroll
+        for (int i = MI / 2; i < MI; ++i) {
+            const int m = min(rbase + i * 16 + l16, p.M - 1);
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) add_hi[i - MI / 2][j] = *(const f4 *) (rsrc + (int64_t) m * p.ldo + cbase + 16 * j + 4 * q);
+        }
+#pragma unroll
+        for (int i = 0; i < MI / 2; ++i)
+            asm volatile("" : "+v"(add_hi[i][0]), "+v"(add_hi[i][1]), "+v"(add_hi[i][2]), "+v"(add_hi[i][3]));
+#pragma unroll
+        for (int i = MI / 2; i < MI; ++i) {
+            const int m = rbase + i * 16 + l16;
+            if (m >= p.M) continue;
+            float * orow = p.outF + (int64_t) m * p.ldo + cbase + 4 * q;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) {
+                f4 v;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = val(i, j, r) + add_hi[i - MI / 2][j][r];
+                if (Q2A_ST) q2a_st(v, (f4 *) (orow + 16 * j));
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS result writes (in-order per wave anyway)
+#pragma unroll
+        for (int i = 0; i < MI / 2; ++i) {
+            const int m = rbase + i * 16 + l16;
+            f4 v[NJ];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) asm volatile("ds_read_b128 %0, %1" : "=v"(v[j]) : "v"(slot(i, j)));
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
+            if (m >= p.M) continue;
+            float * orow = p.outF + (int64_t) m * p.ldo + cbase + 4 * q;
+#pragma unroll
+            for (int j = 0; j < NJ; ++j)
+                if (Q2A_ST) q2a_st(v[j], (f4 *) (orow + 16 * j));
         }
     } else {
         // f32 outputs: residual add (O-proj, fc2), GELU (+ positional rows for conv2), plain store

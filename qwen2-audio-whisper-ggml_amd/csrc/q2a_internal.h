@@ -163,9 +163,9 @@ struct q2a_quant_args {
     int dy_ld;
 };
 hipError_t q2a_launch_quant_act(const q2a_quant_args & a, hipStream_t s);
-// GELU (compact fp16 LUT image gelu_c, staged in LDS) of an fp16 pre-activation written by Q2A_EPI_PRE_H, then Q8_K
-// quantization — the same codes as Q2A_EPI_GELU_H + q2a_launch_quant_act(mode 1, XH). XH [M][K], K % 256 == 0.
-hipError_t q2a_launch_gelu_quant_q8k(const q2a_half * XH, int M, int K, const uint16_t * gelu_c, q2a_half * outH,
+// GELU (ggml's fp16 table gelu_tab, 64 Ki entries, staged in LDS) of an fp16 pre-activation written by Q2A_EPI_PRE_H,
+// then Q8_K quantization — the same codes as Q2A_EPI_GELU_H + q2a_launch_quant_act(mode 1, XH). XH [M][K], K % 256 == 0.
+hipError_t q2a_launch_gelu_quant_q8k(const q2a_half * XH, int M, int K, const uint16_t * gelu_tab, q2a_half * outH,
                                      float * dy, q2a_half * aext, int dy_ld, hipStream_t s);
 
 // One ggml weight matrix [N][K] (raw ggml rows, host memory; F16 / Q4_K / Q8_0 / Q4_0) packed into the GEMM's

@@ -72,40 +72,62 @@ __device__ __forceinline__ int swz_xor_i(int v, int o) {
 }
 __device__ __forceinline__ float swz_xor_f(float v, int o) { return __int_as_float(swz_xor_i(__float_as_int(v), o)); }
 
-__device__ __forceinline__ void quant_q8k_row16(const float (&v)[16], int sub, q2a_half * codes, float * dy_out,
-                                                q2a_half * aext) {
-    float amax = fabsf(v[0]);
+// the arithmetic of quant_q8k_row16 with this lane's 16 codes stored (when st) and the block's d and this lane
+// PAIR's bsum32 (sub-block sub / 2) returned instead of stored
+__device__ __forceinline__ void quant_q8k_row16c(const float (&v)[16], int sub, q2a_half * codes, bool st, float & d_out,
+                                                 int & s_out) {
+    // this lane's first element of largest |x| (a backward scan keeps the earliest on ties), then the block max
+    float lm = v[15];
 #pragma unroll
-    for (int e = 1; e < 16; ++e) amax = fmaxf(amax, fabsf(v[e]));
+    for (int e = 14; e >= 0; --e) lm = fabsf(v[e]) >= fabsf(lm) ? v[e] : lm;
+    float amax = fabsf(lm);
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) amax = fmaxf(amax, swz_xor_f(amax, o));
-    float lf = 0.f;
-    bool has = false;
-#pragma unroll
-    for (int e = 15; e >= 0; --e)
-        if (fabsf(v[e]) == amax) { lf = v[e]; has = true; }
     const int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    const float mx = first_max_value(amax, lf, has, lane, 16);
-    int q[16];
+    const float mx = first_max_value(amax, lm, fabsf(lm) == amax, lane, 16);
+    // codes as floats: rint(iscale x) is the reference's MIN(127, nearest_int(.)) value — the MIN never binds:
+    // |x| <= |mx| and |iscale| <= (127/|mx|)(1 + 2^-24), so |iscale x| < 127.5. The bsum of 16 codes (|s| <= 2032) is
+    // exact in f32. Products two per v_pk_mul_f32.
+    typedef float f2_t __attribute__((ext_vector_type(2)));
+    float q[16];
     float d = 1.f;   // all-zero block: see quant_q8k_block
     if (amax != 0.f) {
         const float iscale = -127.f / mx;
+        const f2_t is2 = {iscale, iscale};
 #pragma unroll
-        for (int e = 0; e < 16; ++e) q[e] = min(127, (int) rintf(iscale * v[e]));
+        for (int e = 0; e < 16; e += 2) {
+            const f2_t y = is2 * f2_t{v[e], v[e + 1]};
+            q[e] = rintf(y[0]);
+            q[e + 1] = rintf(y[1]);
+        }
         d = 1 / iscale;
     } else {
 #pragma unroll
-        for (int e = 0; e < 16; ++e) q[e] = 0;
+        for (int e = 0; e < 16; ++e) q[e] = 0.f;
     }
     typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
     h8_t c0, c1;
-    int s = 0;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) { c0[e] = (_Float16) (float) q[e]; c1[e] = (_Float16) (float) q[8 + e]; s += q[e] + q[8 + e]; }
-    *(h8_t *) codes = c0;
-    *(h8_t *) (codes + 8) = c1;
-    if (sub == 0) *dy_out = d;
+    for (int e = 0; e < 8; ++e) { c0[e] = (_Float16) q[e]; c1[e] = (_Float16) q[8 + e]; }
+    if (st) {
+        *(h8_t *) codes = c0;
+        *(h8_t *) (codes + 8) = c1;
+    }
+    f2_t s2 = {0.f, 0.f};
+#pragma unroll
+    for (int e = 0; e < 16; e += 2) s2 = s2 + f2_t{q[e], q[e + 1]};
+    int s = (int) (s2[0] + s2[1]);
     s += swz_xor_i(s, 1);                                     // bsum32 of sub-block j = sub / 2
+    d_out = d;
+    s_out = s;
+}
+
+__device__ __forceinline__ void quant_q8k_row16(const float (&v)[16], int sub, q2a_half * codes, float * dy_out,
+                                                q2a_half * aext) {
+    float d;
+    int s;
+    quant_q8k_row16c(v, sub, codes, true, d, s);
+    if (sub == 0) *dy_out = d;
     if ((sub & 1) == 0) {
         const int hi = (s >= 0) ? (s >> 6) : -((-s + 63) >> 6);   // floor(s / 64)
         const int lo = s - 64 * hi;
