@@ -64,7 +64,7 @@ constexpr float L2E = 1.4426950408889634f;   // exp(x) = exp2(x * log2 e)
 // Q2A_ATTN_TERMS, diag only)
 template <bool BF, int QT = 3>
 __global__ __launch_bounds__(256, BF ? 3 : Q2A_ATTN_F32_OCC) void k_attn(const q2a_attn_args p) {
-    typedef attn_lds<BF> LY;
+    typedef attn_lds<BF || Q2A_ATTN_F32_OCC >= 3> LY;
     constexpr int KROW = LY::KROW, VROW = LY::VROW;
     constexpr int KIMG = KT * KROW, VIMG = 64 * VROW, STAGE = 2 * KIMG + VIMG;
     __shared__ __attribute__((aligned(16))) char lds[2 * STAGE];

@@ -231,7 +231,7 @@ void expand_rows(const uint8_t * src, int wtype, int K, int Ntot, int r0, int r1
                 dx[(size_t) b * Ntot + n] = deff;
                 dm[(size_t) b * Ntot + n] = q2a_fp16_to_fp32(x->dmin);
                 be[(size_t) b * Ntot + n] = dprev / deff;
-                ga[(size_t) b * Ntot + n] = q2a_fp16_to_fp32(x->dmin) / deff;
+                ga[(size_t) b * Ntot + n] = -(q2a_fp16_to_fp32(x->dmin) / deff);   // negated: the kernels' fma addend
                 dprev = deff;
                 for (int j = 0; j < 8; ++j) {
                     uint8_t sc, m;

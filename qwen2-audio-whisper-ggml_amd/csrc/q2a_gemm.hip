@@ -126,14 +126,15 @@ __device__ __forceinline__ float gelu_lut_c(float x, const uint16_t * lut) {
 
 // Q4_K block-ratio accumulation (every Q4_K kernel, 8-phase and small-tile, runs exactly these float operations in
 // the same order, so a clip's outputs do not depend on the tile regime its batch size selects):
-//   block start  acc <- fma(acc, alpha[m] * beta[n], -(gamma[n] * S2[m][n]))
+//   block start  acc <- fma(acc, alpha[m] * beta[n], ngamma[n] * S2[m][n])   (ngamma = -dmin/dx, stored negated:
+//                the product's sign flip is exact, and no per-element negation is issued)
 //   block body   acc += the block's MFMAs (exact integer products, K order fixed by the 64-deep K-steps)
 //   after last   acc * (dy_last[m] * dx_last[n])
-__device__ __forceinline__ float kq_rescale(float a, float al, float be, float ga, float s2) {
+__device__ __forceinline__ float kq_rescale(float a, float al, float be, float nga, float s2) {
 #pragma clang fp contract(off)
     const float t = al * be;
-    const float u = ga * s2;
-    return __builtin_fmaf(a, t, -u);
+    const float u = nga * s2;
+    return __builtin_fmaf(a, t, u);
 }
 __device__ __forceinline__ float kq_final(float a, float yc, float dx) {
 #pragma clang fp contract(off)
@@ -260,14 +261,14 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (sbuf + (wave * 3 + u) * 1024), 16, 0, 0);
         }
     };
-    // start of block kb: acc <- acc * alpha[m] * beta[n] - gamma[n] * S2[m][n]
+    // start of block kb: acc <- acc * alpha[m] * beta[n] + ngamma[n] * S2[m][n]
     // LDS reads below go through integer AS3 addresses (no IR link to the glds destination array): hipcc would
     // otherwise guard each read of the scale buffer with a vmcnt(0) that drains the whole pipeline
     typedef const __attribute__((address_space(3))) float * lds_fp;
     typedef const __attribute__((address_space(3))) f4 * lds_f4p;
     const uint32_t lds0 = (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) char *) lds_raw;
     const uint32_t sb0 = lds0 + SBUF_OFF;
-    // start of block kb: acc <- acc * alpha[m] * beta[n] - gamma[n] * S2[m][n]. The scale-buffer reads are inline
+    // start of block kb: acc <- acc * alpha[m] * beta[n] + ngamma[n] * S2[m][n]. The scale-buffer reads are inline
     // asm with an explicit lgkmcnt wait tied to their results: a compiler-visible LDS read of this array gets a
     // vmcnt(0) guard against the in-flight glds that would drain the whole pipeline once per block.
     // alpha for this wave's 32 rows of the tile into the alpha array (the block's scales must be resident)
@@ -314,7 +315,13 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             }
             f4 s2v[4];   // the four min-term MFMAs first, their latency under the first rescale products
 #pragma unroll
-            for (int j = 0; j < 4; ++j) s2v[j] = __builtin_amdgcn_mfma_f32_16x16x16f16(we[j], ae[c], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            for (int j = 0; j < 4; ++j) {
+#ifdef Q2A_DIAG_NO_MINTERM   // timing diagnostic only (wrong results): the min-term operands stand in for its MFMA
+                s2v[j] = f4{(float) we[j][0], (float) we[j][1], (float) ae[c][0], (float) ae[c][1]};
+#else
+                s2v[j] = __builtin_amdgcn_mfma_f32_16x16x16f16(we[j], ae[c], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#endif
+            }
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll

@@ -58,7 +58,7 @@ struct q2a_gemm_args {
     const q2a_half * aext;            // [nblk][dy_ld][16] bsum hi/lo pairs (Q4_K only)
     const q2a_half * wext;            // [nblk][N][16] (64*m_j, m_j) pairs (Q4_K only)
     const float * beta;               // [nblk][N] dx_{b-1}/dx_b  (Q4_K 8-phase path: block-ratio rescaling)
-    const float * gamma;              // [nblk][N] dmin_b/dx_b
+    const float * gamma;              // [nblk][N] -(dmin_b/dx_b), negated so the recurrence's addend is gamma * S2
     float * qdy;                      // Q2A_EPI_GELU_Q8K outputs: block-major d [N/256][dy_ld] and
     q2a_half * qaext;                 //   bsum operand [N/256][dy_ld][16] of the produced activation
     int nblk;
