@@ -474,7 +474,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     constexpr bool LUT_EPI = PIPE && (EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_GELU_F || EPI == Q2A_EPI_CONV2 ||
                                       EPI == Q2A_EPI_GELU_Q8K);
     constexpr int EPI_OFF = LUT_EPI ? Q2A_GELU_C_BYTES : 0;
-    constexpr int EPI_WREG = 2 * 32 * (BN / WN + 8) * 2;
+    // per-wave epilogue staging: V^T [64 d][WR + 4 t] fp16 (QKV); the other epilogues keep their 32-row budget
+    constexpr int EPI_WREG = EPI == Q2A_EPI_QKV ? 64 * (BM / WM + 4) * 2 : 2 * 32 * (BN / WN + 8) * 2;
     // small-tile kernels: NS operand stages (NS - 1 K-steps of loads in flight, counted vmcnt, raw barriers) within
     // ~150 KiB of LDS. Q4_K: block b+1's scales arrive by glds in 1 KiB pieces (SBP per block, one per wave on the
     // first SP K-steps of block b) into the other of two buffers, plus one pad piece per wave for the dummy pieces
@@ -926,36 +927,39 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     };
     const int pcol = 16 * (q & 1) + 8 * (q >> 1);    // column of this lane's 16-B piece within a 32-column pair
     if (EPI == Q2A_EPI_QKV && part == 2) {
-        // V^T [clip][head][d][TP]: per 32-row pass, stage [col][row] fp16 in LDS, then 8 B (4 t) per lane
-        constexpr int PR = 32;
-        constexpr int WREG = 2 * PR * (WC + 8) * 2;
-        static_assert(WREG == EPI_WREG, "epilogue staging layout");
-        char * wl = lds_raw + EPI_OFF + wave * WREG;
-        __syncthreads();
-#pragma unroll
-        for (int ps = 0; ps < WR / PR; ++ps) {
-#pragma unroll
-            for (int ii = 0; ii < PR / 16; ++ii)
-#pragma unroll
+      if constexpr (EPI == Q2A_EPI_QKV) {
+            // V^T [clip][head][d][TP]: the wave's WR rows (t) of its 64 columns (d, one head) staged [d][t] in its own LDS
+            // region, then stored two d-rows per instruction, 32 lanes x 8 B (4 t) = 256 contiguous bytes per row. (Per
+            // 32-row pass with one lane per d-row, every store instruction touched 64 rows of 8 B: 3.5 ms/step more than
+            // the bytes cost.) T % 4 == 0, so a 4-t group never straddles a clip boundary.
+            constexpr int VS = WR + 4;                       // halfs per staged d-row
+            static_assert(64 * VS * 2 <= EPI_WREG, "epilogue staging layout");
+            _Float16 * wl = (_Float16 *) (lds_raw + EPI_OFF + wave * EPI_WREG);
+            __syncthreads();
+    #pragma unroll
+            for (int i = 0; i < MI; ++i)
+    #pragma unroll
                 for (int j = 0; j < NJ; ++j)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        ((_Float16 *) wl)[(j * 16 + 4 * q + r) * (PR + 4) + ii * 16 + l16] = to16<BF>(val(ps * (PR / 16) + ii, j, r));
-            __syncthreads();
-            const int prow = rbase + ps * PR;
-            const int c = cbase - 2 * p.D + lane, h = c >> 6, d = c & 63;
-            const int clip0 = prow / p.T, t0 = prow - clip0 * p.T;   // one division per pass (T >= PR)
-#pragma unroll
-            for (int a = 0; a < PR / 4; ++a) {
-                const int m = prow + 4 * a;
-                if (m >= p.M) break;
-                const bool wrap = t0 + 4 * a >= p.T;
-                const int clip = clip0 + (wrap ? 1 : 0), t = t0 + 4 * a - (wrap ? p.T : 0);
-                const uint2 v = *(const uint2 *) ((const _Float16 *) wl + lane * (PR + 4) + 4 * a);
-                if (Q2A_ST && Q2A_ST_VT) q2a_st(v, (uint2 *) (p.vt + (((int64_t) clip * p.H + h) * 64 + d) * p.TP + t));
+    #pragma unroll
+                    for (int r = 0; r < 4; ++r) wl[(j * 16 + 4 * q + r) * VS + i * 16 + l16] = to16<BF>(val(i, j, r));
+            // wave-private region: the wave's LDS writes are ordered before its reads
+            const int h = (cbase - 2 * p.D) >> 6;
+            const int clip0 = rbase / p.T, t0 = rbase - clip0 * p.T;   // WR <= T: at most one wrap
+            const int tg = lane & 31;
+    #pragma unroll
+            for (int dd = 0; dd < 64; dd += 2) {
+                const int d = dd + (lane >> 5);
+    #pragma unroll
+                for (int a = tg; a < WR / 4; a += 32) {
+                    const int m = rbase + 4 * a;
+                    if (m >= p.M) continue;
+                    const bool wrap = t0 + 4 * a >= p.T;
+                    const int clip = clip0 + (wrap ? 1 : 0), t = t0 + 4 * a - (wrap ? p.T : 0);
+                    const uint2 v = *(const uint2 *) (wl + d * VS + 4 * a);
+                    if (Q2A_ST && Q2A_ST_VT) q2a_st(v, (uint2 *) (p.vt + (((int64_t) clip * p.H + h) * 64 + d) * p.TP + t));
+                }
             }
-            __syncthreads();
-        }
+      }
     } else if (EPI == Q2A_EPI_QKV || EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_PRE_H) {
         // output row remap (conv1's padded per-clip rows): one division per wave, its rows span < o_rpg
         constexpr bool REMAP = EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_PRE_H;
