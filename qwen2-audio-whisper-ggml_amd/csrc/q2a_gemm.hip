@@ -1044,8 +1044,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
         //      XOR-swizzled by row: the column-chunk reads are conflict-free); one wait
         //   2. their results (acc + bias) + x back into the same LDS slots: acc rows 0..63 are dead
         //   3. rows 64..127 by register loads into the freed registers; one wait
-        //   4. stores: rows 64..127 from registers, then rows 0..63 from LDS (integer-address LDS reads, opaque to the
-        //      compiler: no vmcnt guard for the glds target behind the stores)
+        //   4. stores of rows 0..63 out of LDS, row-contiguous (4 rows x 256 B per instruction instead of 16 rows x
+        //      64 B); then rows 64..127's results into the same slots and stored the same way. Integer-address LDS
+        //      reads/writes, opaque to the compiler: no vmcnt guard for the glds target behind the stores.
         const float * rsrc = p.resid ? p.resid : p.outF;
         char * rl = lds_raw + wave * (64 * 256);
 #pragma unroll
@@ -1085,33 +1086,43 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
 #pragma unroll
         for (int i = 0; i < MI / 2; ++i)
             asm volatile("" : "+v"(add_hi[i][0]), "+v"(add_hi[i][1]), "+v"(add_hi[i][2]), "+v"(add_hi[i][3]));
+        // stores out of LDS, row-contiguous: instruction k writes rows 4k .. 4k + 3 of the 64-row half, 256 B each
+        // (lane l: row 4k + l/16, 16-B chunk l % 16)
+        auto store_half = [&](int r0) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            const int ch = lane & 15;
+#pragma unroll
+            for (int k0 = 0; k0 < 16; k0 += 8) {   // 8 reads behind one wait, then their 8 stores
+                f4 v[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int lr = 4 * (k0 + k) + (lane >> 4);
+                    asm volatile("ds_read_b128 %0, %1" : "=v"(v[k]) : "v"(rl0 + (uint32_t) lr * 256 + ((uint32_t) (ch ^ (lr & 15)) << 4)));
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]),
+                             "+v"(v[7]));
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    const int m = rbase + r0 + 4 * (k0 + k) + (lane >> 4);
+                    if (m < p.M && Q2A_ST) q2a_st(v[k], (f4 *) (p.outF + (int64_t) m * p.ldo + cbase + ch * 4));
+                }
+            }
+        };
+        store_half(0);
+        // rows 64..127: (acc + bias) + x into the same LDS slots (each wave reads only its own region, in order), then
+        // stored the same way
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
         for (int i = MI / 2; i < MI; ++i) {
-            const int m = rbase + i * 16 + l16;
-            if (m >= p.M) continue;
-            float * orow = p.outF + (int64_t) m * p.ldo + cbase + 4 * q;
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
                 f4 v;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = val(i, j, r) + add_hi[i - MI / 2][j][r];
-                if (Q2A_ST) q2a_st(v, (f4 *) (orow + 16 * j));
+                asm volatile("ds_write_b128 %0, %1" :: "v"(slot(i - MI / 2, j)), "v"(v) : "memory");
             }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's LDS result writes (in-order per wave anyway)
-#pragma unroll
-        for (int i = 0; i < MI / 2; ++i) {
-            const int m = rbase + i * 16 + l16;
-            f4 v[NJ];
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) asm volatile("ds_read_b128 %0, %1" : "=v"(v[j]) : "v"(slot(i, j)));
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]));
-            if (m >= p.M) continue;
-            float * orow = p.outF + (int64_t) m * p.ldo + cbase + 4 * q;
-#pragma unroll
-            for (int j = 0; j < NJ; ++j)
-                if (Q2A_ST) q2a_st(v[j], (f4 *) (orow + 16 * j));
-        }
+        store_half(64);
     } else {
         // f32 outputs: residual add (O-proj, fc2), GELU (+ positional rows for conv2), plain store
         const int pq = EPI == Q2A_EPI_CONV2 ? rbase / p.T : 0;
