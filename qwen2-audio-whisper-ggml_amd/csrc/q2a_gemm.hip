@@ -136,6 +136,16 @@ __device__ __forceinline__ float kq_rescale(float a, float al, float be, float n
     const float u = nga * s2;
     return __builtin_fmaf(a, t, u);
 }
+// kq_rescale on elements 2h, 2h + 1 of an accumulator float4 (same IEEE operations, two lanes per packed op)
+__device__ __forceinline__ void kq_rescale2(f4 & a, int h, float al, const f4 & be, const f4 & nga, const f4 & s2) {
+#pragma clang fp contract(off)
+    const f2 a2 = {a[2 * h], a[2 * h + 1]};
+    const f2 t = f2{al, al} * f2{be[2 * h], be[2 * h + 1]};
+    const f2 u = f2{nga[2 * h], nga[2 * h + 1]} * f2{s2[2 * h], s2[2 * h + 1]};
+    const f2 r = __builtin_elementwise_fma(a2, t, u);
+    a[2 * h] = r[0];
+    a[2 * h + 1] = r[1];
+}
 __device__ __forceinline__ float kq_final(float a, float yc, float dx) {
 #pragma clang fp contract(off)
     const float t = yc * dx;
@@ -293,40 +303,49 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
         const uint32_t s_we = sb0 + 13 * 1024 + (wn * 64 + (lane & 15)) * 32 + (lane >> 4) * 8;
         f4 bet[4], gam[4];
         half4 we[4];
-        float al[2];
-        half4 ae[2];
+        float al[3];
+        half4 ae[3];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(bet[j]) : "v"(s_cn), "i"(j * 64));
             asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(gam[j]) : "v"(s_cn), "i"(1024 + j * 64));
             asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(we[j]) : "v"(s_we), "i"(j * 512));
         }
-        asm volatile("ds_read_b32 %0, %1" : "=v"(al[0]) : "v"(s_al));
-        asm volatile("ds_read_b64 %0, %1" : "=v"(ae[0]) : "v"(s_ae));
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(al[i]) : "v"(s_al), "i"(i * 64));
+            asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(ae[i]) : "v"(s_ae), "i"(i * 512));
+        }
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(bet[0]), "+v"(bet[1]), "+v"(bet[2]), "+v"(bet[3]), "+v"(gam[0]),
                      "+v"(gam[1]), "+v"(gam[2]), "+v"(gam[3]), "+v"(we[0]), "+v"(we[1]), "+v"(we[2]), "+v"(we[3]),
-                     "+v"(al[0]), "+v"(ae[0]));
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int c = i & 1, n = c ^ 1;
-            if (i + 1 < 8) {   // next row block's data in flight while this one is processed
-                asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(al[n]) : "v"(s_al), "i"((i + 1) * 64));
-                asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(ae[n]) : "v"(s_ae), "i"((i + 1) * 512));
-            }
-            f4 s2v[4];   // the four min-term MFMAs first, their latency under the first rescale products
+                     "+v"(al[0]), "+v"(ae[0]), "+v"(al[1]), "+v"(ae[1]));
+        // min-term MFMAs one row block ahead of their rescale (their latency under the previous block's VALU), row
+        // data two ahead
+        auto minterm = [&](f4 (&s2)[4], half4 a) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
 #ifdef Q2A_DIAG_NO_MINTERM   // timing diagnostic only (wrong results): the min-term operands stand in for its MFMA
-                s2v[j] = f4{(float) we[j][0], (float) we[j][1], (float) ae[c][0], (float) ae[c][1]};
+                s2[j] = f4{(float) we[j][0], (float) we[j][1], (float) a[0], (float) a[1]};
 #else
-                s2v[j] = __builtin_amdgcn_mfma_f32_16x16x16f16(we[j], ae[c], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                s2[j] = __builtin_amdgcn_mfma_f32_16x16x16f16(we[j], a, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
 #endif
             }
+        };
+        f4 s2v[2][4];
+        minterm(s2v[0], ae[0]);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            if (i + 2 < 8) {
+                asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(al[(i + 2) % 3]) : "v"(s_al), "i"((i + 2) * 64));
+                asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(ae[(i + 2) % 3]) : "v"(s_ae), "i"((i + 2) * 512));
+            }
+            if (i + 1 < 8) minterm(s2v[(i + 1) & 1], ae[(i + 1) % 3]);
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) acc[i][j][r] = kq_rescale(acc[i][j][r], al[c], bet[j][r], gam[j][r], s2v[j][r]);
-            if (i + 1 < 8) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(al[n]), "+v"(ae[n]));
+                for (int h = 0; h < 2; ++h)   // kq_rescale two columns per instruction (v_pk_mul / v_pk_fma)
+                    kq_rescale2(acc[i][j], h, al[i % 3], bet[j], gam[j], s2v[i & 1][j]);
+            if (i + 2 < 8) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(al[(i + 2) % 3]), "+v"(ae[(i + 2) % 3]));
             __builtin_amdgcn_sched_barrier(0);   // one row block at a time: bounds the live min-term results
         }
     };
