@@ -7,7 +7,7 @@ import sys
 src = sys.argv[1]
 pat = re.compile(sys.argv[2]) if len(sys.argv) > 2 else None
 cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Iinclude",
-       "-Iqwen2-audio-whisper-ggml_amd/csrc", "-w", "-c", src, "-o", "/tmp/kres.o", "-Rpass-analysis=kernel-resource-usage"]
+       "-Iqwen2-audio-whisper-ggml_amd/csrc", "-w"] + sys.argv[3:] + ["-c", src, "-o", "/tmp/kres.o", "-Rpass-analysis=kernel-resource-usage"]
 out = subprocess.run(cmd, capture_output=True, text=True).stderr
 cur = None
 rows = []
