@@ -183,13 +183,21 @@ __device__ __forceinline__ double wave_sum_d(double v) {
     return v;
 }
 
+// NBQ > 0 (whole-row Q8_K, D = 256 NBQ): 8 rows per workgroup (512 threads); the rows' d and bsum operands are staged
+// in LDS and stored by the workgroup as whole sectors (32 B of d, 256 B of bsums per block column) — one row's 4-B d
+// and 32-B bsum pieces stored by its own wave reach HBM as partial writes (diag/bwbench.hip)
 template <int MODE, bool LN, bool HIN = false, int NBQ = 0>
-__global__ __launch_bounds__(256) void k_rownorm(const float * __restrict__ X, int M, int D, const float * __restrict__ g,
+__global__ __launch_bounds__(NBQ ? 512 : 256) void k_rownorm(const float * __restrict__ X, int M, int D, const float * __restrict__ g,
                                                  const float * __restrict__ b, q2a_half * outH, float * dy, q2a_half * aext,
                                                  int nseg, int ld) {
     const int lane = threadIdx.x & 63;
-    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (row >= M) return;
+    constexpr int RPB = NBQ ? 8 : 4;   // rows per workgroup
+    const int row0 = blockIdx.x * RPB;
+    const int row_raw = row0 + (threadIdx.x >> 6);
+    if constexpr (!NBQ) {
+        if (row_raw >= M) return;
+    }
+    const int row = min(row_raw, M - 1);   // NBQ: every wave stays for the workgroup's barrier
     const float4 * x4 = (const float4 *) (X + (int64_t) row * D);
     const int nch = D / 4;
     constexpr int MAXC = 8;   // D <= 2048
@@ -254,8 +262,21 @@ __global__ __launch_bounds__(256) void k_rownorm(const float * __restrict__ X, i
                 y[u] = v[u];
             }
         }
-        quant_q8k_blocks<NBQ>(y, lane, outH + (int64_t) row * D + 4 * lane, 256, dy + row, ld, aext + (int64_t) row * 16,
-                              (int64_t) ld * 16);
+        __shared__ float sd[8][NBQ];
+        __shared__ __attribute__((aligned(16))) q2a_half sa[8][NBQ][16];
+        const int r = threadIdx.x >> 6;
+        // codes of a clamped duplicate row (past M) are the real last row's: rewriting them changes nothing
+        quant_q8k_blocks<NBQ>(y, lane, outH + (int64_t) row * D + 4 * lane, 256, &sd[r][0], 1, &sa[r][0][0], 16);
+        __syncthreads();
+        const int t = threadIdx.x;
+        if (t < NBQ * 8) {     // d: block column u, rows row0 .. row0 + 7 (32 B)
+            const int u = t >> 3, rr = t & 7;
+            if (row0 + rr < M) dy[(int64_t) u * ld + row0 + rr] = sd[rr][u];
+        }
+        if (t < NBQ * 64) {    // bsum operand: block column u, 8 rows x 32 B contiguous, 4 B per thread
+            const int u = t >> 6, w = t & 63, rr = w >> 3, j2 = w & 7;
+            if (row0 + rr < M) *(uint32_t *) (aext + ((int64_t) u * ld + row0 + rr) * 16 + 2 * j2) = *(const uint32_t *) &sa[rr][u][2 * j2];
+        }
         return;
     }
 #pragma unroll
@@ -515,7 +536,8 @@ hipError_t q2a_launch_layernorm(const q2a_ln_args & a, hipStream_t s) {
     else if (a.mode == 3) hipLaunchKernelGGL((k_rownorm<3, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else if (a.mode == 4) hipLaunchKernelGGL((k_rownorm<4, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else if (a.mode == 1 && a.D == 1280 && !getenv("Q2A_QUANT_V1"))
-        hipLaunchKernelGGL((k_rownorm<1, true, false, 5>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
+        hipLaunchKernelGGL((k_rownorm<1, true, false, 5>), dim3((a.M + 7) / 8), dim3(512), 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy,
+                           a.aext, 1, a.dy_ld);
     else if (a.mode == 1) hipLaunchKernelGGL((k_rownorm<1, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else hipLaunchKernelGGL((k_rownorm<2, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     return hipGetLastError();
@@ -550,7 +572,8 @@ hipError_t q2a_launch_quant_act(const q2a_quant_args & a, hipStream_t s) {
     } else if (a.mode == 2 && a.XH) {
         hipLaunchKernelGGL((k_rownorm<2, false, true>), grid, blk, 0, s, X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext, nseg, a.dy_ld);
     } else if (a.mode == 1 && seg == 1280 && nseg == 1) {   // f32 rows of D = 1280 (attention output): 5 blocks interleaved
-        hipLaunchKernelGGL((k_rownorm<1, false, false, 5>), grid, blk, 0, s, X, a.M, seg, nullptr, nullptr, a.outH, a.dy, a.aext, 1, a.dy_ld);
+        hipLaunchKernelGGL((k_rownorm<1, false, false, 5>), dim3((a.M + 7) / 8), dim3(512), 0, s, X, a.M, seg, nullptr, nullptr,
+                           a.outH, a.dy, a.aext, 1, a.dy_ld);
     } else if (a.mode == 1) {
         hipLaunchKernelGGL((k_rownorm<1, false>), grid, blk, 0, s, X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext, nseg, a.dy_ld);
     } else if (a.mode == 2) {
