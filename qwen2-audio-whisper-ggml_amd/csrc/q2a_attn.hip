@@ -24,6 +24,7 @@ typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void * lds_ptr_t;
 
 // 32x32x16 MFMA on fp16 operands, or on the same bits read as bf16 (bf16-activation mode)
 template <bool BF>
@@ -239,6 +240,173 @@ __global__ __launch_bounds__(256, BF ? 3 : Q2A_ATTN_F32_OCC) void k_attn(const q
                 const float v2 = o[dt][4 * g + 2] * inv, v3 = o[dt][4 * g + 3] * inv;
                 if (p.outH) {
                     const half4 hv = {to16<BF>(v0), to16<BF>(v1), to16<BF>(v2), to16<BF>(v3)};
+                    *(half4 *) (p.outH + orow + d) = hv;
+                } else {
+                    *(float4 *) (p.outF + orow + d) = make_float4(v0, v1, v2, v3);
+                }
+            }
+    }
+}
+
+// ---- F32-class default (Q2A_ATTN_G=0: k_attn instead): k_attn's arithmetic op for op, but the next tile's K hi,
+// K lo and V^T arrive by global_load_lds straight into the other of two LDS stages (two __shared__ arrays, the loop
+// unrolled by two, so the compiler sees no alias between the stage it reads and the one in flight) instead of through
+// 24 staging VGPRs: 48 KiB of LDS and < 168 VGPRs, i.e. three workgroups per CU instead of two. LDS images unpadded,
+// 16-B granules XOR-swizzled by row (K: chunk ch of row r at ch ^ ((r >> 1) & 7); V^T: granule g at g ^ ((r >> 1) & 7),
+// its two 8-B halves in order — the DMA moves whole granules, with the swizzle on the source address).
+struct attn_lds_g {
+    static constexpr int KROW = 128, VROW = 128;
+    static __device__ __forceinline__ int k(int r, int ch) { return (ch ^ ((r >> 1) & 7)) << 4; }
+    static __device__ __forceinline__ int v(int r, int c8) { return (((c8 >> 1) ^ ((r >> 1) & 7)) << 4) + ((c8 & 1) << 3); }
+};
+__global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
+    typedef attn_lds_g LY;
+    constexpr int KROW = LY::KROW, VROW = LY::VROW;
+    constexpr int KIMG = KT * KROW, VIMG = 64 * VROW, STAGE = 2 * KIMG + VIMG;
+    __shared__ __attribute__((aligned(16))) char ldsA[STAGE];
+    __shared__ __attribute__((aligned(16))) char ldsB[STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int T = p.T, D = p.D;
+    const int nq = (T + 127) / 128, total = (int) gridDim.x;
+    const int L = (int) blockIdx.x;
+    const int w = (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);   // XCD-contiguous work order (k_attn)
+    const int qt = w % nq, h = (w / nq) % p.H, clip = w / (nq * p.H);
+    const int q0 = qt * 128 + wave * 32;
+    const int64_t rowbase = (int64_t) clip * T;
+    const int hi = lane >> 5, col = lane & 31;
+
+    half8 qh[4], ql[4];
+    {
+        const int q = min(q0 + col, T - 1);
+        const q2a_half * sh = p.qh + (rowbase + q) * D + h * 64 + 8 * hi;
+        const q2a_half * sl = p.ql + (rowbase + q) * D + h * 64 + 8 * hi;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            qh[s] = *(const half8 *) (sh + 16 * s);
+            ql[s] = *(const half8 *) (sl + 16 * s);
+        }
+    }
+    const q2a_half * vt_base = p.vt + ((int64_t) clip * p.H + h) * 64 * p.TP;
+    // tile t -> stage: wave w's instruction i covers rows (2w + i) * 8 .. +7 of each image (1 KiB), lane l row
+    // + l / 8, LDS granule l % 8 <- source granule (l % 8) ^ ((row >> 1) & 7)
+    auto dma_tile = [&](char * st, int t) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int row = (2 * wave + i) * 8 + (lane >> 3), g = (lane & 7) ^ ((row >> 1) & 7);
+            const int key = min(t * KT + row, T - 1);
+            const int64_t ko = (rowbase + key) * D + h * 64 + g * 8;
+            __builtin_amdgcn_global_load_lds((const void *) (p.kh + ko), (lds_ptr_t) (st + (2 * wave + i) * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *) (p.kl + ko), (lds_ptr_t) (st + KIMG + (2 * wave + i) * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *) (vt_base + (int64_t) row * p.TP + t * KT + g * 8),
+                                             (lds_ptr_t) (st + 2 * KIMG + (2 * wave + i) * 1024), 16, 0, 0);
+        }
+    };
+
+    f16v o[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+    float m_run = -1e30f, l_run = 0.f;
+    const int ntiles = (T + KT - 1) / KT;
+
+    auto tile = [&](const char * kh_img, int t) {
+        const char * kl_img = kh_img + KIMG;
+        const char * vt_img = kh_img + 2 * KIMG;
+        f16v sc[2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sc[kb][r] = 0.f;
+            const int krow = kb * 32 + col;
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                const int off = krow * KROW + LY::k(krow, 2 * st + hi);
+                const half8 ah = *(const half8 *) (kh_img + off);
+                sc[kb] = mma32<false>(ah, qh[st], sc[kb]);
+                const half8 al = *(const half8 *) (kl_img + off);
+                sc[kb] = mma32<false>(al, qh[st], sc[kb]);
+                sc[kb] = mma32<false>(ah, ql[st], sc[kb]);
+            }
+        }
+        if (t == ntiles - 1) {   // keys >= T exist only in the last tile (row of reg r = (r&3) + 8(r>>2) + 4hi)
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (t * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi >= T) sc[kb][r] = -1e30f;
+        }
+        float mx = sc[0][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sc[0][r]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[1][r]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        const float m_new = fmaxf(m_run, mx);
+        const float nm = -m_new * L2E;
+        const float alpha = __builtin_amdgcn_exp2f(fmaf(m_run, L2E, nm));
+        float ls = 0.f;
+        half8 pf[2][2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float pv = __builtin_amdgcn_exp2f(fmaf(sc[kb][r], L2E, nm));
+                ls += pv;
+                pf[kb][r >> 3][r & 7] = (_Float16) pv;
+            }
+        l_run = l_run * alpha + ls;
+        m_run = m_new;
+        if (__any(alpha != 1.0f)) {
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+        }
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt) {
+                const int vr = dt * 32 + col;
+                const char * vrow = vt_img + vr * VROW;
+#pragma unroll
+                for (int sp = 0; sp < 2; ++sp) {
+                    const int c8 = 8 * kb + 4 * sp + hi;
+                    const half4 v0 = *(const half4 *) (vrow + LY::v(vr, c8));
+                    const half4 v1 = *(const half4 *) (vrow + LY::v(vr, c8 + 2));
+                    const half8 va = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+                    o[dt] = mma32<false>(va, pf[kb][sp], o[dt]);
+                }
+            }
+    };
+
+    dma_tile(ldsA, 0);
+    asm volatile("" :: "v"(qh[0]), "v"(qh[1]), "v"(qh[2]), "v"(qh[3]), "v"(ql[0]), "v"(ql[1]), "v"(ql[2]), "v"(ql[3]));
+    __syncthreads();   // (waits for the DMA: a pending LDS-DMA is a vmcnt event)
+    for (int t = 0; t < ntiles; t += 2) {
+        if (t + 1 < ntiles) dma_tile(ldsB, t + 1);
+        tile(ldsA, t);
+        __syncthreads();   // tile t + 1 landed (vmcnt(0) in the barrier), every wave done with A
+        if (t + 1 >= ntiles) break;
+        if (t + 2 < ntiles) dma_tile(ldsA, t + 2);
+        tile(ldsB, t + 1);
+        __syncthreads();
+    }
+
+    const float l_tot = l_run + __shfl_xor(l_run, 32);
+    const float inv = 1.0f / l_tot;
+    const int q = q0 + col;
+    if (q < T) {
+        const int64_t orow = (rowbase + q) * D + h * 64;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d = dt * 32 + 8 * g + 4 * hi;
+                const float v0 = o[dt][4 * g + 0] * inv, v1 = o[dt][4 * g + 1] * inv;
+                const float v2 = o[dt][4 * g + 2] * inv, v3 = o[dt][4 * g + 3] * inv;
+                if (p.outH) {
+                    const half4 hv = {(_Float16) v0, (_Float16) v1, (_Float16) v2, (_Float16) v3};
                     *(half4 *) (p.outH + orow + d) = hv;
                 } else {
                     *(float4 *) (p.outF + orow + d) = make_float4(v0, v1, v2, v3);
@@ -508,7 +676,11 @@ hipError_t q2a_launch_attention(const q2a_attn_args & a, hipStream_t s) {
         if (!a.outH) return hipErrorInvalidValue;
         hipLaunchKernelGGL(k_attn<true>, grid, dim3(256), 0, s, a);
     } else {
-        if (terms == 2) hipLaunchKernelGGL((k_attn<false, 2>), grid, dim3(256), 0, s, a);
+        // F32-class default: k_attn_g (K/V by LDS-DMA, three workgroups per CU: 52 -> 49 ms/step at 64 clips);
+        // Q2A_ATTN_G=0 runs the register-staged k_attn (A/B)
+        static const bool g = [] { const char * v = getenv("Q2A_ATTN_G"); return !v || atoi(v); }();
+        if (g && terms == 3) hipLaunchKernelGGL(k_attn_g, grid, dim3(256), 0, s, a);
+        else if (terms == 2) hipLaunchKernelGGL((k_attn<false, 2>), grid, dim3(256), 0, s, a);
         else if (terms == 1) hipLaunchKernelGGL((k_attn<false, 1>), grid, dim3(256), 0, s, a);
         else hipLaunchKernelGGL(k_attn<false>, grid, dim3(256), 0, s, a);
     }
