@@ -52,6 +52,8 @@ typedef struct {
     int n_buffer_reallocs; /* backend lifetime: scratch / V^T / fp16-shadow reallocations (each drops every captured
                               HIP graph, whose launches hold those buffers' addresses) */
     int n_mul_mat_conv_total; /* backend lifetime: n_mul_mat_conv summed over every graph_compute that ran its nodes */
+    int n_repack_lazy;  /* backend lifetime: weights repacked at their first MUL_MAT (a device->host copy + host pack)
+                           because their upload was not a whole host write the buffer could pack on arrival */
 } ggml_backend_q2a_stats;
 GGML_API void ggml_backend_q2a_get_stats(ggml_backend_t backend, ggml_backend_q2a_stats * stats);
 

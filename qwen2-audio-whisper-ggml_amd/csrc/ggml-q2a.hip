@@ -586,6 +586,7 @@ struct q2a_backend_ctx {
     uint64_t graph_clock = 0;
     int n_buffer_reallocs = 0;         // scratch / V^T / shadow reallocations (each drops the captured graphs)
     int n_mul_mat_conv_total = 0;      // conv MUL_MATs run on the hi/lo path over the backend's lifetime
+    int n_repack_lazy = 0;             // get_packed cache misses over the backend's lifetime
 };
 
 q2a_reg_ctx * reg_ctx();
@@ -645,11 +646,34 @@ void buf_memset_tensor(ggml_backend_buffer_t b, ggml_tensor * t, uint8_t v, size
     invalidate(c->device, (char *) t->data + off, n);
     Q2A_HIP(hipMemset((char *) t->data + off, v, n));
 }
+// Upload-time repack: the model loader writes each weight whole from host memory (qwen2-whisper.cpp:1845-1849),
+// before it marks the buffer WEIGHTS (:1867), so a whole write of a 2-D tensor that the fast MUL_MAT path could take
+// (mm_fast_ok's shape rule) is packed here from the host bytes, and the first whisper_full finds it in the cache
+// instead of paying a device->host copy + host repack per weight. Anything else is packed lazily by get_packed.
+void prepack(int device, const ggml_tensor * t, const void * host, size_t off, size_t n) {
+    if (off != 0 || n != ggml_nbytes(t) || t->view_src) return;
+    if (t->type != GGML_TYPE_F16 && t->type != GGML_TYPE_Q4_K && t->type != GGML_TYPE_Q8_0 && t->type != GGML_TYPE_Q4_0)
+        return;
+    if (t->ne[2] != 1 || t->ne[3] != 1 || !ggml_is_contiguous(t)) return;
+    const int64_t K = t->ne[0], N = t->ne[1];
+    if (N % 128 != 0 || K % 256 != 0 || K > 8192 || N > (1 << 30)) return;
+    packed_w p;
+    p.raw = (const char *) t->data; p.raw_bytes = n; p.type = t->type; p.N = (int) N; p.K = (int) K;
+    std::vector<uint8_t> out;
+    if (q2a_pack_linear((const uint8_t *) host, t->type, p.N, p.K, out, p.off) != 0) return;
+    Q2A_HIP(hipMalloc(&p.dev, out.size()));
+    Q2A_HIP(hipMemcpy(p.dev, out.data(), out.size(), hipMemcpyHostToDevice));
+    q2a_device_ctx * d = dev_ctx(device);
+    std::lock_guard<std::mutex> lk(d->mu);
+    d->wcache.push_back(p);
+}
+
 void buf_set_tensor(ggml_backend_buffer_t b, ggml_tensor * t, const void * data, size_t off, size_t n) {
     q2a_buffer_ctx * c = (q2a_buffer_ctx *) b->context;
     Q2A_HIP(hipSetDevice(c->device));
     invalidate(c->device, (char *) t->data + off, n);
     Q2A_HIP(hipMemcpy((char *) t->data + off, data, n, hipMemcpyHostToDevice));
+    prepack(c->device, t, data, off, n);
 }
 void buf_get_tensor(ggml_backend_buffer_t b, const ggml_tensor * t, void * data, size_t off, size_t n) {
     q2a_buffer_ctx * c = (q2a_buffer_ctx *) b->context;
@@ -774,6 +798,7 @@ packed_w get_packed(q2a_backend_ctx * b, const ggml_tensor * w) {
             if (p.raw == (const char *) w->data && p.type == w->type && p.N == w->ne[1] && p.K == w->ne[0]) return p;
     }
     // first use: repack on the host from the device bytes (one-time, per weight tensor)
+    ++b->n_repack_lazy;
     const size_t nb = ggml_nbytes(w);
     std::vector<uint8_t> raw(nb);
     Q2A_HIP(hipStreamSynchronize(b->stream));
@@ -1541,6 +1566,7 @@ void be_set_tensor_async(ggml_backend_t be, ggml_tensor * t, const void * data, 
     GGML_ASSERT(buf && is_q2a_buffer(buf) && "unsupported buffer type");
     invalidate(b->device, (char *) t->data + off, n);
     Q2A_HIP(hipMemcpyAsync((char *) t->data + off, data, n, hipMemcpyHostToDevice, b->stream));
+    prepack(b->device, t, data, off, n);   // reads the host bytes only (the pack does not wait for the copy)
 }
 void be_get_tensor_async(ggml_backend_t be, const ggml_tensor * t, void * data, size_t off, size_t n) {
     q2a_backend_ctx * b = (q2a_backend_ctx *) be->context;
@@ -1719,6 +1745,7 @@ void ggml_backend_q2a_get_stats(ggml_backend_t backend, ggml_backend_q2a_stats *
         *stats = b->stats;
         stats->n_buffer_reallocs = b->n_buffer_reallocs;
         stats->n_mul_mat_conv_total = b->n_mul_mat_conv_total;
+        stats->n_repack_lazy = b->n_repack_lazy;
     }
 }
 

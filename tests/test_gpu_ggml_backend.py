@@ -51,6 +51,8 @@ def test_reference_whisper_full_on_backend_tiny(harness, make_model, make_clip, 
     L = 2
     assert info["mul_mat_fast"] == 6 * L and info["attn_fused"] == L and info["mul_mat_f32"] == 0, info
     assert info["n_splits_encode"] == 1, info
+    # weights were packed as the loader uploaded them (ggml-q2a.hip prepack), not at the first MUL_MAT
+    assert info["repack_lazy"] == 0, info
     if wt == "f16":
         mx, l2 = rel_errors(emb, g["tiny_f16_c0"])
         assert mx < 1e-3 and l2 < 1e-4, (mx, l2)
@@ -72,7 +74,7 @@ def test_backend_unfused_attention_path(harness, make_model, make_clip, golden, 
 def test_reference_whisper_full_on_backend_full_size(harness, make_model, make_clip, golden, xbuild_bar, wt, tmp_path):
     _, g = golden
     emb, info = run(harness, make_model("full", wt), make_clip(0), tmp_path)
-    assert info["mul_mat_fast"] == 6 * 32 and info["attn_fused"] == 32, info
+    assert info["mul_mat_fast"] == 6 * 32 and info["attn_fused"] == 32 and info["repack_lazy"] == 0, info
     o = emb.reshape(-1)
     mxs, l2s = rel_errors(o[g[f"full_{wt}_c0_idx"]], g[f"full_{wt}_c0_val"])
     rn = np.linalg.norm(emb.astype(np.float64), axis=1)
