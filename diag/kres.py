@@ -26,4 +26,4 @@ for r in rows:
     if pat and not pat.search(r["name"]):
         continue
     print(f"{r['name'][:90]:90s} V{r.get('VGPRs','?'):>4} A{r.get('AGPRs','?'):>4} spV{r.get('VGPRs Spill','?'):>3} "
-          f"spS{r.get('SGPRs Spill','?'):>3} LDS{r.get('LDS Size [bytes/block]','?'):>7} occ{r.get('Occupancy [waves/SIMD]','?')}")
+          f"spS{r.get('SGPRs Spill','?'):>3} scr{r.get('ScratchSize [bytes/lane]','?'):>3} LDS{r.get('LDS Size [bytes/block]','?'):>7} occ{r.get('Occupancy [waves/SIMD]','?')}")

@@ -257,8 +257,13 @@ __global__ __launch_bounds__(256, BF ? 3 : Q2A_ATTN_F32_OCC) void k_attn(const q
 struct attn_lds_g {
     static constexpr int KROW = 128, VROW = 128;
     static __device__ __forceinline__ int k(int r, int ch) { return (ch ^ ((r >> 1) & 7)) << 4; }
-    static __device__ __forceinline__ int v(int r, int c8) { return (((c8 >> 1) ^ ((r >> 1) & 7)) << 4) + ((c8 & 1) << 3); }
+    static __device__ __forceinline__ int vg(int r, int g) { return (g ^ ((r >> 1) & 7)) << 4; }
 };
+// K row loaded into row i of the QK^T A operand: i with bits 2 and 3 swapped. S^T's accumulator row for register r
+// of lane half hi is (r&3) + 8(r>>2) + 4hi, so register r then holds key 16(r>>3) + 8hi + (r&7): the 8 keys a lane
+// half feeds the P.V MFMA as one B fragment are contiguous, and their V^T operand is ONE 16-B LDS read instead of
+// two 8-B reads and a register shuffle (softmax is order-free over the keys of a tile)
+__device__ __forceinline__ int kperm(int c) { return (c & ~12) | ((c & 4) << 1) | ((c & 8) >> 1); }
 __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
     typedef attn_lds_g LY;
     constexpr int KROW = LY::KROW, VROW = LY::VROW;
@@ -289,16 +294,21 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
     const q2a_half * vt_base = p.vt + ((int64_t) clip * p.H + h) * 64 * p.TP;
     // tile t -> stage: wave w's instruction i covers rows (2w + i) * 8 .. +7 of each image (1 KiB), lane l row
     // + l / 8, LDS granule l % 8 <- source granule (l % 8) ^ ((row >> 1) & 7)
+    // sources as a uniform (clip, head) base + a 32-bit per-lane byte offset (the saddr form of the DMA: no 64-bit
+    // address arithmetic per tile; a clip's K rows span T·D·2 B, its head's V^T 64·TP·2 B)
+    const char * khb = (const char *) (p.kh + rowbase * D + h * 64);
+    const char * klb = (const char *) (p.kl + rowbase * D + h * 64);
+    const char * vtb = (const char *) vt_base;
     auto dma_tile = [&](char * st, int t) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int row = (2 * wave + i) * 8 + (lane >> 3), g = (lane & 7) ^ ((row >> 1) & 7);
             const int key = min(t * KT + row, T - 1);
-            const int64_t ko = (rowbase + key) * D + h * 64 + g * 8;
-            __builtin_amdgcn_global_load_lds((const void *) (p.kh + ko), (lds_ptr_t) (st + (2 * wave + i) * 1024), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void *) (p.kl + ko), (lds_ptr_t) (st + KIMG + (2 * wave + i) * 1024), 16, 0, 0);
-            __builtin_amdgcn_global_load_lds((const void *) (vt_base + (int64_t) row * p.TP + t * KT + g * 8),
-                                             (lds_ptr_t) (st + 2 * KIMG + (2 * wave + i) * 1024), 16, 0, 0);
+            const uint32_t ko = (uint32_t) (key * D + g * 8) * 2u;
+            const uint32_t vo = (uint32_t) (row * p.TP + t * KT + g * 8) * 2u;
+            __builtin_amdgcn_global_load_lds((const void *) (khb + ko), (lds_ptr_t) (st + (2 * wave + i) * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *) (klb + ko), (lds_ptr_t) (st + KIMG + (2 * wave + i) * 1024), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void *) (vtb + vo), (lds_ptr_t) (st + 2 * KIMG + (2 * wave + i) * 1024), 16, 0, 0);
         }
     };
 
@@ -318,7 +328,7 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
         for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) sc[kb][r] = 0.f;
-            const int krow = kb * 32 + col;
+            const int krow = kb * 32 + kperm(col);
 #pragma unroll
             for (int st = 0; st < 4; ++st) {
                 const int off = krow * KROW + LY::k(krow, 2 * st + hi);
@@ -329,12 +339,12 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
                 sc[kb] = mma32<false>(ah, ql[st], sc[kb]);
             }
         }
-        if (t == ntiles - 1) {   // keys >= T exist only in the last tile (row of reg r = (r&3) + 8(r>>2) + 4hi)
+        if (t == ntiles - 1) {   // keys >= T exist only in the last tile (key of reg r: 16(r>>3) + 8hi + (r&7))
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
-                    if (t * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi >= T) sc[kb][r] = -1e30f;
+                    if (t * KT + kb * 32 + 16 * (r >> 3) + 8 * hi + (r & 7) >= T) sc[kb][r] = -1e30f;
         }
         float mx = sc[0][0];
 #pragma unroll
@@ -368,13 +378,9 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
 #pragma unroll
             for (int dt = 0; dt < 2; ++dt) {
                 const int vr = dt * 32 + col;
-                const char * vrow = vt_img + vr * VROW;
 #pragma unroll
-                for (int sp = 0; sp < 2; ++sp) {
-                    const int c8 = 8 * kb + 4 * sp + hi;
-                    const half4 v0 = *(const half4 *) (vrow + LY::v(vr, c8));
-                    const half4 v1 = *(const half4 *) (vrow + LY::v(vr, c8 + 2));
-                    const half8 va = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+                for (int sp = 0; sp < 2; ++sp) {   // keys 32kb + 16sp + 8hi .. +7: one 16-B granule of the V^T row
+                    const half8 va = *(const half8 *) (vt_img + vr * VROW + LY::vg(vr, 4 * kb + 2 * sp + hi));
                     o[dt] = mma32<false>(va, pf[kb][sp], o[dt]);
                 }
             }
@@ -427,7 +433,10 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
 template <bool BF>
 __global__ __launch_bounds__(512, 2) void k_attn_pp(const q2a_attn_args p) {
     typedef attn_lds<false> LY;
-    constexpr int KROW = LY::KROW, VROW = LY::VROW;
+    // V^T rows padded to 144 B like K's (16-B granules in order: conflict-free for the 16-lane groups of a b128 read,
+    // one base register + immediates; an XOR swizzle needs an address register per granule and costs the 4th wave)
+    // so the 8 keys of a P.V B fragment (K rows permuted by kperm, as in k_attn_g) are ONE ds_read_b128
+    constexpr int KROW = LY::KROW, VROW = LY::KROW;
     constexpr int KIMG = KT * KROW, VIMG = 64 * VROW;
     constexpr int NK = BF ? 1 : 2;                 // K images per stage (hi, lo)
     constexpr int STAGE = NK * KIMG + VIMG;
@@ -483,9 +492,10 @@ __global__ __launch_bounds__(512, 2) void k_attn_pp(const q2a_attn_args p) {
             if (img < NK) {
                 *(uint4 *) (st + img * KIMG + r * KROW + LY::k(r, pc)) = rg[u];
             } else {
-                char * vr = st + NK * KIMG + r * VROW;
-                *(uint2 *) (vr + LY::v(r, 2 * pc)) = make_uint2(rg[u].x, rg[u].y);
-                *(uint2 *) (vr + LY::v(r, 2 * pc + 1)) = make_uint2(rg[u].z, rg[u].w);
+                // (two 8-B stores: written as one uint4 here the compiler merges both branches and moves rg to scratch)
+                char * vr = st + NK * KIMG + r * VROW + pc * 16;
+                *(uint2 *) vr = make_uint2(rg[u].x, rg[u].y);
+                *(uint2 *) (vr + 8) = make_uint2(rg[u].z, rg[u].w);
             }
         }
     };
@@ -518,13 +528,9 @@ __global__ __launch_bounds__(512, 2) void k_attn_pp(const q2a_attn_args p) {
 #pragma unroll
                 for (int dt = 0; dt < 2; ++dt) {
                     const int vr = dt * 32 + col;
-                    const char * vrow = vt_img + vr * VROW;
 #pragma unroll
-                    for (int sp = 0; sp < 2; ++sp) {
-                        const int c8 = 8 * kb + 4 * sp + hi;
-                        const half4 v0 = *(const half4 *) (vrow + LY::v(vr, c8));
-                        const half4 v1 = *(const half4 *) (vrow + LY::v(vr, c8 + 2));
-                        const half8 va = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+                    for (int sp = 0; sp < 2; ++sp) {   // keys 32kb + 16sp + 8hi .. +7
+                        const half8 va = *(const half8 *) (vt_img + vr * VROW + (4 * kb + 2 * sp + hi) * 16);
                         o[dt] = mma32<BF>(va, pf[kb][sp], o[dt]);
                     }
                 }
@@ -533,7 +539,7 @@ __global__ __launch_bounds__(512, 2) void k_attn_pp(const q2a_attn_args p) {
             const char * kh_img = lds + (t % NST) * STAGE;
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb) {
-                const int krow = kb * 32 + col;
+                const int krow = kb * 32 + kperm(col);
 #pragma unroll
                 for (int r = 0; r < 16; ++r) sc[kb][r] = 0.f;
 #pragma unroll
@@ -552,12 +558,12 @@ __global__ __launch_bounds__(512, 2) void k_attn_pp(const q2a_attn_args p) {
     };
     // VALU segment V(t): online-softmax update of tile t's scores -> pf, alpha (applied at the next P.V)
     auto valu_seg = [&](int t, int ntiles) __attribute__((always_inline)) {
-        if (t == ntiles - 1) {   // keys >= T exist only in the last tile (row of reg r = (r&3) + 8(r>>2) + 4hi)
+        if (t == ntiles - 1) {   // keys >= T exist only in the last tile (key of reg r: 16(r>>3) + 8hi + (r&7))
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
                 for (int r = 0; r < 16; ++r)
-                    if (t * KT + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi >= T) sc[kb][r] = -1e30f;
+                    if (t * KT + kb * 32 + 16 * (r >> 3) + 8 * hi + (r & 7) >= T) sc[kb][r] = -1e30f;
         }
         float mx0 = sc[0][0], mx1 = sc[1][0];
 #pragma unroll
@@ -597,10 +603,8 @@ __global__ __launch_bounds__(512, 2) void k_attn_pp(const q2a_attn_args p) {
                     *(uint4 *) (st + img * KIMG + r * KROW + LY::k(r, pc)) =
                         *(const uint4 *) (src + (rowbase + min(kb0 + r, T - 1)) * D + h * 64 + pc * 8);
                 } else {
-                    const uint4 v = *(const uint4 *) (vt_base + (int64_t) r * p.TP + kb0 + pc * 8);
-                    char * vr = st + NK * KIMG + r * VROW;
-                    *(uint2 *) (vr + LY::v(r, 2 * pc)) = make_uint2(v.x, v.y);
-                    *(uint2 *) (vr + LY::v(r, 2 * pc + 1)) = make_uint2(v.z, v.w);
+                    *(uint4 *) (st + NK * KIMG + r * VROW + pc * 16) =
+                        *(const uint4 *) (vt_base + (int64_t) r * p.TP + kb0 + pc * 8);
                 }
             }
         }
