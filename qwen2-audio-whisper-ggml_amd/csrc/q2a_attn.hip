@@ -264,6 +264,30 @@ struct attn_lds_g {
 // half feeds the P.V MFMA as one B fragment are contiguous, and their V^T operand is ONE 16-B LDS read instead of
 // two 8-B reads and a register shuffle (softmax is order-free over the keys of a tile)
 __device__ __forceinline__ int kperm(int c) { return (c & ~12) | ((c & 4) << 1) | ((c & 8) >> 1); }
+// max of x over lanes l and l ^ 32: v_permlane32_swap exchanges the two wave halves in a VALU slot (no LDS round
+// trip as ds_bpermute, no lgkmcnt wait); one of the two results is the lane's own value (attention -1 %, same box)
+#ifndef Q2A_ATTN_PERM32
+#define Q2A_ATTN_PERM32 1
+#endif
+__device__ __forceinline__ float max_lane32(float x) {
+#if Q2A_ATTN_PERM32
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+#else
+    return fmaxf(x, __shfl_xor(x, 32));
+#endif
+}
+// Q2A_ATTN_PRIO: 1 = s_setprio 1 around the QK^T MFMA cluster, 2 = around the QK^T and the P.V clusters (the wave
+// with matrix work ready wins issue arbitration over the co-resident waves in their softmax)
+#ifndef Q2A_ATTN_PRIO
+#define Q2A_ATTN_PRIO 0
+#endif
+#ifndef Q2A_ATTN_DIAG_NOSM
+#define Q2A_ATTN_DIAG_NOSM 0   // diagnostic builds only (diag/build_attn_variant.sh): no softmax VALU
+#endif
+#ifndef Q2A_ATTN_DIAG_NOPV
+#define Q2A_ATTN_DIAG_NOPV 0   // diagnostic builds only: no P.V MFMAs
+#endif
 __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
     typedef attn_lds_g LY;
     constexpr int KROW = LY::KROW, VROW = LY::VROW;
@@ -324,6 +348,7 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
         const char * kl_img = kh_img + KIMG;
         const char * vt_img = kh_img + 2 * KIMG;
         f16v sc[2];
+        if (Q2A_ATTN_PRIO >= 1) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
@@ -339,6 +364,7 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
                 sc[kb] = mma32<false>(ah, ql[st], sc[kb]);
             }
         }
+        if (Q2A_ATTN_PRIO >= 1) __builtin_amdgcn_s_setprio(0);
         if (t == ntiles - 1) {   // keys >= T exist only in the last tile (key of reg r: 16(r>>3) + 8hi + (r&7))
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb)
@@ -346,12 +372,21 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
                 for (int r = 0; r < 16; ++r)
                     if (t * KT + kb * 32 + 16 * (r >> 3) + 8 * hi + (r & 7) >= T) sc[kb][r] = -1e30f;
         }
+#if Q2A_ATTN_DIAG_NOSM   // diagnostic timing build: no max / exp (P = S / 64), wrong values on purpose
+        const float alpha = 1.0f;
+        float ls = 1.0f;
+        half8 pf[2][2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) pf[kb][r >> 3][r & 7] = (_Float16) (sc[kb][r] * 0.015625f);
+#else
         float mx = sc[0][0];
 #pragma unroll
         for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sc[0][r]);
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[1][r]);
-        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        mx = max_lane32(mx);
         const float m_new = fmaxf(m_run, mx);
         const float nm = -m_new * L2E;
         const float alpha = __builtin_amdgcn_exp2f(fmaf(m_run, L2E, nm));
@@ -365,14 +400,18 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
                 ls += pv;
                 pf[kb][r >> 3][r & 7] = (_Float16) pv;
             }
+#endif
         l_run = l_run * alpha + ls;
+#if !Q2A_ATTN_DIAG_NOSM
         m_run = m_new;
+#endif
         if (__any(alpha != 1.0f)) {
 #pragma unroll
             for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
         }
+        if (Q2A_ATTN_PRIO >= 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -381,9 +420,11 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
 #pragma unroll
                 for (int sp = 0; sp < 2; ++sp) {   // keys 32kb + 16sp + 8hi .. +7: one 16-B granule of the V^T row
                     const half8 va = *(const half8 *) (vt_img + vr * VROW + LY::vg(vr, 4 * kb + 2 * sp + hi));
-                    o[dt] = mma32<false>(va, pf[kb][sp], o[dt]);
+                    if (!Q2A_ATTN_DIAG_NOPV) o[dt] = mma32<false>(va, pf[kb][sp], o[dt]);
+                    else o[dt][0] += (float) pf[kb][sp][0] + (float) va[1];   // diagnostic: keep P and V live
                 }
             }
+        if (Q2A_ATTN_PRIO >= 2) __builtin_amdgcn_s_setprio(0);
     };
 
     dma_tile(ldsA, 0);
@@ -400,6 +441,335 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
     }
 
     const float l_tot = l_run + __shfl_xor(l_run, 32);
+    const float inv = 1.0f / l_tot;
+    const int q = q0 + col;
+    if (q < T) {
+        const int64_t orow = (rowbase + q) * D + h * 64;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d = dt * 32 + 8 * g + 4 * hi;
+                const float v0 = o[dt][4 * g + 0] * inv, v1 = o[dt][4 * g + 1] * inv;
+                const float v2 = o[dt][4 * g + 2] * inv, v3 = o[dt][4 * g + 3] * inv;
+                if (p.outH) {
+                    const half4 hv = {(_Float16) v0, (_Float16) v1, (_Float16) v2, (_Float16) v3};
+                    *(half4 *) (p.outH + orow + d) = hv;
+                } else {
+                    *(float4 *) (p.outF + orow + d) = make_float4(v0, v1, v2, v3);
+                }
+            }
+    }
+}
+
+// ---- F32-class, 32-key tiles (k_attn_g32): k_attn_g's arithmetic per 32-key half tile — the same three MFMAs per
+// 16-deep step in the same order, the same exp2/fp16 P — with the online-softmax update once per 32 keys instead of
+// once per 64, so only 16 score registers are live and the kernel fits 128 VGPRs: FOUR workgroups (16 waves) per CU
+// instead of three, for latency hiding. A stage is 12 KiB (K hi, K lo: 32 rows x 128 B; V^T: 64 rows x 64 B), two
+// stages 24 KiB, four workgroups 96 KiB of LDS. Per tile each wave DMAs one 1-KiB piece of each image. LDS layouts:
+// K as k_attn_g (16-B chunk ch of row r at ch ^ ((r >> 1) & 7)); V^T granule g of row r at g ^ ((r >> 2) & 3), which
+// makes the 16 rows of each ds_read_b128 lane group hit 16 distinct 16-B bank groups of the 64-B rows.
+// NOTE: per-32-key updates change where the running max is re-based (m after 32 keys instead of 64): P values are
+// exp2 of a different (equally valid) shift, so results are F32-class-equal to k_attn_g, not bit-identical.
+constexpr int KT32 = 32;
+__global__ __launch_bounds__(256, 4) void k_attn_g32(const q2a_attn_args p) {
+    constexpr int KROW = 128, VROW = 64;
+    constexpr int KIMG = KT32 * KROW, VIMG = 64 * VROW, STAGE = 2 * KIMG + VIMG;
+    __shared__ __attribute__((aligned(16))) char ldsA[STAGE];
+    __shared__ __attribute__((aligned(16))) char ldsB[STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int T = p.T, D = p.D;
+    const int nq = (T + 127) / 128, total = (int) gridDim.x;
+    const int L = (int) blockIdx.x;
+    const int w = (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);   // XCD-contiguous work order (k_attn)
+    const int qt = w % nq, h = (w / nq) % p.H, clip = w / (nq * p.H);
+    const int q0 = qt * 128 + wave * 32;
+    const int64_t rowbase = (int64_t) clip * T;
+    const int hi = lane >> 5, col = lane & 31;
+
+    half8 qh[4], ql[4];
+    {
+        const int q = min(q0 + col, T - 1);
+        const q2a_half * sh = p.qh + (rowbase + q) * D + h * 64 + 8 * hi;
+        const q2a_half * sl = p.ql + (rowbase + q) * D + h * 64 + 8 * hi;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            qh[s] = *(const half8 *) (sh + 16 * s);
+            ql[s] = *(const half8 *) (sl + 16 * s);
+        }
+    }
+    const char * khb = (const char *) (p.kh + rowbase * D + h * 64);
+    const char * klb = (const char *) (p.kl + rowbase * D + h * 64);
+    const char * vtb = (const char *) (p.vt + ((int64_t) clip * p.H + h) * 64 * p.TP);
+    // wave w: rows 8w .. 8w+7 of the K hi and K lo images (lane: row + lane / 8, LDS chunk lane % 8), rows
+    // 16w .. 16w+15 of the V^T image (lane: row + lane / 4, LDS granule lane % 4); swizzles on the source address
+    const int krow_d = 8 * wave + (lane >> 3), kg = (lane & 7) ^ ((krow_d >> 1) & 7);
+    const int vrow_d = 16 * wave + (lane >> 2), vg = (lane & 3) ^ ((vrow_d >> 2) & 3);
+    auto dma_tile = [&](char * st, int t) {
+        const int key = min(t * KT32 + krow_d, T - 1);
+        const uint32_t ko = (uint32_t) (key * D + kg * 8) * 2u;
+        const uint32_t vo = (uint32_t) (vrow_d * p.TP + t * KT32 + vg * 8) * 2u;
+        __builtin_amdgcn_global_load_lds((const void *) (khb + ko), (lds_ptr_t) (st + wave * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void *) (klb + ko), (lds_ptr_t) (st + KIMG + wave * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void *) (vtb + vo), (lds_ptr_t) (st + 2 * KIMG + wave * 1024), 16, 0, 0);
+    };
+
+    f16v o[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+    float m_run = -1e30f, l_run = 0.f;
+    const int ntiles = (T + KT32 - 1) / KT32;
+    const int krow = kperm(col);
+
+    auto tile = [&](const char * kh_img, int t) {
+        const char * kl_img = kh_img + KIMG;
+        const char * vt_img = kh_img + 2 * KIMG;
+        f16v sc;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc[r] = 0.f;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            const int off = krow * KROW + attn_lds_g::k(krow, 2 * st + hi);
+            const half8 ah = *(const half8 *) (kh_img + off);
+            sc = mma32<false>(ah, qh[st], sc);
+            const half8 al = *(const half8 *) (kl_img + off);
+            sc = mma32<false>(al, qh[st], sc);
+            sc = mma32<false>(ah, ql[st], sc);
+        }
+        if (t == ntiles - 1) {   // keys >= T exist only in the last tile (key of reg r: 16(r>>3) + 8hi + (r&7))
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (t * KT32 + 16 * (r >> 3) + 8 * hi + (r & 7) >= T) sc[r] = -1e30f;
+        }
+        float mx = sc[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sc[r]);
+        mx = max_lane32(mx);
+        const float m_new = fmaxf(m_run, mx);
+        const float nm = -m_new * L2E;
+        const float alpha = __builtin_amdgcn_exp2f(fmaf(m_run, L2E, nm));
+        float ls = 0.f;
+        half8 pf[2];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float pv = __builtin_amdgcn_exp2f(fmaf(sc[r], L2E, nm));
+            ls += pv;
+            pf[r >> 3][r & 7] = (_Float16) pv;
+        }
+        l_run = l_run * alpha + ls;
+        m_run = m_new;
+        if (__any(alpha != 1.0f)) {
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+        }
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+            const int vr = dt * 32 + col;
+#pragma unroll
+            for (int sp = 0; sp < 2; ++sp) {   // keys 16sp + 8hi .. +7: one 16-B granule of the V^T row
+                const half8 va = *(const half8 *) (vt_img + vr * VROW + (((2 * sp + hi) ^ ((vr >> 2) & 3)) << 4));
+                o[dt] = mma32<false>(va, pf[sp], o[dt]);
+            }
+        }
+    };
+
+    dma_tile(ldsA, 0);
+    asm volatile("" :: "v"(qh[0]), "v"(qh[1]), "v"(qh[2]), "v"(qh[3]), "v"(ql[0]), "v"(ql[1]), "v"(ql[2]), "v"(ql[3]));
+    __syncthreads();   // (waits for the DMA: a pending LDS-DMA is a vmcnt event)
+    for (int t = 0; t < ntiles; t += 2) {
+        if (t + 1 < ntiles) dma_tile(ldsB, t + 1);
+        tile(ldsA, t);
+        __syncthreads();   // tile t + 1 landed (vmcnt(0) in the barrier), every wave done with A
+        if (t + 1 >= ntiles) break;
+        if (t + 2 < ntiles) dma_tile(ldsA, t + 2);
+        tile(ldsB, t + 1);
+        __syncthreads();
+    }
+
+    float l_tot = l_run;
+    {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run), __float_as_uint(l_run), false, false);
+        l_tot = __uint_as_float(r[0]) + __uint_as_float(r[1]);   // the lane's own sum plus its partner's
+    }
+    const float inv = 1.0f / l_tot;
+    const int q = q0 + col;
+    if (q < T) {
+        const int64_t orow = (rowbase + q) * D + h * 64;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d = dt * 32 + 8 * g + 4 * hi;
+                const float v0 = o[dt][4 * g + 0] * inv, v1 = o[dt][4 * g + 1] * inv;
+                const float v2 = o[dt][4 * g + 2] * inv, v3 = o[dt][4 * g + 3] * inv;
+                if (p.outH) {
+                    const half4 hv = {(_Float16) v0, (_Float16) v1, (_Float16) v2, (_Float16) v3};
+                    *(half4 *) (p.outH + orow + d) = hv;
+                } else {
+                    *(float4 *) (p.outF + orow + d) = make_float4(v0, v1, v2, v3);
+                }
+            }
+    }
+}
+
+// ---- F32-class, software-pipelined (k_attn_p32): k_attn_g32's per-32-key arithmetic, but iteration t issues the
+// QK^T MFMAs of tile t+1 in the same scheduling region as the online-softmax VALU of tile t (independent, so the
+// wave's own matrix pipe and VALU overlap: sched_group_barrier interleaves one MFMA with a group of VALU), then the
+// P.V MFMAs of tile t. Three LDS stages (tile t's V^T, tile t+1's K, tile t+2 in flight), 36 KiB, one barrier per
+// tile. The QK^T of the (non-existent) tile after the last one reads a stale stage; its scores are discarded.
+#ifndef Q2A_ATTN_P32_OCC
+#define Q2A_ATTN_P32_OCC 3
+#endif
+#ifndef Q2A_ATTN_P32_SCHED
+#define Q2A_ATTN_P32_SCHED 1
+#endif
+__global__ __launch_bounds__(256, Q2A_ATTN_P32_OCC) void k_attn_p32(const q2a_attn_args p) {
+    constexpr int KROW = 128, VROW = 64;
+    constexpr int KIMG = KT32 * KROW, VIMG = 64 * VROW, STAGE = 2 * KIMG + VIMG;
+    __shared__ __attribute__((aligned(16))) char ldsA[STAGE];
+    __shared__ __attribute__((aligned(16))) char ldsB[STAGE];
+    __shared__ __attribute__((aligned(16))) char ldsC[STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int T = p.T, D = p.D;
+    const int nq = (T + 127) / 128, total = (int) gridDim.x;
+    const int L = (int) blockIdx.x;
+    const int w = (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);   // XCD-contiguous work order (k_attn)
+    const int qt = w % nq, h = (w / nq) % p.H, clip = w / (nq * p.H);
+    const int q0 = qt * 128 + wave * 32;
+    const int64_t rowbase = (int64_t) clip * T;
+    const int hi = lane >> 5, col = lane & 31;
+
+    half8 qh[4], ql[4];
+    {
+        const int q = min(q0 + col, T - 1);
+        const q2a_half * sh = p.qh + (rowbase + q) * D + h * 64 + 8 * hi;
+        const q2a_half * sl = p.ql + (rowbase + q) * D + h * 64 + 8 * hi;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            qh[s] = *(const half8 *) (sh + 16 * s);
+            ql[s] = *(const half8 *) (sl + 16 * s);
+        }
+    }
+    const char * khb = (const char *) (p.kh + rowbase * D + h * 64);
+    const char * klb = (const char *) (p.kl + rowbase * D + h * 64);
+    const char * vtb = (const char *) (p.vt + ((int64_t) clip * p.H + h) * 64 * p.TP);
+    const int krow_d = 8 * wave + (lane >> 3), kg = (lane & 7) ^ ((krow_d >> 1) & 7);
+    const int vrow_d = 16 * wave + (lane >> 2), vg = (lane & 3) ^ ((vrow_d >> 2) & 3);
+    auto dma_tile = [&](char * st, int t) {
+        const int key = min(t * KT32 + krow_d, T - 1);
+        const uint32_t ko = (uint32_t) (key * D + kg * 8) * 2u;
+        const uint32_t vo = (uint32_t) (vrow_d * p.TP + t * KT32 + vg * 8) * 2u;
+        __builtin_amdgcn_global_load_lds((const void *) (khb + ko), (lds_ptr_t) (st + wave * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void *) (klb + ko), (lds_ptr_t) (st + KIMG + wave * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void *) (vtb + vo), (lds_ptr_t) (st + 2 * KIMG + wave * 1024), 16, 0, 0);
+    };
+
+    f16v o[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+    float m_run = -1e30f, l_run = 0.f;
+    const int ntiles = (T + KT32 - 1) / KT32;
+    const int krow = kperm(col);
+
+    auto qk = [&](const char * kh_img) {
+        const char * kl_img = kh_img + KIMG;
+        f16v s;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = 0.f;
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            const int off = krow * KROW + attn_lds_g::k(krow, 2 * st + hi);
+            const half8 ah = *(const half8 *) (kh_img + off);
+            s = mma32<false>(ah, qh[st], s);
+            const half8 al = *(const half8 *) (kl_img + off);
+            s = mma32<false>(al, qh[st], s);
+            s = mma32<false>(ah, ql[st], s);
+        }
+        return s;
+    };
+
+    f16v sc;
+    // iteration t: K of tile t+1 in sK, V^T of tile t in sV, tile t+2 DMA'd into sD
+    auto iter = [&](const char * sK, const char * sV, char * sD, int t) {
+        if (t + 2 < ntiles) dma_tile(sD, t + 2);
+        if (t == ntiles - 1) {   // keys >= T exist only in the last tile (key of reg r: 16(r>>3) + 8hi + (r&7))
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (t * KT32 + 16 * (r >> 3) + 8 * hi + (r & 7) >= T) sc[r] = -1e30f;
+        }
+        // ---- one scheduling region: QK^T(t+1) MFMAs beside softmax(t) VALU
+        const f16v sn = qk(sK);
+        float mx = sc[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sc[r]);
+        mx = max_lane32(mx);
+        const float m_new = fmaxf(m_run, mx);
+        const float nm = -m_new * L2E;
+        const float alpha = __builtin_amdgcn_exp2f(fmaf(m_run, L2E, nm));
+        float ls = 0.f;
+        half8 pf[2];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float pv = __builtin_amdgcn_exp2f(fmaf(sc[r], L2E, nm));
+            ls += pv;
+            pf[r >> 3][r & 7] = (_Float16) pv;
+        }
+        l_run = l_run * alpha + ls;
+        m_run = m_new;
+        // P complete before the rescale branch below (otherwise the exp2 loop is sunk past it, out of the MFMAs' region)
+        asm volatile("" :: "v"(pf[0]), "v"(pf[1]), "v"(l_run));
+#if Q2A_ATTN_P32_SCHED
+        // 8 K-fragment reads first, then 12 x {1 MFMA, 6 VALU}
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+        for (int i = 0; i < 12; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 6, 0);
+        }
+#endif
+        if (__any(alpha != 1.0f)) {
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+        }
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt) {
+            const int vr = dt * 32 + col;
+#pragma unroll
+            for (int sp = 0; sp < 2; ++sp) {   // keys 16sp + 8hi .. +7: one 16-B granule of the V^T row
+                const half8 va = *(const half8 *) (sV + 2 * KIMG + vr * VROW + (((2 * sp + hi) ^ ((vr >> 2) & 3)) << 4));
+                o[dt] = mma32<false>(va, pf[sp], o[dt]);
+            }
+        }
+        sc = sn;
+        __syncthreads();   // tile t+2 landed (vmcnt(0) in the barrier); every wave done with tile t's stage
+    };
+
+    dma_tile(ldsA, 0);
+    if (ntiles > 1) dma_tile(ldsB, 1);
+    asm volatile("" :: "v"(qh[0]), "v"(qh[1]), "v"(qh[2]), "v"(qh[3]), "v"(ql[0]), "v"(ql[1]), "v"(ql[2]), "v"(ql[3]));
+    __syncthreads();
+    sc = qk(ldsA);
+    for (int t = 0; t < ntiles; t += 3) {
+        iter(ldsB, ldsA, ldsC, t);
+        if (t + 1 >= ntiles) break;
+        iter(ldsC, ldsB, ldsA, t + 1);
+        if (t + 2 >= ntiles) break;
+        iter(ldsA, ldsC, ldsB, t + 2);
+    }
+
+    float l_tot;
+    {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run), __float_as_uint(l_run), false, false);
+        l_tot = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
     const float inv = 1.0f / l_tot;
     const int q = q0 + col;
     if (q < T) {
@@ -683,7 +1053,11 @@ hipError_t q2a_launch_attention(const q2a_attn_args & a, hipStream_t s) {
         // F32-class default: k_attn_g (K/V by LDS-DMA, three workgroups per CU: 52 -> 49 ms/step at 64 clips);
         // Q2A_ATTN_G=0 runs the register-staged k_attn (A/B)
         static const bool g = [] { const char * v = getenv("Q2A_ATTN_G"); return !v || atoi(v); }();
-        if (g && terms == 3) hipLaunchKernelGGL(k_attn_g, grid, dim3(256), 0, s, a);
+        static const bool g32 = [] { const char * v = getenv("Q2A_ATTN_G32"); return v && atoi(v); }();
+        static const bool p32 = [] { const char * v = getenv("Q2A_ATTN_P32"); return v && atoi(v); }();
+        if (g && p32 && terms == 3) hipLaunchKernelGGL(k_attn_p32, grid, dim3(256), 0, s, a);
+        else if (g && g32 && terms == 3) hipLaunchKernelGGL(k_attn_g32, grid, dim3(256), 0, s, a);
+        else if (g && terms == 3) hipLaunchKernelGGL(k_attn_g, grid, dim3(256), 0, s, a);
         else if (terms == 2) hipLaunchKernelGGL((k_attn<false, 2>), grid, dim3(256), 0, s, a);
         else if (terms == 1) hipLaunchKernelGGL((k_attn<false, 1>), grid, dim3(256), 0, s, a);
         else hipLaunchKernelGGL(k_attn<false>, grid, dim3(256), 0, s, a);
