@@ -10,7 +10,7 @@ d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 print(sys.argv[1], d['ms_per_step'], 'attention', d['per_kernel']['attention']['ms_per_step'])" $1; }
 for i in 1 2; do
   timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/u_base.json && s gpurun_out/u_base.json || exit 1
-  for v in av_nosm av_nopv av_none; do
+  for v in av_nosm av_noexp; do
     Q2A_DIAG_BUILD=1 Q2A_LIB_PATH=diag/$v/libq2a.so timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/u_$v.json && s gpurun_out/u_$v.json || exit 1
   done
 done

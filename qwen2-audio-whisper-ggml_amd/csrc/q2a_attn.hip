@@ -263,6 +263,26 @@ struct attn_lds_g {
 // of lane half hi is (r&3) + 8(r>>2) + 4hi, so register r then holds key 16(r>>3) + 8hi + (r&7): the 8 keys a lane
 // half feeds the P.V MFMA as one B fragment are contiguous, and their V^T operand is ONE 16-B LDS read instead of
 // two 8-B reads and a register shuffle (softmax is order-free over the keys of a tile)
+// exp2 of x <= 0 on the FMA pipe instead of the transcendental unit (v_exp_f32 is the softmax's bottleneck: ~17
+// cycles per wave instruction, not overlapped with the MFMAs — profiles/r02q_attention_sq.json). x rounded to the
+// nearest integer n by the 1.5*2^23 shift, f = x - n in [-0.5, 0.5], 2^f by a degree-5 polynomial (relative error
+// 3.4e-7 in fp32 Horner, vs ~1 ulp for v_exp_f32), n added to the exponent bits. x is clamped at -125 (2^-125 is 0
+// once P is rounded to fp16 and nothing against the row sum).
+__device__ __forceinline__ float exp2_poly(float x) {
+    x = fmaxf(x, -125.0f);
+    const float t = x + 12582912.0f;
+    const float f = x - (t - 12582912.0f);
+    float p = __builtin_fmaf(0.0012915669940412045f, f, 0.009668530896306038f);
+    p = __builtin_fmaf(p, f, 0.055516887456178665f);
+    p = __builtin_fmaf(p, f, 0.24022264778614044f);
+    p = __builtin_fmaf(p, f, 0.6931464672088623f);
+    p = __builtin_fmaf(p, f, 1.0f);
+    return __uint_as_float(__float_as_uint(p) + (__float_as_uint(t) << 23));
+}
+// Q2A_ATTN_POLY: how many of every 16 score exponentials of a lane go through exp2_poly (the rest v_exp_f32)
+#ifndef Q2A_ATTN_POLY
+#define Q2A_ATTN_POLY 0
+#endif
 __device__ __forceinline__ int kperm(int c) { return (c & ~12) | ((c & 4) << 1) | ((c & 8) >> 1); }
 // max of x over lanes l and l ^ 32: v_permlane32_swap exchanges the two wave halves in a VALU slot (no LDS round
 // trip as ds_bpermute, no lgkmcnt wait); one of the two results is the lane's own value (attention -1 %, same box)
@@ -284,6 +304,9 @@ __device__ __forceinline__ float max_lane32(float x) {
 #endif
 #ifndef Q2A_ATTN_DIAG_NOSM
 #define Q2A_ATTN_DIAG_NOSM 0   // diagnostic builds only (diag/build_attn_variant.sh): no softmax VALU
+#endif
+#ifndef Q2A_ATTN_DIAG_NOEXP
+#define Q2A_ATTN_DIAG_NOEXP 0  // diagnostic builds only: exp2 of the scores replaced by a multiply
 #endif
 #ifndef Q2A_ATTN_DIAG_NOPV
 #define Q2A_ATTN_DIAG_NOPV 0   // diagnostic builds only: no P.V MFMAs
@@ -396,7 +419,12 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-                const float pv = __builtin_amdgcn_exp2f(fmaf(sc[kb][r], L2E, nm));
+#if Q2A_ATTN_DIAG_NOEXP   // diagnostic: the transcendental replaced by a multiply (wrong values on purpose)
+                const float pv = fmaf(sc[kb][r], L2E, nm) * 0.01f;
+#else
+                const float xr = fmaf(sc[kb][r], L2E, nm);
+                const float pv = (r & 3) < Q2A_ATTN_POLY / 4 ? exp2_poly(xr) : __builtin_amdgcn_exp2f(xr);
+#endif
                 ls += pv;
                 pf[kb][r >> 3][r & 7] = (_Float16) pv;
             }
@@ -791,6 +819,182 @@ __global__ __launch_bounds__(256, Q2A_ATTN_P32_OCC) void k_attn_p32(const q2a_at
     }
 }
 
+// ---- F32-class ping-pong on 32-key tiles (k_attn_pp32). The timing decomposition of k_attn_g (profiles/
+// r02q_attention_sq.json) shows the online-softmax VALU adding its full time to the MFMA time: within one wave they
+// are dependent, and the co-resident waves of other workgroups do not fill the gaps. Here one 512-thread workgroup =
+// 8 waves x 32 queries (256 queries of one (clip, head)); waves w and w + 4 share a SIMD and run the same loop one
+// segment apart (group B starts after one extra barrier), so in every segment one of them issues MFMAs
+// (P.V of tile t-1 + QK^T of tile t: 16 MFMAs) while the other runs the softmax of its tile. k_attn_g32's per-32-key
+// arithmetic (same MFMA order, same exp2 / fp16 P, max, row sums), so the output equals k_attn_g32's bit for bit.
+// The 32-key tiles keep 16 score registers live: <= 128 VGPRs, two workgroups (16 waves) per CU. Three LDS stages of
+// 12 KiB (36 KiB per workgroup): group A DMAs tile t+1 at the start of its MFMA segment t and waits for it before
+// the barrier that ends its softmax segment t, two segments later. LDS reads use integer LDS addresses (the compiler
+// would otherwise guard them with vmcnt(0) against the DMA in flight), barriers are raw s_barrier.
+#ifndef Q2A_ATTN_PP32_PRIO
+#define Q2A_ATTN_PP32_PRIO 1   // static s_setprio 1 for group B (MI355X_MICROARCH.md, two waves per SIMD, item 4)
+#endif
+__global__ __launch_bounds__(512, 2) void k_attn_pp32(const q2a_attn_args p) {
+    constexpr int KROW = 128, VROW = 64;
+    constexpr int KIMG = KT32 * KROW, VIMG = 64 * VROW, STAGE = 2 * KIMG + VIMG;
+    __shared__ __attribute__((aligned(16))) char lds[3 * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int grp = wave >> 2, gw = wave & 3;
+    const int T = p.T, D = p.D;
+    const int nq = (T + 255) / 256, total = (int) gridDim.x;
+    const int L = (int) blockIdx.x;
+    const int w = (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);   // XCD-contiguous work order (k_attn)
+    const int qt = w % nq, h = (w / nq) % p.H, clip = w / (nq * p.H);
+    const int q0 = qt * 256 + wave * 32;
+    const int64_t rowbase = (int64_t) clip * T;
+    const int hi = lane >> 5, col = lane & 31;
+
+    half8 qh[4], ql[4];
+    {
+        const int q = min(q0 + col, T - 1);
+        const q2a_half * sh = p.qh + (rowbase + q) * D + h * 64 + 8 * hi;
+        const q2a_half * sl = p.ql + (rowbase + q) * D + h * 64 + 8 * hi;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            qh[s] = *(const half8 *) (sh + 16 * s);
+            ql[s] = *(const half8 *) (sl + 16 * s);
+        }
+    }
+    const char * khb = (const char *) (p.kh + rowbase * D + h * 64);
+    const char * klb = (const char *) (p.kl + rowbase * D + h * 64);
+    const char * vtb = (const char *) (p.vt + ((int64_t) clip * p.H + h) * 64 * p.TP);
+    // group A's wave gw DMAs rows 8gw .. +7 of the K hi / K lo images and rows 16gw .. +15 of the V^T image
+    const int krow_d = 8 * gw + (lane >> 3), kg = (lane & 7) ^ ((krow_d >> 1) & 7);
+    const int vrow_d = 16 * gw + (lane >> 2), vg = (lane & 3) ^ ((vrow_d >> 2) & 3);
+    auto dma_tile = [&](int t) {
+        char * st = lds + (t % 3) * STAGE;
+        const int key = min(t * KT32 + krow_d, T - 1);
+        const uint32_t ko = (uint32_t) (key * D + kg * 8) * 2u;
+        const uint32_t vo = (uint32_t) (vrow_d * p.TP + t * KT32 + vg * 8) * 2u;
+        __builtin_amdgcn_global_load_lds((const void *) (khb + ko), (lds_ptr_t) (st + gw * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void *) (klb + ko), (lds_ptr_t) (st + KIMG + gw * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void *) (vtb + vo), (lds_ptr_t) (st + 2 * KIMG + gw * 1024), 16, 0, 0);
+    };
+    typedef const __attribute__((address_space(3))) half8 * lds_h8p;
+    const uint32_t lds0 = (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) char *) lds;
+    const int krow = kperm(col);
+
+    f16v o[2];
+#pragma unroll
+    for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+    float m_run = -1e30f, l_run = 0.f;
+    const int ntiles = (T + KT32 - 1) / KT32;
+    f16v sc;
+    half8 pf[2];
+
+    auto barrier = [&]() {
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+    };
+    // MFMA segment t: P.V of tile t-1 (its V^T in stage (t-1)%3), QK^T of tile t (stage t%3)
+    auto mfma_seg = [&](int t) {
+        if (t >= 1) {
+            const uint32_t sv = lds0 + ((t - 1) % 3) * STAGE + 2 * KIMG;
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt) {
+                const int vr = dt * 32 + col;
+#pragma unroll
+                for (int sp = 0; sp < 2; ++sp) {
+                    const half8 va = *(lds_h8p) (uintptr_t) (sv + vr * VROW + (((2 * sp + hi) ^ ((vr >> 2) & 3)) << 4));
+                    o[dt] = mma32<false>(va, pf[sp], o[dt]);
+                }
+            }
+        }
+        if (t < ntiles) {
+            const uint32_t sk = lds0 + (t % 3) * STAGE;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sc[r] = 0.f;
+#pragma unroll
+            for (int st = 0; st < 4; ++st) {
+                const uint32_t off = (uint32_t) (krow * KROW + attn_lds_g::k(krow, 2 * st + hi));
+                const half8 ah = *(lds_h8p) (uintptr_t) (sk + off);
+                sc = mma32<false>(ah, qh[st], sc);
+                const half8 al = *(lds_h8p) (uintptr_t) (sk + KIMG + off);
+                sc = mma32<false>(al, qh[st], sc);
+                sc = mma32<false>(ah, ql[st], sc);
+            }
+        }
+    };
+    // VALU segment t: online-softmax update of tile t's scores (k_attn_g32's operations), P into pf
+    auto valu_seg = [&](int t) {
+        if (t == ntiles - 1) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                if (t * KT32 + 16 * (r >> 3) + 8 * hi + (r & 7) >= T) sc[r] = -1e30f;
+        }
+        float mx = sc[0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, sc[r]);
+        mx = max_lane32(mx);
+        const float m_new = fmaxf(m_run, mx);
+        const float nm = -m_new * L2E;
+        const float alpha = __builtin_amdgcn_exp2f(fmaf(m_run, L2E, nm));
+        float ls = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const float pv = __builtin_amdgcn_exp2f(fmaf(sc[r], L2E, nm));
+            ls += pv;
+            pf[r >> 3][r & 7] = (_Float16) pv;
+        }
+        l_run = l_run * alpha + ls;
+        m_run = m_new;
+        if (__any(alpha != 1.0f)) {
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+        }
+    };
+
+    if (grp == 0) dma_tile(0);
+    asm volatile("" :: "v"(qh[0]), "v"(qh[1]), "v"(qh[2]), "v"(qh[3]), "v"(ql[0]), "v"(ql[1]), "v"(ql[2]), "v"(ql[3]));
+    __syncthreads();
+    if (Q2A_ATTN_PP32_PRIO && grp == 1) __builtin_amdgcn_s_setprio(1);
+    if (grp == 1) barrier();   // group B runs one segment behind
+    for (int t = 0; t <= ntiles; ++t) {
+        if (grp == 0 && t + 1 < ntiles) dma_tile(t + 1);   // stage (t+1)%3: its last reader (B's P.V of t-2) is done
+        mfma_seg(t);
+        barrier();
+        if (t < ntiles) valu_seg(t);
+        if (grp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tile t+1 landed before the next barrier
+        barrier();
+    }
+    if (grp == 0) barrier();
+    if (Q2A_ATTN_PP32_PRIO && grp == 1) __builtin_amdgcn_s_setprio(0);
+
+    float l_tot;
+    {
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(l_run), __float_as_uint(l_run), false, false);
+        l_tot = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+    const float inv = 1.0f / l_tot;
+    const int q = q0 + col;
+    if (q < T) {
+        const int64_t orow = (rowbase + q) * D + h * 64;
+#pragma unroll
+        for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const int d = dt * 32 + 8 * g + 4 * hi;
+                const float v0 = o[dt][4 * g + 0] * inv, v1 = o[dt][4 * g + 1] * inv;
+                const float v2 = o[dt][4 * g + 2] * inv, v3 = o[dt][4 * g + 3] * inv;
+                if (p.outH) {
+                    const half4 hv = {(_Float16) v0, (_Float16) v1, (_Float16) v2, (_Float16) v3};
+                    *(half4 *) (p.outH + orow + d) = hv;
+                } else {
+                    *(float4 *) (p.outF + orow + d) = make_float4(v0, v1, v2, v3);
+                }
+            }
+    }
+}
+
 // ---- ping-pong variant (default): one 512-thread workgroup = 8 waves x 32 queries (256 queries of one (clip, head)),
 // the two waves that share a SIMD (w and w + 4) run the same loop one segment apart: while group A (waves 0-3) is in
 // its MFMA segment (P.V of the previous tile + QK^T of this one, 32 MFMAs) group B (waves 4-7) is in its VALU segment
@@ -1055,6 +1259,11 @@ hipError_t q2a_launch_attention(const q2a_attn_args & a, hipStream_t s) {
         static const bool g = [] { const char * v = getenv("Q2A_ATTN_G"); return !v || atoi(v); }();
         static const bool g32 = [] { const char * v = getenv("Q2A_ATTN_G32"); return v && atoi(v); }();
         static const bool p32 = [] { const char * v = getenv("Q2A_ATTN_P32"); return v && atoi(v); }();
+        static const bool ppk32 = [] { const char * v = getenv("Q2A_ATTN_PP32"); return v && atoi(v); }();
+        if (g && ppk32 && terms == 3) {
+            hipLaunchKernelGGL(k_attn_pp32, dim3(((a.T + 255) / 256) * a.H * a.n_clips), dim3(512), 0, s, a);
+            return hipGetLastError();
+        }
         if (g && p32 && terms == 3) hipLaunchKernelGGL(k_attn_p32, grid, dim3(256), 0, s, a);
         else if (g && g32 && terms == 3) hipLaunchKernelGGL(k_attn_g32, grid, dim3(256), 0, s, a);
         else if (g && terms == 3) hipLaunchKernelGGL(k_attn_g, grid, dim3(256), 0, s, a);
