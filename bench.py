@@ -36,6 +36,7 @@ CONFIGS = {
     "q4k64": ("q4_k", 64, "configs[2]: batch=64 30 s clips, Q4_K quantized weights, 1xMI355X per rank"),
     "f16x1": ("f16", 1, "configs[1]: single 30 s synthetic 16 kHz clip, fp16 weights, 1xMI355X per rank"),
     "f16x64": ("f16", 64, "batch=64 30 s clips, fp16 weights (F16 path at the configs[2] batch)"),
+    "q4kx1": ("q4_k", 1, "single 30 s synthetic 16 kHz clip, Q4_K weights (the configs[2] contract at batch 1)"),
     "q80x64": ("q8_0", 64, "batch=64 30 s clips, Q8_0 weights (exact Q8_0 x Q8_0 contract)"),
     # configs[4] per rank: Q8_0 file, weights dequantized to bf16, bf16 inter-op activations (Q2A_ACT_BF16)
     "q80bf16x64": ("q8_0", 64, "configs[4] per rank: batch=64 30 s clips (512 over 8 GPUs), Q8_0 weights + bf16 "
@@ -175,6 +176,18 @@ def host_cpu_info() -> dict:
     except Exception:  # noqa: BLE001
         pass
     return info
+
+
+def fc1_kernel_label(wt: str, bf16: bool, M: int) -> str:
+    """The k_gemm instantiation the engine launches for fc1 (N = 5120, K = 1280), mirroring q2a_gemm.hip's tile
+    regimes: 256x256 8-phase tiles once ceil(M/256) x 20 tiles >= 512 (M >= 6401), else 128x128 two-stage tiles."""
+    epi = "GELU_H" if (bf16 or wt != "q4_k") else "PRE_H"
+    blk = "BF16" if bf16 else {"q4_k": "256", "f16": "0", "q8_0": "32"}[wt]
+    if (M + 255) // 256 * 20 >= 512 and blk != "32":
+        return f"k_gemm<256,256,2,4,{epi},{blk},1>"
+    if (M + 255) // 256 * 20 >= 512:
+        return f"k_gemm<128,256,2,4,{epi},{blk},0>"
+    return f"k_gemm<128,128,2,2,{epi},{blk},0>"
 
 
 def main():
@@ -365,9 +378,8 @@ def main():
                    "seq_len": T_MEL, "parallelism": f"dp{ws}"},
         "clips_per_s": round(total_clips / elapsed, 3),
         "tflops_total": round(FLOP_PER_CLIP * total_clips / elapsed / 1e12, 1),
-        "roofline": {"bound": "mfma", "kernel": "gemm_fc1 (k_gemm<256,256,2,4,%s>), M=%d N=5120 K=1280" % (
-                         {"q4_k": "PRE_H,256,1", "f16": "GELU_H,0,1", "q8_0": "GELU_H,32,0"}[wt] if "bf16" not in args.config
-                         else "GELU_H,BF16,1", T * clips_per_gpu),
+        "roofline": {"bound": "mfma", "kernel": "gemm_fc1 (%s), M=%d N=5120 K=1280" % (fc1_kernel_label(
+                         wt, "bf16" in args.config, T * clips_per_gpu), T * clips_per_gpu),
                      "achieved": round(achieved, 1), "peak": PEAK_FP16_MFMA_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_FP16_MFMA_TFLOPS, 4), "traffic": traffic,
                      "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
