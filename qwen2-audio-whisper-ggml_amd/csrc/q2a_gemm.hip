@@ -1240,7 +1240,8 @@ hipError_t launch_cfg(const q2a_gemm_args & a, hipStream_t s) {
 // small M (one or a few clips): 64-row tiles when 128x128 tiles would leave CUs idle
 bool narrow_tiles(int M, int N) {
     static const int off = [] { const char * v = getenv("Q2A_GEMM_NO_NARROW"); return v ? atoi(v) : 0; }();
-    return !off && (int64_t) ((M + 127) / 128) * (N / 128) < 256;
+    static const int all = [] { const char * v = getenv("Q2A_GEMM_NARROW_ALL"); return v ? atoi(v) : 0; }();
+    return !off && (all || (int64_t) ((M + 127) / 128) * (N / 128) < 256);
 }
 
 bool wide_tiles(int M, int N) {
