@@ -504,13 +504,19 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     constexpr int SBP = BLK == 256 ? (SB + 1023) / 1024 : 0;          // 1 KiB pieces per Q4_K block
     constexpr int SP = BLK == 256 ? (SBP + NW - 1) / NW : 0;          // K-steps per block that issue a piece
     static_assert(BLK != 256 || SP <= 4, "Q4_K scale pieces must fit the block's 4 K-steps");
-    constexpr int SCALE_LDS = BLK == 256 ? (2 * SBP + NW) * 1024 : BLK ? NSB * SB : 0;
+    // the two-stage 128-row Q4_K tiles keep ONE scale buffer: block b+1's pieces are issued on steps 4b+1 .. 4b+SP,
+    // after the barrier that ends block b's start (the only reader of block b's scales besides the final multiply of
+    // the last block), and land within their step (NS = 2 drains every step). 90 -> 79 KiB of LDS for 128x128, so two
+    // workgroups share a CU as in the F16 tiles (a single clip's QKV / fc1 GEMMs are latency-bound at one per CU)
+    constexpr int NBUF = (BLK == 256 && !PIPE && BM > 64) ? 1 : 2;
+    constexpr int SCALE_LDS = BLK == 256 ? (NBUF * SBP + NW) * 1024 : BLK ? NSB * SB : 0;
     constexpr int NS_FIT = (150 * 1024 - SCALE_LDS) / OPB;
     constexpr int NS_MAX = BLK == 256 ? 6 - SP : 5;
     // deep pipelines only on the narrow 64-row tiles (grids under one workgroup per CU); the 128-row tiles keep two
     // stages so two workgroups share a CU (their grids have several tiles per CU)
     constexpr int NS = PIPE || BLK == 32 || BM > 64 ? 2 : (NS_FIT >= NS_MAX ? NS_MAX : NS_FIT >= 2 ? NS_FIT : 2);
     static_assert(PIPE || BLK != 256 || SP + NS <= 6, "Q4_K scale prefetch distance");
+    static_assert(NBUF == 2 || (NS == 2 && SP <= 3), "single Q4_K scale buffer: pieces on steps 4b+1 .. 4b+3");
     constexpr int LDS_MAIN = PIPE ? (BLK ? SBUF_OFF + SBUF_BYTES : 2 * OPB) : NS * OPB + SCALE_LDS;
     constexpr int LDS_BYTES = LDS_MAIN > EPI_OFF + NW * EPI_WREG ? LDS_MAIN : EPI_OFF + NW * EPI_WREG;
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
@@ -608,8 +614,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
             const int c = q * 64 + lane;
             const bool real = q < SBP && g < p.K / 256 && c < SB / 16;
             const uint4 * src = real ? scale_src(c, g) : (const uint4 *) p.dy + lane;
-            char * dst = real ? sbuf + (g & 1) * SBP * 1024 + q * 1024 : sbuf + 2 * SBP * 1024 + wave * 1024;
-            if (q >= SBP || g >= p.K / 256) dst = sbuf + 2 * SBP * 1024 + wave * 1024;
+            char * dst = real ? sbuf + (g & (NBUF - 1)) * SBP * 1024 + q * 1024 : sbuf + NBUF * SBP * 1024 + wave * 1024;
+            if (q >= SBP || g >= p.K / 256) dst = sbuf + NBUF * SBP * 1024 + wave * 1024;
             __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) dst, 16, 0, 0);
         };
         uint4 sreg[BLK == 32 ? SCH : 1];
@@ -695,8 +701,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
             // Q8_0: the next K-step's two blocks are fetched one step ahead into the other buffer.
             bool sload = false;
             if (BLK == 256) {
-                if (kt % 4 == 0) kq_block_start(sbuf + ((kt / 4) & 1) * SBP * 1024);
-                if (kt % 4 < SP) scale_piece((kt % 4) * NW + wave, kt / 4 + 1);   // uniform: one per wave
+                if (kt % 4 == 0) kq_block_start(sbuf + ((kt / 4) & (NBUF - 1)) * SBP * 1024);
+                if (NBUF == 2 && kt % 4 < SP) scale_piece((kt % 4) * NW + wave, kt / 4 + 1);   // uniform: one per wave
+                if (NBUF == 1 && kt % 4 >= 1 && kt % 4 <= SP) scale_piece((kt % 4 - 1) * NW + wave, kt / 4 + 1);
             } else if (BLK == 32 && kt + 1 < nk) {
                 sload = true;
                 scale_load(gb0 + kt + 1);
@@ -773,7 +780,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if constexpr (BLK == 256) {
             // acc is in units of the last block's scale: multiply by dy_last[m] * dx_last[n]
-            const char * sb = sbuf + ((nkb - 1) & 1) * SBP * 1024;
+            const char * sb = sbuf + ((nkb - 1) & (NBUF - 1)) * SBP * 1024;
             const float * s_dy = (const float *) sb + BM;
             const float * s_dx = (const float *) (sb + BM * 40 + BN * 8);
     #pragma unroll
