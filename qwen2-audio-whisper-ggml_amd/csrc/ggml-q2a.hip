@@ -887,6 +887,16 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
         a.W2 = (const q2a_half *) sec->w->data;
         a.bias2 = sec->bias; a.store_bias2 = sec->bias != nullptr;
         a.outF2 = (float *) sec->out->data; a.out_scale2 = sec->oscale;
+        if (blk == 256) {   // the second weight's packed image: operand and block scales like the first's below
+            const packed_w p2 = get_packed(b, sec->w);
+            const char * base2 = (const char *) p2.dev;
+            a.W2 = (const q2a_half *) (base2 + p2.off[0]);
+            a.dx2 = (const float *) (base2 + p2.off[1]);
+            a.dmin2 = (const float *) (base2 + p2.off[2]);
+            a.wext2 = (const q2a_half *) (base2 + p2.off[3]);
+            a.beta2 = (const float *) (base2 + p2.off[4]);
+            a.gamma2 = (const float *) (base2 + p2.off[5]);
+        }
     }
     if (split) {
         a.part = (float *) (s + a_bytes + dy_bytes + ae_bytes);
@@ -1335,7 +1345,8 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                 while (node(j2) && is_view_op(node(j2))) ++j2;
                 ggml_tensor * m2 = node(j2);
                 if (c1.epi == Q2A_EPI_STORE_F && !no_fuse && m2 && m2->op == GGML_OP_MUL_MAT && m2->src[1] == op->src[1] &&
-                    op->src[0]->type == GGML_TYPE_F16 && m2->src[0]->type == GGML_TYPE_F16 && mm_fast_ok(m2) &&
+                    (op->src[0]->type == GGML_TYPE_F16 || op->src[0]->type == GGML_TYPE_Q4_K) &&
+                    m2->src[0]->type == op->src[0]->type && mm_fast_ok(m2) &&
                     !match_attention(g, j2) && ggml_are_same_shape(m2->src[0], op->src[0]) && !mm_is_pipe8(op)) {
                     const mm_chain c2 = chain_of(j2);
                     if (c2.epi == Q2A_EPI_STORE_F) {

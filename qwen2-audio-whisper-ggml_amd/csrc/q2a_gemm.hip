@@ -533,7 +533,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (__builtin_amdgcn_s_memrealtime() - t0 < dt) __builtin_amdgcn_s_sleep(8);
     }
-    constexpr bool GROUPABLE = !PIPE && !BF && BLK == 0 && EPI == Q2A_EPI_STORE_F;
+    constexpr bool GROUPABLE = !PIPE && !BF && (BLK == 0 || BLK == 256) && EPI == Q2A_EPI_STORE_F;
     const int ngrp = (GROUPABLE && p.ngroup == 2) ? 2 : 1;
     const int ksplit = (!PIPE && (BLK == 0 || BLK == 32) && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) &&
                         p.ksplit > 1 && ngrp == 1) ? p.ksplit : 1;
@@ -544,6 +544,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
         if (ngrp == 2 && wgid_all >= ntl) {
             wgid_all -= ntl;
             p.W = p.W2; p.bias = p.bias2; p.outF = p.outF2; p.out_scale = p.out_scale2; p.store_bias = p.store_bias2;
+            if constexpr (BLK == 256) { p.dx = p.dx2; p.dmin = p.dmin2; p.beta = p.beta2; p.gamma = p.gamma2; p.wext = p.wext2; }
         }
     }
     const int ks = wgid_all / ntl, wgid = wgid_all - ks * ntl;   // K-split index, tile index
@@ -1227,7 +1228,7 @@ __global__ void k_split_reduce(const float * __restrict__ part, int S, int64_t s
 
 template <int BM, int BN, int WM, int WN, int EPI, int BLK, int PIPE = 0>
 hipError_t launch_cfg(const q2a_gemm_args & a, hipStream_t s) {
-    const bool grouped = !PIPE && BLK == 0 && EPI == Q2A_EPI_STORE_F && a.ngroup == 2;
+    const bool grouped = !PIPE && (BLK == 0 || BLK == 256) && EPI == Q2A_EPI_STORE_F && a.ngroup == 2;
     const bool split = !PIPE && (BLK == 0 || BLK == Q2A_BLK_BF16 || BLK == 32) &&
                        (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) && a.ksplit > 1 && !grouped;
     const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM) * (split ? a.ksplit : 1) * (grouped ? 2 : 1);
@@ -1349,7 +1350,8 @@ hipError_t q2a_launch_gemm(const q2a_gemm_args & a_in, int epi, int blk, hipStre
     q2a_gemm_args a = a_in;
     a.stagger_ns = st_ns; a.stagger_g = st_g;
     a.group_m = grp;
-    if (a.ngroup == 2 && (epi != Q2A_EPI_STORE_F || blk != 0 || wide_tiles(a.M, a.N))) return hipErrorInvalidValue;
+    if (a.ngroup == 2 && (epi != Q2A_EPI_STORE_F || (blk != 0 && blk != 256) || wide_tiles(a.M, a.N))) return hipErrorInvalidValue;
+    if (a.ngroup == 2 && blk == 256 && (!a.dx2 || !a.beta2 || !a.gamma2 || !a.wext2)) return hipErrorInvalidValue;
     if (!(epi == Q2A_EPI_RESID || (epi == Q2A_EPI_STORE_F && a.split_store)) || !a.part || a.ldo != a.N || a.ngroup == 2)
         a.ksplit = 0;
     else if (blk == 256 || blk == 32) a.ksplit = a.split_kq ? q2a_gemm_kq_ksplit(a.M, a.N, a.K, blk) : 0;

@@ -75,14 +75,20 @@ struct q2a_gemm_args {
     int store_bias;                   // Q2A_EPI_STORE_F: 1 = outF = acc + bias[n], 0 = raw accumulators
     float out_scale;                  // Q2A_EPI_STORE_F: != 0 -> outF = (acc [+ bias]) * out_scale (ggml_scale after the add)
     int split_store;                  // Q2A_EPI_STORE_F: 1 = allow the small-tile split-K (part/split_stride) like RESID
-    // Q2A_EPI_STORE_F, small tiles, fp16 weights: ngroup = 2 runs a second GEMM with the same A, M, N, K in the same
-    // launch (its own W / bias / output / scale), e.g. the K and Q projections of one layer; no split-K then
+    // Q2A_EPI_STORE_F, small tiles, fp16 or Q4_K weights: ngroup = 2 runs a second GEMM with the same A (and, for
+    // Q4_K, the same Q8_K activation scales), M, N, K in the same launch (its own W / bias / output / scale and
+    // weight block scales), e.g. the K and Q projections of one layer; no split-K then
     int ngroup;
     const q2a_half * W2;
     const float * bias2;
     float * outF2;
     float out_scale2;
     int store_bias2;
+    const float * dx2;                // Q4_K second weight: dx / dmin / beta / gamma / wext like the first
+    const float * dmin2;
+    const float * beta2;
+    const float * gamma2;
+    const q2a_half * wext2;
     int split_kq;                     // allow the small-tile split-K for k-quant / Q8_0 / Q4_0 weights (q2a_gemm_kq_ksplit)
 };
 

@@ -115,8 +115,8 @@ def test_backend_fusions_match_per_node(harness, make_model, make_clip, tmp_path
     # the attention output CONT;
     # plus the final LayerNorm affine
     assert info_f["fused"] == 14 * L + 2, info_f
-    # the K and Q projections of each layer run as one grouped launch (F16 weights)
-    assert info_f["mm_grouped"] == (L if wt == "f16" else 0), info_f
+    # the K and Q projections of each layer run as one grouped launch (F16 and Q4_K weights)
+    assert info_f["mm_grouped"] == (L if wt in ("f16", "q4_k") else 0), info_f
     assert info_f["other"] < info_p["other"], (info_f, info_p)
     assert np.array_equal(fused, plain)
 
