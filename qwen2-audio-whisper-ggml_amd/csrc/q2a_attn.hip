@@ -302,6 +302,9 @@ __device__ __forceinline__ float max_lane32(float x) {
 #ifndef Q2A_ATTN_PRIO
 #define Q2A_ATTN_PRIO 0
 #endif
+#ifndef Q2A_ATTN_KPF
+#define Q2A_ATTN_KPF 1   // k_attn_g: both 32-key QK^T chains per 16-deep step (136 VGPRs; 0 = chain after chain, 163)
+#endif
 #ifndef Q2A_ATTN_DIAG_NOSM
 #define Q2A_ATTN_DIAG_NOSM 0   // diagnostic builds only (diag/build_attn_variant.sh): no softmax VALU
 #endif
@@ -372,6 +375,35 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
         const char * vt_img = kh_img + 2 * KIMG;
         f16v sc[2];
         if (Q2A_ATTN_PRIO >= 1) __builtin_amdgcn_s_setprio(1);
+#if Q2A_ATTN_KPF
+        // K fragments one 16-deep step ahead: the reads of step st+1 (both 32-key halves) are issued before the MFMAs
+        // of step st, so each MFMA group waits only for its own reads (lgkmcnt(4), not 0); same MFMA order per chain
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) sc[kb][r] = 0.f;
+        half8 fh[2], fl[2];
+        auto rdk = [&](int st, int kb, half8 & h, half8 & l) {
+            const int krow = kb * 32 + kperm(col);
+            const int off = krow * KROW + LY::k(krow, 2 * st + hi);
+            h = *(const half8 *) (kh_img + off);
+            l = *(const half8 *) (kl_img + off);
+        };
+        rdk(0, 0, fh[0], fl[0]);
+        rdk(0, 1, fh[1], fl[1]);
+#pragma unroll
+        for (int st = 0; st < 4; ++st) {
+            half8 nh[2], nl[2];
+            if (st < 3) { rdk(st + 1, 0, nh[0], nl[0]); rdk(st + 1, 1, nh[1], nl[1]); }
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) {
+                sc[kb] = mma32<false>(fh[kb], qh[st], sc[kb]);
+                sc[kb] = mma32<false>(fl[kb], qh[st], sc[kb]);
+                sc[kb] = mma32<false>(fh[kb], ql[st], sc[kb]);
+            }
+            if (st < 3) { fh[0] = nh[0]; fh[1] = nh[1]; fl[0] = nl[0]; fl[1] = nl[1]; }
+        }
+#else
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
@@ -387,6 +419,7 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
                 sc[kb] = mma32<false>(ah, ql[st], sc[kb]);
             }
         }
+#endif
         if (Q2A_ATTN_PRIO >= 1) __builtin_amdgcn_s_setprio(0);
         if (t == ntiles - 1) {   // keys >= T exist only in the last tile (key of reg r: 16(r>>3) + 8hi + (r&7))
 #pragma unroll
