@@ -21,6 +21,7 @@
 #include "q2a_quant.h"
 
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 namespace {
@@ -145,6 +146,12 @@ __device__ __forceinline__ void kq_rescale2(f4 & a, int h, float al, const f4 & 
     const f2 r = __builtin_elementwise_fma(a2, t, u);
     a[2 * h] = r[0];
     a[2 * h + 1] = r[1];
+}
+// block 0 of the recurrence: acc is 0, so kq_rescale2 reduces to its second product (fma(0, t, u) = u exactly)
+__device__ __forceinline__ void kq_first2(f4 & a, int h, const f4 & nga, const f4 & s2) {
+    const f2 u = f2{nga[2 * h], nga[2 * h + 1]} * f2{s2[2 * h], s2[2 * h + 1]};
+    a[2 * h] = u[0];
+    a[2 * h + 1] = u[1];
 }
 __device__ __forceinline__ float kq_final(float a, float yc, float dx) {
 #pragma clang fp contract(off)
@@ -291,7 +298,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
         const float al = kq_alpha(yp, yc);
         asm volatile("ds_write_b32 %0, %1" :: "v"(sb0 + ALPHA_OFF + row * 4), "v"(al) : "memory");
     };
-    auto block_start = [&]() {
+    auto block_start = [&](auto first) {   // first: std::true_type for block 0 (acc = 0: only the min term)
 #ifdef Q2A_DIAG_NO_RESCALE
         return;   // timing diagnostic only (wrong results)
 #endif
@@ -343,8 +350,10 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #pragma unroll
             for (int j = 0; j < 4; ++j)
 #pragma unroll
-                for (int h = 0; h < 2; ++h)   // kq_rescale two columns per instruction (v_pk_mul / v_pk_fma)
-                    kq_rescale2(acc[i][j], h, al[i % 3], bet[j], gam[j], s2v[i & 1][j]);
+                for (int h = 0; h < 2; ++h) {   // kq_rescale two columns per instruction (v_pk_mul / v_pk_fma)
+                    if constexpr (decltype(first)::value) kq_first2(acc[i][j], h, gam[j], s2v[i & 1][j]);
+                    else kq_rescale2(acc[i][j], h, al[i % 3], bet[j], gam[j], s2v[i & 1][j]);
+                }
             if (i + 2 < 8) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(al[(i + 2) % 3]), "+v"(ae[(i + 2) % 3]));
             __builtin_amdgcn_sched_barrier(0);   // one row block at a time: bounds the live min-term results
         }
@@ -431,7 +440,8 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
         asm volatile("" ::: "memory");
         int kt = 0;
         for (; kt < nk - 4; kt += 4) {
-            block_start();
+            if (kt == 0) block_start(std::true_type{});
+            else block_start(std::false_type{});
             asm volatile("" ::: "memory");
             Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
                       stage(0, 3, kt + 2), 10, 13, 13, 13);
@@ -442,7 +452,8 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             Q2A_KSTEP(1, stage(0, 1, kt + 4), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5), 10, 10, 10, 10);
         }
         // last block: its scales stay in place for the final multiply (the scale re-stage keeps the vmcnt counts)
-        block_start();
+        if (kt == 0) block_start(std::true_type{});
+        else block_start(std::false_type{});
         asm volatile("" ::: "memory");
         Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4)), stage(0, 2, kt + 2),
                   stage(0, 3, kt + 2), 10, 13, 13, 13);
@@ -644,7 +655,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                 for (int j = 0; j < (BLK == 32 ? NJ : 1); ++j) blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
         }
         // Q4_K (BLK = 256): the block-ratio recurrence of the 8-phase kernel (kq_rescale), op for op
-        auto kq_block_start = [&](const char * sb) {
+        auto kq_block_start = [&](const char * sb, auto first) {   // first: std::true_type for block 0 (acc = 0)
             const float * s_dyp = (const float *) sb;
             const float * s_dy = s_dyp + BM;
             const q2a_half * s_ae = (const q2a_half *) (sb + BM * 8);
@@ -669,7 +680,10 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                 for (int j = 0; j < NJ; ++j) {
                     const f4 s2 = __builtin_amdgcn_mfma_f32_16x16x16f16(we[j], ae, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
     #pragma unroll
-                    for (int r = 0; r < 4; ++r) acc[i][j][r] = kq_rescale(acc[i][j][r], al, be[j][r], ga[j][r], s2[r]);
+                    for (int r = 0; r < 4; ++r) {
+                        if constexpr (decltype(first)::value) acc[i][j][r] = ga[j][r] * s2[r];   // = kq_rescale(0, ...)
+                        else acc[i][j][r] = kq_rescale(acc[i][j][r], al, be[j][r], ga[j][r], s2[r]);
+                    }
                 }
             }
         };
@@ -702,7 +716,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
             // Q8_0: the next K-step's two blocks are fetched one step ahead into the other buffer.
             bool sload = false;
             if (BLK == 256) {
-                if (kt % 4 == 0) kq_block_start(sbuf + ((kt / 4) & (NBUF - 1)) * SBP * 1024);
+                if (kt == 0) kq_block_start(sbuf, std::true_type{});
+                else if (kt % 4 == 0) kq_block_start(sbuf + ((kt / 4) & (NBUF - 1)) * SBP * 1024, std::false_type{});
                 if (NBUF == 2 && kt % 4 < SP) scale_piece((kt % 4) * NW + wave, kt / 4 + 1);   // uniform: one per wave
                 if (NBUF == 1 && kt % 4 >= 1 && kt % 4 <= SP) scale_piece((kt % 4 - 1) * NW + wave, kt / 4 + 1);
             } else if (BLK == 32 && kt + 1 < nk) {
