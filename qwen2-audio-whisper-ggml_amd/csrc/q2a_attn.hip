@@ -302,6 +302,12 @@ __device__ __forceinline__ float max_lane32(float x) {
 #ifndef Q2A_ATTN_PRIO
 #define Q2A_ATTN_PRIO 0
 #endif
+#ifndef Q2A_ATTN_LAZY
+#define Q2A_ATTN_LAZY 1   // k_attn_g: lazy re-basing of the softmax max (0 = eager, every tile)
+#endif
+#ifndef Q2A_ATTN_LAZY_TAU
+#define Q2A_ATTN_LAZY_TAU 5.0f
+#endif
 #ifndef Q2A_ATTN_KPF
 #define Q2A_ATTN_KPF 1   // k_attn_g: both 32-key QK^T chains per 16-deep step (136 VGPRs; 0 = chain after chain, 163)
 #endif
@@ -367,7 +373,7 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
     for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
-    float m_run = -1e30f, l_run = 0.f;
+    float m_run = -1e30f, l_run = 0.f, nm_run = 0.f;
     const int ntiles = (T + KT - 1) / KT;
 
     auto tile = [&](const char * kh_img, int t) {
@@ -429,13 +435,12 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
                     if (t * KT + kb * 32 + 16 * (r >> 3) + 8 * hi + (r & 7) >= T) sc[kb][r] = -1e30f;
         }
 #if Q2A_ATTN_DIAG_NOSM   // diagnostic timing build: no max / exp (P = S / 64), wrong values on purpose
-        const float alpha = 1.0f;
-        float ls = 1.0f;
         half8 pf[2][2];
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int r = 0; r < 16; ++r) pf[kb][r >> 3][r & 7] = (_Float16) (sc[kb][r] * 0.015625f);
+        l_run += 1.0f;
 #else
         float mx = sc[0][0];
 #pragma unroll
@@ -443,6 +448,36 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) mx = fmaxf(mx, sc[1][r]);
         mx = max_lane32(mx);
+#if Q2A_ATTN_LAZY && !Q2A_ATTN_DIAG_NOEXP && !Q2A_ATTN_POLY
+        // lazy re-basing: the exponent's reference m_run moves only when some score of the wave's queries exceeds it
+        // by more than Q2A_ATTN_LAZY_TAU (natural-log units: P <= e^TAU in between, well inside fp16), so most tiles
+        // skip the alpha exponential and the O / l rescale (fma(m_run, L2E, -m_new L2E) is the product's rounding
+        // error, not 0, when the max did not move: the eager form multiplied O by 1 + ulp on almost every tile)
+        if (__any(mx > m_run + Q2A_ATTN_LAZY_TAU)) {
+            const float m_new = fmaxf(m_run, mx);
+            const float nm_new = -m_new * L2E;
+            const float alpha = __builtin_amdgcn_exp2f(fmaf(m_run, L2E, nm_new));
+            l_run *= alpha;
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
+            m_run = m_new;
+            nm_run = nm_new;
+        }
+        const float nm = nm_run;
+        float ls = 0.f;
+        half8 pf[2][2];
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const float pv = __builtin_amdgcn_exp2f(fmaf(sc[kb][r], L2E, nm));
+                ls += pv;
+                pf[kb][r >> 3][r & 7] = (_Float16) pv;
+            }
+        l_run += ls;
+#else
         const float m_new = fmaxf(m_run, mx);
         const float nm = -m_new * L2E;
         const float alpha = __builtin_amdgcn_exp2f(fmaf(m_run, L2E, nm));
@@ -461,17 +496,16 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
                 ls += pv;
                 pf[kb][r >> 3][r & 7] = (_Float16) pv;
             }
-#endif
         l_run = l_run * alpha + ls;
-#if !Q2A_ATTN_DIAG_NOSM
         m_run = m_new;
-#endif
         if (__any(alpha != 1.0f)) {
 #pragma unroll
             for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
                 for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
         }
+#endif
+#endif
         if (Q2A_ATTN_PRIO >= 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
