@@ -716,8 +716,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
             // Q8_0: the next K-step's two blocks are fetched one step ahead into the other buffer.
             bool sload = false;
             if (BLK == 256) {
-                if (kt == 0) kq_block_start(sbuf, std::true_type{});
-                else if (kt % 4 == 0) kq_block_start(sbuf + ((kt / 4) & (NBUF - 1)) * SBP * 1024, std::false_type{});
+                // (block 0 through the general form as well: fma(0, t, u) = u is what the 8-phase kernel's block-0
+                // start computes; a second inlined copy here costs 248 -> 272 registers, one workgroup per CU)
+                if (kt % 4 == 0) kq_block_start(sbuf + ((kt / 4) & (NBUF - 1)) * SBP * 1024, std::false_type{});
                 if (NBUF == 2 && kt % 4 < SP) scale_piece((kt % 4) * NW + wave, kt / 4 + 1);   // uniform: one per wave
                 if (NBUF == 1 && kt % 4 >= 1 && kt % 4 <= SP) scale_piece((kt % 4 - 1) * NW + wave, kt / 4 + 1);
             } else if (BLK == 32 && kt + 1 < nk) {
