@@ -139,6 +139,17 @@ int q2a_test_block(q2a_engine * e, int layer, float * x_dev, int n_clips, void *
  * [M][F] (fp16 values for F16 files; Q8_K / Q8_0 integer codes held in fp16 for quantized files). Per-layer
  * divergence trace against the reference's own intermediates (diag/layer_trace.py). */
 int q2a_test_block_taps(q2a_engine * e, int layer, float * x_dev, int n_clips, void * const * taps, void * stream);
+/* Front end only: PCM [n_clips][pcm_stride] (device) -> log-mel -> conv1 + GELU -> conv2 + GELU -> + positions, the
+ * first block's input X [n_clips*T][D] f32 (device) — the reference's embd_conv + pe (qwen2-whisper.cpp:1892-2005). */
+int q2a_test_frontend(q2a_engine * e, const float * pcm_dev, int64_t pcm_stride, const int32_t * n_samples, int n_clips,
+                      float * x_dev, void * stream);
+/* AvgPool1d(2) + final LayerNorm only: X [n_clips*T][D] f32 (device) -> out [n_clips][T/2][D] f32 (device)
+ * (qwen2-whisper.cpp:2157-2181). */
+int q2a_test_pool_ln(q2a_engine * e, const float * x_dev, int n_clips, float * out_dev, void * stream);
+/* Q4_K files: how fc1's output reaches fc2 as Q8_K codes — 0 (default) fp16 pre-activation + GELU inside the
+ * quantizer, 1 GELU in the fc1 epilogue + quantizer, 2 GELU + Q8_K fused into the fc1 epilogue. All three give
+ * identical codes (tests/test_gpu_parity.py::test_deferred_gelu_equals_epilogue_gelu); a test hook, not a tuning knob. */
+int q2a_test_fc1_path(q2a_engine * e, int path);
 /* Attention only: q,k,v [n_clips*T][D] f32 (q already scaled), out [n_clips*T][D] f32. */
 int q2a_test_attention(q2a_engine * e, const float * q_dev, const float * k_dev, const float * v_dev, int n_clips,
                        float * out_dev, void * stream);
@@ -153,7 +164,9 @@ typedef struct q2a_projector q2a_projector;
 q2a_projector * q2a_projector_open(const char * path, int device);
 void q2a_projector_close(q2a_projector * p);
 int q2a_projector_get_dims(const q2a_projector * p, int * d_in, int * d_out, int * wtype);
-/* y_dev [rows][d_out] f32 = x_dev [rows][d_in] f32 (device) projected; asynchronous on `stream` (NULL = own stream). */
+/* y_dev [rows][d_out] f32 = x_dev [rows][d_in] f32 (device) projected; asynchronous on `stream` (NULL = own stream).
+ * A projector handle owns ONE workspace (the quantized activation operand): calls on one handle must be ordered on one
+ * stream (or the caller synchronises between streams); use one handle per stream for concurrent projections. */
 int q2a_projector_apply(q2a_projector * p, const float * x_dev, int64_t rows, float * y_dev, void * stream);
 
 #ifdef __cplusplus

@@ -447,14 +447,14 @@ __global__ __launch_bounds__(256) void k_mm_f32(mm_args p) {
 // attention operands for the fused path: per-head fp16 hi/lo halves of Q (already scaled) and K, V^T
 template <bool WITH_V>
 __global__ void k_attn_prep(tview q, tview k, tview v, _Float16 * qh, _Float16 * ql, _Float16 * kh, _Float16 * kl,
-                            _Float16 * vt, int T, int H, int TP, int64_t n) {
+                            _Float16 * vt, _Float16 * vtl, int T, int H, int TP, int64_t n) {
     // element (d, t, h): q/k/v views have ne = [64, T, H]; q,k -> [t][h*64+d], v -> vt[h][d][t]
     const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int d = (int) (i & 63);
     const int r = (int) (i >> 6);
     const int t = r % T, h = r / T;
-    const float qv = *(const float *) (q.base + voff(q, d, t, h, 0));
+    const float qv = *(const float *) (q.base + voff(q, d, t, h, 0)) * Q2A_LOG2E;   // the attention's log2 units
     const float kv = *(const float *) (k.base + voff(k, d, t, h, 0));
     const int64_t o = (int64_t) t * H * 64 + h * 64 + d;
     const _Float16 a = (_Float16) qv, b = (_Float16) kv;
@@ -462,14 +462,17 @@ __global__ void k_attn_prep(tview q, tview k, tview v, _Float16 * qh, _Float16 *
     kh[o] = b; kl[o] = (_Float16) (kv - (float) b);
     if (WITH_V) {
         const float vv = *(const float *) (v.base + voff(v, t, d, h, 0));
-        vt[((int64_t) h * 64 + d) * TP + t] = (_Float16) vv;
+        const _Float16 vh = (_Float16) vv;
+        vt[((int64_t) h * 64 + d) * TP + t] = vh;
+        if (vtl) vtl[((int64_t) h * 64 + d) * TP + t] = (_Float16) (vv - (float) vh);
     }
 }
 
 // V^T operand of the fused attention, produced at the graph's CONT(permute(V)) node (qwen2-whisper.cpp:2081-2089)
 // from the CONT's source view (ne = [T, 64, H]; the CONT would copy it verbatim): vt[h][d][t] = fp16 V(t, d, h),
-// zero for T <= t < TP. One 64(t) x 64(d) tile per workgroup through LDS: reads run along d, writes along t.
-__global__ __launch_bounds__(256) void k_vt_tile(tview v, _Float16 * vt, int T, int TP) {
+// zero for T <= t < TP, and (vtl != NULL: the reference-contract attention's V hi/lo split) the lo image
+// fp16(v - fp16(v)). One 64(t) x 64(d) tile per workgroup through LDS: reads run along d, writes along t.
+__global__ __launch_bounds__(256) void k_vt_tile(tview v, _Float16 * vt, _Float16 * vtl, int T, int TP) {
     __shared__ float tile[64][65];
     const int t0 = (int) blockIdx.x * 64, h = (int) blockIdx.y;
     for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
@@ -479,7 +482,10 @@ __global__ __launch_bounds__(256) void k_vt_tile(tview v, _Float16 * vt, int T, 
     __syncthreads();
     for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
         const int dd = idx >> 6, tt = idx & 63;
-        vt[((int64_t) h * 64 + dd) * TP + t0 + tt] = (_Float16) tile[tt][dd];
+        const float x = tile[tt][dd];
+        const _Float16 xh = (_Float16) x;
+        vt[((int64_t) h * 64 + dd) * TP + t0 + tt] = xh;
+        if (vtl) vtl[((int64_t) h * 64 + dd) * TP + t0 + tt] = (_Float16) (x - (float) xh);
     }
 }
 
@@ -585,6 +591,7 @@ struct q2a_backend_ctx {
     std::vector<captured> graphs;
     uint64_t graph_clock = 0;
     int n_buffer_reallocs = 0;         // scratch / V^T / shadow reallocations (each drops the captured graphs)
+    bool capture_aborted = false;      // a reallocation ended an in-progress capture (graph_compute re-runs directly)
     int n_mul_mat_conv_total = 0;      // conv MUL_MATs run on the hi/lo path over the backend's lifetime
     int n_repack_lazy = 0;             // get_packed cache misses over the backend's lifetime
 };
@@ -652,6 +659,10 @@ void buf_memset_tensor(ggml_backend_buffer_t b, ggml_tensor * t, uint8_t v, size
 // instead of paying a device->host copy + host repack per weight. Anything else is packed lazily by get_packed.
 void prepack(int device, const ggml_tensor * t, const void * host, size_t off, size_t n) {
     if (off != 0 || n != ggml_nbytes(t) || t->view_src) return;
+    // gallocr COMPUTE buffers hold activations (an F16 input set every step would be host-packed on every write, and
+    // its cache entry would outlive a kernel's later overwrite of the same address): only weight-bearing buffers,
+    // which are still ANY while the loader uploads (qwen2-whisper.cpp:1845-1867)
+    if (t->buffer && ggml_backend_buffer_get_usage(t->buffer) == GGML_BACKEND_BUFFER_USAGE_COMPUTE) return;
     if (t->type != GGML_TYPE_F16 && t->type != GGML_TYPE_Q4_K && t->type != GGML_TYPE_Q8_0 && t->type != GGML_TYPE_Q4_0)
         return;
     if (t->ne[2] != 1 || t->ne[3] != 1 || !ggml_is_contiguous(t)) return;
@@ -752,6 +763,21 @@ dim3 grid1(int64_t n) { return dim3((unsigned) ((n + 255) / 256)); }
 // Captured HIP graphs bake in the addresses of the scratch, V^T and fp16-shadow buffers: whenever one of them is
 // reallocated, every captured exec is destroyed (its cgraph is re-captured on its next sightings against the new
 // buffers), so no replay can touch freed memory.
+// A buffer must grow while graph_compute is capturing (the second sighting of a cgraph whose node sequence needs more
+// than its first run did): a capturing stream cannot be synchronised and the capture would bake in the buffer about
+// to be freed. End the capture and discard it (nothing captured has run); run_nodes stops at the next node and
+// graph_compute runs the cgraph again directly, against the new buffers.
+void abort_capture(q2a_backend_ctx * b) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(b->stream, &st) == hipSuccess && st == hipStreamCaptureStatusActive) {
+        hipGraph_t gr = nullptr;
+        (void) hipStreamEndCapture(b->stream, &gr);
+        if (gr) (void) hipGraphDestroy(gr);
+        (void) hipGetLastError();
+        b->capture_aborted = true;
+    }
+}
+
 void drop_graphs(q2a_backend_ctx * b) {
     for (auto & e : b->graphs) {
         if (e.exec) (void) hipGraphExecDestroy(e.exec);
@@ -764,6 +790,7 @@ void drop_graphs(q2a_backend_ctx * b) {
 void * scratch(q2a_backend_ctx * b, size_t bytes) {
     if (bytes > b->scratch_bytes) {
         b->quant_src = nullptr;
+        abort_capture(b);
         Q2A_HIP(hipStreamSynchronize(b->stream));
         if (b->scratch) Q2A_HIP(hipFree(b->scratch));
         b->scratch = nullptr;
@@ -1066,6 +1093,7 @@ ggml_tensor * match_attention(ggml_cgraph * g, int i) {
 
 _Float16 * vt_buffer(q2a_backend_ctx * b, size_t bytes) {
     if (bytes > b->vt_bytes) {
+        abort_capture(b);
         Q2A_HIP(hipStreamSynchronize(b->stream));
         if (b->vt_buf) Q2A_HIP(hipFree(b->vt_buf));
         b->vt_buf = nullptr;
@@ -1081,6 +1109,7 @@ _Float16 * claim_a16(q2a_backend_ctx * b, const ggml_tensor * t) {
     const int k = 1 - b->a16_last;
     const size_t bytes = (size_t) ggml_nelements(t) * 2;
     if (bytes > b->a16_bytes[k]) {
+        abort_capture(b);
         Q2A_HIP(hipStreamSynchronize(b->stream));
         if (b->a16[k]) Q2A_HIP(hipFree(b->a16[k]));
         b->a16[k] = nullptr;
@@ -1106,22 +1135,26 @@ int run_fused_attention(q2a_backend_ctx * b, ggml_cgraph * g, int i, bool vt_rea
     const int TP = (int) ((T + 63) / 64 * 64);
     const int64_t D = H * 64, n = T * D;
     const size_t hb = ((size_t) n * 2 + 255) & ~size_t(255);
-    const size_t vb = ((size_t) H * 64 * TP * 2 + 255) & ~size_t(255);
+    const bool vlo = q2a_attention_wants_vlo();
+    const size_t vb1 = ((size_t) H * 64 * TP * 2 + 255) & ~size_t(255);
+    const size_t vb = vlo ? 2 * vb1 : vb1;   // V^T [| V^T lo]
     char * s = (char *) scratch(b, 4 * hb + vb + (size_t) n * 4);
     b->quant_src = nullptr;   // the attention operands overwrite the scratch
     _Float16 *qh = (_Float16 *) s, *ql = (_Float16 *) (s + hb), *kh = (_Float16 *) (s + 2 * hb), *kl = (_Float16 *) (s + 3 * hb);
     _Float16 * vt = vt_ready ? b->vt_buf : (_Float16 *) (s + 4 * hb);
+    _Float16 * vtl = vlo ? (_Float16 *) ((char *) vt + vb1) : nullptr;
     float * o = merged ? (float *) merged->data : (float *) (s + 4 * hb + vb);
     if (vt_ready) {
         hipLaunchKernelGGL(k_attn_prep<false>, grid1(n), dim3(256), 0, b->stream, tv(Q), tv(K), tv(V), qh, ql, kh, kl, vt,
-                           (int) T, (int) H, TP, n);
+                           vtl, (int) T, (int) H, TP, n);
     } else {
         Q2A_HIP(hipMemsetAsync(vt, 0, vb, b->stream));   // V^T tail columns past T are read as zero weights
         hipLaunchKernelGGL(k_attn_prep<true>, grid1(n), dim3(256), 0, b->stream, tv(Q), tv(K), tv(V), qh, ql, kh, kl, vt,
-                           (int) T, (int) H, TP, n);
+                           vtl, (int) T, (int) H, TP, n);
     }
     q2a_attn_args at{(const q2a_half *) qh, (const q2a_half *) ql, (const q2a_half *) kh, (const q2a_half *) kl,
                      (const q2a_half *) vt, 1, (int) T, (int) D, (int) H, TP, nullptr, o};
+    at.vtl = vtl;
     Q2A_HIP(q2a_launch_attention(at, b->stream));
     if (!merged)
         hipLaunchKernelGGL(k_attn_out, grid1(n), dim3(256), 0, b->stream, (const float *) o, tv(kqv), (int) T, (int) H, n);
@@ -1259,6 +1292,7 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
     // f32 activations some F16-weight MUL_MAT converts to fp16: their producer also writes the fp16 copy
     std::unordered_map<const ggml_tensor *, int> want16;
     b->a16_src[0] = b->a16_src[1] = nullptr;
+    b->a16_last = 1;   // slot assignment deterministic per cgraph: a replayed capture sees the same slots as its run
     b->quant_src = nullptr;
     if (!no_fuse) {
         for (int j = 0; j < nn; ++j) {
@@ -1300,6 +1334,7 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
         return c;
     };
     for (int i = 0; i < nn; ++i) {
+        if (b->capture_aborted) return GGML_STATUS_SUCCESS;   // graph_compute re-runs the whole cgraph directly
         ggml_tensor * op = ggml_graph_node(g, i);
         if (ggml_is_empty(op) || op->op == GGML_OP_NONE || op->op == GGML_OP_RESHAPE || op->op == GGML_OP_VIEW ||
             op->op == GGML_OP_PERMUTE || op->op == GGML_OP_TRANSPOSE)
@@ -1432,8 +1467,11 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                 if (vprep.count(op) && !vt_ready_for) {   // V of a fused attention: its V^T operand instead of the f32 copy
                     // (one pending at a time: a second V before the first attention is copied normally)
                     const int T = (int) op->ne[0], H = (int) op->ne[2], TP = (T + 63) / 64 * 64;
-                    _Float16 * vt = vt_buffer(b, (size_t) H * 64 * TP * 2);
-                    hipLaunchKernelGGL(k_vt_tile, dim3((unsigned) (TP / 64), (unsigned) H), dim3(256), 0, st, tv(op->src[0]), vt, T, TP);
+                    const size_t vb1 = ((size_t) H * 64 * TP * 2 + 255) & ~size_t(255);
+                    const bool vlo = q2a_attention_wants_vlo();   // (run_fused_attention finds the lo image at +vb1)
+                    _Float16 * vt = vt_buffer(b, vlo ? 2 * vb1 : vb1);
+                    hipLaunchKernelGGL(k_vt_tile, dim3((unsigned) (TP / 64), (unsigned) H), dim3(256), 0, st, tv(op->src[0]), vt,
+                                       vlo ? (_Float16 *) ((char *) vt + vb1) : nullptr, T, TP);
                     vt_ready_for = op;
                     b->stats.n_other++;
                     break;
@@ -1528,8 +1566,14 @@ ggml_status graph_compute(ggml_backend_t backend, ggml_cgraph * g) {
     }
     if (++c->seen == 2) {   // second sighting (weights packed, scratch sized): capture once, then launch
         hipGraph_t graph = nullptr;
+        b->capture_aborted = false;
         if (hipStreamBeginCapture(b->stream, hipStreamCaptureModeThreadLocal) == hipSuccess) {
             const ggml_status st = run_nodes(b, g);
+            if (b->capture_aborted) {   // a buffer grew mid-capture: the capture is gone, nothing of it ran
+                b->capture_aborted = false;
+                c->seen = 1;            // captured again on its next sighting, against the grown buffers
+                return run_nodes(b, g);
+            }
             const hipError_t ec = hipStreamEndCapture(b->stream, &graph);
             hipGraphExec_t exec = nullptr;
             if (st == GGML_STATUS_SUCCESS && ec == hipSuccess && graph &&

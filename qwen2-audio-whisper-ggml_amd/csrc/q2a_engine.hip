@@ -46,7 +46,8 @@ void set_err(const char * fmt, ...) {
 // packed device blob: 16 KiB self-describing header + 256-B aligned sections
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t BLOB_MAGIC = 0x42413251u;   // "Q2AB"
-constexpr uint32_t BLOB_VERSION = 2;
+// version 3: the Q4_K gamma array holds -(dmin/dx) (stored negated); a version-2 blob (positive gamma) is refused
+constexpr uint32_t BLOB_VERSION = 3;
 constexpr int MAX_LAYERS = 64;
 constexpr size_t HEADER_BYTES = 32768;
 
@@ -443,23 +444,27 @@ int q2a_pack_linear(const uint8_t * raw, int wtype, int N, int K, std::vector<ui
 
 namespace {
 
-__global__ void k_split_hilo(const float * x, q2a_half * hi, q2a_half * lo, int64_t n) {
+__global__ void k_split_hilo(const float * x, q2a_half * hi, q2a_half * lo, int64_t n, float scale) {
     const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float v = x[i];
+    const float v = x[i] * scale;
     const _Float16 h = (_Float16) v;
     hi[i] = h;
     lo[i] = (_Float16) (v - (float) h);
 }
 
-__global__ void k_to_vt(const float * v, q2a_half * vt, int clips, int T, int H, int TP) {
+// V [clips*T][D] f32 -> V^T [clip][head][d][TP] fp16, and its lo image fp16(v - fp16(v)) when vtl is set
+__global__ void k_to_vt(const float * v, q2a_half * vt, q2a_half * vtl, int clips, int T, int H, int TP) {
     const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     const int64_t D = (int64_t) H * 64;
     if (i >= (int64_t) clips * T * D) return;
     const int64_t m = i / D;
     const int c = (int) (i % D);
     const int clip = (int) (m / T), t = (int) (m % T);
-    vt[(((int64_t) clip * H + c / 64) * 64 + (c % 64)) * TP + t] = (_Float16) v[i];
+    const int64_t o = (((int64_t) clip * H + c / 64) * 64 + (c % 64)) * TP + t;
+    const _Float16 h = (_Float16) v[i];
+    vt[o] = h;
+    if (vtl) vtl[o] = (_Float16) (v[i] - (float) h);
 }
 
 __global__ void k_to_half(const float * x, q2a_half * y, int64_t n) {
@@ -515,7 +520,15 @@ struct q2a_engine {
     int64_t cap_samples = 0;
     void * ws = nullptr;
     size_t ws_bytes = 0;
-    float * pcm_stage = nullptr;     // host-API staging [cap][cap_samples]
+    // host API (q2a_encode_host*): a copy stream and two sets of pinned + device staging buffers, so the PCIe copies
+    // of one chunk of clips run beside the encode of the neighbouring chunk (host_pipe)
+    struct host_buf {
+        float * pin_in = nullptr; float * pin_out = nullptr; float * d_in = nullptr; float * d_out = nullptr;
+        size_t in_cap = 0, out_cap = 0;   // floats
+        hipEvent_t h2d = nullptr, comp = nullptr, d2h = nullptr;
+    };
+    hipStream_t copy_stream = nullptr;
+    host_buf hb[2];
     float * out_stage = nullptr;     // unused (outputs are written straight to the user buffer)
     int32_t * meta = nullptr;        // device: nsamp | seek | clip_ok | clip_max
     int32_t * meta_host = nullptr;   // pinned
@@ -531,6 +544,7 @@ struct q2a_engine {
     q2a_half * aextD = nullptr;
     q2a_half * aextF = nullptr;
     q2a_half *qh = nullptr, *ql = nullptr, *kh = nullptr, *kl = nullptr, *vt = nullptr;
+    q2a_half * vtl = nullptr;        // V^T lo image, when the attention build reads one (q2a_attention_wants_vlo)
     float * attF = nullptr;
     float * hF = nullptr;
     float * part = nullptr;          // split-K partials of the small-tile residual GEMMs (NULL: big batches)
@@ -538,11 +552,11 @@ struct q2a_engine {
     int TP = 0;
     int dy_ld = 0;
     bool force_encode = false;   // encode windows with under 1 s of audio too (whisper_full with duration_ms set)
-    // fc1 epilogue quantization (Q2A_FUSE_Q8K=1): correct, but at present no faster than the fp16 GELU output
-    // plus the bandwidth-bound quantizer, so off by default
-    int fuse_q8k = [] { const char * v = getenv("Q2A_FUSE_Q8K"); return v ? atoi(v) : -1; }();
-    // Q4_K fc1: GELU in the GEMM epilogue (1) or deferred to the Q8_K quantizer (0, default; A/B: Q2A_GELU_IN_EPI=1)
-    int gelu_in_epi = [] { const char * v = getenv("Q2A_GELU_IN_EPI"); return v ? atoi(v) : 0; }();
+    // Q4_K fc1 -> fc2 operand path (q2a_test_fc1_path; the three produce identical Q8_K codes):
+    //   0 (default) fc1 writes its fp16 pre-activation, the Q8_K quantizer applies the GELU table on the way
+    //   1 GELU in the fc1 epilogue, then the fp16-input quantizer
+    //   2 GELU + Q8_K quantization fused into the fc1 epilogue (8-phase tiles only; no faster at present)
+    int fc1_path = 0;
     // q2a_test_block_taps: device buffers receiving the GEMM A operands of one block (LN1 -> QKV, attention -> O,
     // LN2 -> fc1, GELU -> fc2) as they were fed to the MFMA, for the per-layer divergence trace (NULL: off)
     void * taps[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -590,9 +604,56 @@ int engine_adopt_header(q2a_engine * e) {
 void free_ws(q2a_engine * e) {
     if (e->ws) (void) hipFree(e->ws);
     if (e->meta_host) (void) hipHostFree(e->meta_host);
-    if (e->pcm_stage) (void) hipFree(e->pcm_stage);
-    e->ws = nullptr; e->meta_host = nullptr; e->pcm_stage = nullptr;
+    e->ws = nullptr; e->meta_host = nullptr;
     e->cap_clips = 0; e->ws_bytes = 0;
+}
+
+void free_host_bufs(q2a_engine * e) {
+    if (e->copy_stream) (void) hipStreamSynchronize(e->copy_stream);
+    for (auto & b : e->hb) {
+        if (b.pin_in) (void) hipHostFree(b.pin_in);
+        if (b.pin_out) (void) hipHostFree(b.pin_out);
+        if (b.d_in) (void) hipFree(b.d_in);
+        if (b.d_out) (void) hipFree(b.d_out);
+        for (hipEvent_t ev : {b.h2d, b.comp, b.d2h}) if (ev) (void) hipEventDestroy(ev);
+        b = q2a_engine::host_buf{};
+    }
+    if (e->copy_stream) (void) hipStreamDestroy(e->copy_stream);
+    e->copy_stream = nullptr;
+}
+
+// staging for host-API chunks of up to `clips` clips of `maxn` samples (grows; never shrinks)
+int ensure_host_bufs(q2a_engine * e, int clips, int64_t maxn) {
+    if (!e->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking));
+    const size_t in = (size_t) clips * maxn, out = (size_t) clips * e->d.TO * e->d.D;
+    for (auto & b : e->hb) {
+        if (!b.h2d) {
+            HIP_TRY(hipEventCreateWithFlags(&b.h2d, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&b.comp, hipEventDisableTiming));
+            HIP_TRY(hipEventCreateWithFlags(&b.d2h, hipEventDisableTiming));
+        }
+        if (in > b.in_cap || out > b.out_cap) {
+            HIP_TRY(hipStreamSynchronize(e->copy_stream));
+            HIP_TRY(hipStreamSynchronize(e->stream));
+        }
+        if (in > b.in_cap) {
+            if (b.pin_in) (void) hipHostFree(b.pin_in);
+            if (b.d_in) (void) hipFree(b.d_in);
+            b.pin_in = nullptr; b.d_in = nullptr; b.in_cap = 0;
+            HIP_TRY(hipHostMalloc((void **) &b.pin_in, in * 4, hipHostMallocDefault));
+            HIP_TRY(hipMalloc((void **) &b.d_in, in * 4));
+            b.in_cap = in;
+        }
+        if (out > b.out_cap) {
+            if (b.pin_out) (void) hipHostFree(b.pin_out);
+            if (b.d_out) (void) hipFree(b.d_out);
+            b.pin_out = nullptr; b.d_out = nullptr; b.out_cap = 0;
+            HIP_TRY(hipHostMalloc((void **) &b.pin_out, out * 4, hipHostMallocDefault));
+            HIP_TRY(hipMalloc((void **) &b.d_out, out * 4));
+            b.out_cap = out;
+        }
+    }
+    return Q2A_OK;
 }
 
 int reserve(q2a_engine * e, int B) {
@@ -618,6 +679,8 @@ int reserve(q2a_engine * e, int B) {
     const size_t o_kh = take((size_t) BT * d.D * 2);
     const size_t o_kl = take((size_t) BT * d.D * 2);
     const size_t o_vt = take((size_t) B * d.H * 64 * e->TP * 2);
+    const bool vlo = !e->bf16 && q2a_attention_wants_vlo();
+    const size_t o_vtl = vlo ? take((size_t) B * d.H * 64 * e->TP * 2) : 0;
     size_t o_dyD = 0, o_dyF = 0, o_aD = 0, o_aF = 0, o_att = 0, o_hF = 0, o_part = 0;
     // split-K partials of the small-tile residual GEMMs (O-proj, fc2): up to 4 x [rows][D] f32. Sized for every
     // row count that takes the small-tile path (M <= 26 112 at D = 1280), whatever the capacity, so whether a
@@ -657,6 +720,7 @@ int reserve(q2a_engine * e, int B) {
     e->qh = (q2a_half *) (b + o_qh); e->ql = (q2a_half *) (b + o_ql);
     e->kh = (q2a_half *) (b + o_kh); e->kl = (q2a_half *) (b + o_kl);
     e->vt = (q2a_half *) (b + o_vt);
+    e->vtl = vlo ? (q2a_half *) (b + o_vtl) : nullptr;
     e->part = split ? (float *) (b + o_part) : nullptr;
     if (quant) {
         e->dyD = (float *) (b + o_dyD); e->dyF = (float *) (b + o_dyF);
@@ -744,12 +808,15 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
     {
         q2a_gemm_args a = gemm_base(e, l, 0, e->actD, M);
         a.bias = e->lv<const float *>(l, L_BQKV);
-        a.qh = e->qh; a.ql = e->ql; a.kh = e->kh; a.kl = e->kl; a.vt = e->vt;
-        a.qscale = 1.0f / sqrtf((float) (d.D / d.H));
+        a.qh = e->qh; a.ql = e->ql; a.kh = e->kh; a.kl = e->kl; a.vt = e->vt; a.vtl = e->vtl;
+        // ggml_scale(Q, 1/sqrt(dh)) (:2054); the reference-contract attention also wants log2(e) folded in (its
+        // softmax runs in log2 units): one f32 multiply by fl(log2 e)/8, 2^-3 being exact
+        a.qscale = (1.0f / sqrtf((float) (d.D / d.H))) * (e->bf16 ? 1.0f : Q2A_LOG2E);
         PLAUNCH(e, s, Q2A_PROF_GEMM_QKV, q2a_launch_gemm(a, Q2A_EPI_QKV, e->gblk, s));
     }
     {
         q2a_attn_args at{e->qh, e->ql, e->kh, e->kl, e->vt, B, d.T, d.D, d.H, e->TP, nullptr, nullptr, e->bf16 ? 1 : 0};
+        at.vtl = e->vtl;
         if (mode == 0 || mode == 4) at.outH = e->actD; else at.outF = e->attF;
         PLAUNCH(e, s, Q2A_PROF_ATTN, q2a_launch_attention(at, s));
         if (mode == 3) {
@@ -781,11 +848,11 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
             a.o_dup = mode == 3 ? 2 * d.F : 0;
             PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_H, e->gblk, s));
         } else if (mode == 1 && q2a_gemm_wide_tiles(M, d.F, e->blk) &&
-                   e->fuse_q8k == 1 && q2a_gemm_pipe8(a, e->blk)) {
+                   e->fc1_path == 2 && q2a_gemm_pipe8(a, e->blk)) {
             // fused fc1 + GELU + Q8_K quantization of the fc2 input (one Q8_K block per 256-column tile)
             a.outH = e->actF; a.ldo = d.F; a.qdy = e->dyF; a.qaext = e->aextF;
             PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_GELU_Q8K, e->blk, s));
-        } else if (mode == 1 && !e->gelu_in_epi) {
+        } else if (mode == 1 && e->fc1_path != 1) {
             // fc1 writes its fp16 pre-activation (plain stores); the Q8_K quantizer of the fc2 input applies the
             // GELU table from LDS on the way (same codes as the GELU epilogue + quantizer below)
             q2a_half * hH = (q2a_half *) e->hF;
@@ -999,6 +1066,7 @@ void q2a_close(q2a_engine * e) {
     if (!e) return;
     (void) hipSetDevice(e->device);
     if (e->stream) (void) hipStreamSynchronize(e->stream);
+    free_host_bufs(e);
     free_ws(e);
     for (auto & r : e->pending) { (void) hipEventDestroy(r.a); (void) hipEventDestroy(r.b); }
     for (auto ev : e->pool) (void) hipEventDestroy(ev);
@@ -1048,25 +1116,63 @@ int q2a_encode_host_ex(q2a_engine * e, const float * const * pcm, const int32_t 
                        int n_clips, int offset_ms, float * out_host, int32_t * status) {
     if (!e || !pcm || !n_samples || !out_host || n_clips <= 0) { set_err("invalid arguments"); return Q2A_ERR_ARG; }
     HIP_TRY(hipSetDevice(e->device));
+    // Chunks of clips through two staging sets: chunk k's host->pinned copy and H2D (copy stream) run while chunk k-1
+    // encodes (compute stream), and chunk k-1's D2H + pinned->host copy while chunk k encodes. One chunk below 32
+    // clips (nothing to overlap with); else at least two, at most 64 clips each. Clips are independent and every
+    // tile regime sums in one K order, so the chunking changes no output bit (batch invariance).
+    // Outputs of skipped clips (< 1 s after the offset) are never copied back: the caller's contents stay untouched.
+    const int nchunk = n_clips < 32 ? 1 : std::max(2, (n_clips + 63) / 64);
+    const int C = (n_clips + nchunk - 1) / nchunk;
     int64_t maxn = 1;
     for (int c = 0; c < n_clips; ++c) maxn = std::max<int64_t>(maxn, n_samples[c]);
     maxn = (maxn + 63) & ~int64_t(63);
-    float * dpcm = nullptr;
-    float * dout = nullptr;
-    const size_t out_bytes = (size_t) n_clips * e->d.TO * e->d.D * 4;
-    HIP_TRY(hipMalloc((void **) &dpcm, (size_t) n_clips * maxn * 4));
-    if (hipMalloc((void **) &dout, out_bytes) != hipSuccess) { (void) hipFree(dpcm); set_err("alloc failed"); return Q2A_ERR_OOM; }
+    if (int rc = ensure_host_bufs(e, C, maxn)) return rc;
+    const size_t per_out = (size_t) e->d.TO * e->d.D;
+    std::vector<int32_t> st(n_clips);
+    hipStream_t cs = e->copy_stream, s = e->stream;
     int rc = Q2A_OK;
-    for (int c = 0; c < n_clips && rc == Q2A_OK; ++c)
-        if (hipMemcpyAsync(dpcm + c * maxn, pcm[c], (size_t) n_samples[c] * 4, hipMemcpyHostToDevice, e->stream) != hipSuccess)
+    auto copy_out = [&](int k) {   // chunk k's encoded outputs: pinned -> caller (after its D2H)
+        const int c0 = k * C, n = std::min(C, n_clips - c0);
+        q2a_engine::host_buf & b = e->hb[k & 1];
+        if (hipEventSynchronize(b.d2h) != hipSuccess) return Q2A_ERR_HIP;
+        for (int c = 0; c < n; ++c)
+            if (st[c0 + c] == Q2A_CLIP_ENCODED)
+                memcpy(out_host + (c0 + c) * per_out, b.pin_out + c * per_out, per_out * 4);
+        return Q2A_OK;
+    };
+    for (int k = 0; k < nchunk && rc == Q2A_OK; ++k) {
+        const int c0 = k * C, n = std::min(C, n_clips - c0);
+        q2a_engine::host_buf & b = e->hb[k & 1];
+        // staging set k&1 was last used by chunk k-2: its H2D must have left pin_in, its D2H must have left d_out
+        if (hipEventSynchronize(b.h2d) != hipSuccess) { rc = Q2A_ERR_HIP; break; }
+        for (int c = 0; c < n; ++c) {
+            memcpy(b.pin_in + c * maxn, pcm[c0 + c], (size_t) n_samples[c0 + c] * 4);
+        }
+        if (hipStreamWaitEvent(cs, b.comp, 0) != hipSuccess ||   // chunk k-2's encode no longer reads d_in
+            hipMemcpyAsync(b.d_in, b.pin_in, (size_t) n * maxn * 4, hipMemcpyHostToDevice, cs) != hipSuccess ||
+            hipEventRecord(b.h2d, cs) != hipSuccess ||
+            hipStreamWaitEvent(s, b.h2d, 0) != hipSuccess ||     // PCM landed
+            hipStreamWaitEvent(s, b.d2h, 0) != hipSuccess) {     // chunk k-2's outputs left d_out
             rc = Q2A_ERR_HIP;
-    // outputs of skipped clips are left untouched: seed the device buffer with the caller's current contents
-    if (rc == Q2A_OK && hipMemcpyAsync(dout, out_host, out_bytes, hipMemcpyHostToDevice, e->stream) != hipSuccess) rc = Q2A_ERR_HIP;
-    if (rc == Q2A_OK) rc = encode_impl(e, dpcm, maxn, n_samples, n_clips, offset_ms, offsets_ms, dout, status, e->stream);
-    if (rc == Q2A_OK && hipMemcpyAsync(out_host, dout, out_bytes, hipMemcpyDeviceToHost, e->stream) != hipSuccess) rc = Q2A_ERR_HIP;
-    if (hipStreamSynchronize(e->stream) != hipSuccess && rc == Q2A_OK) { set_err("stream error"); rc = Q2A_ERR_HIP; }
-    (void) hipFree(dpcm);
-    (void) hipFree(dout);
+            break;
+        }
+        rc = encode_impl(e, b.d_in, maxn, n_samples + c0, n, offset_ms, offsets_ms ? offsets_ms + c0 : nullptr, b.d_out,
+                         st.data() + c0, s);
+        if (rc) break;
+        if (hipEventRecord(b.comp, s) != hipSuccess || hipStreamWaitEvent(cs, b.comp, 0) != hipSuccess ||
+            hipMemcpyAsync(b.pin_out, b.d_out, (size_t) n * per_out * 4, hipMemcpyDeviceToHost, cs) != hipSuccess ||
+            hipEventRecord(b.d2h, cs) != hipSuccess) {
+            rc = Q2A_ERR_HIP;
+            break;
+        }
+        if (k >= 1) rc = copy_out(k - 1);   // runs while chunk k encodes
+    }
+    if (rc == Q2A_OK) rc = copy_out(nchunk - 1);
+    if (hipStreamSynchronize(cs) != hipSuccess || hipStreamSynchronize(s) != hipSuccess) {
+        if (rc == Q2A_OK) { set_err("stream error"); rc = Q2A_ERR_HIP; }
+    }
+    if (rc == Q2A_ERR_HIP && g_err.empty()) set_err("host-path copy failed");
+    if (status) for (int c = 0; c < n_clips; ++c) status[c] = st[c];
     return rc;
 }
 
@@ -1209,6 +1315,45 @@ int q2a_test_block_taps(q2a_engine * e, int layer, float * x, int n_clips, void 
     return rc;
 }
 
+int q2a_test_frontend(q2a_engine * e, const float * pcm_dev, int64_t pcm_stride, const int32_t * n_samples, int n_clips,
+                      float * x_dev, void * stream) {
+    if (!e || !pcm_dev || !n_samples || !x_dev || n_clips <= 0) return Q2A_ERR_ARG;
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = stream ? (hipStream_t) stream : e->stream;
+    int rc = reserve(e, n_clips);
+    if (rc) return rc;
+    int max_frames = 0;
+    rc = prepare_meta(e, n_samples, n_clips, 0, nullptr, nullptr, max_frames, pcm_stride > 0 ? pcm_stride : -1, s);
+    if (rc) return rc;
+    rc = run_frontend(e, pcm_dev, pcm_stride, n_clips, max_frames, s);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(x_dev, e->X, (size_t) n_clips * e->d.T * e->d.D * 4, hipMemcpyDeviceToDevice, s));
+    return Q2A_OK;
+}
+
+int q2a_test_pool_ln(q2a_engine * e, const float * x_dev, int n_clips, float * out_dev, void * stream) {
+    if (!e || !x_dev || !out_dev || n_clips <= 0) return Q2A_ERR_ARG;
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t s = stream ? (hipStream_t) stream : e->stream;
+    int rc = reserve(e, n_clips);
+    if (rc) return rc;
+    HIP_TRY(hipEventSynchronize(e->meta_evt));
+    for (int c = 0; c < n_clips; ++c) e->meta_host[2 * n_clips + c] = 1;   // every clip "encoded"
+    HIP_TRY(hipMemcpyAsync(e->meta + 2 * n_clips, e->meta_host + 2 * n_clips, (size_t) n_clips * 4, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipEventRecord(e->meta_evt, s));
+    HIP_TRY(hipMemcpyAsync(e->X, x_dev, (size_t) n_clips * e->d.T * e->d.D * 4, hipMemcpyDeviceToDevice, s));
+    q2a_pool_args pa{e->X, n_clips, e->d.T, e->d.D, e->g<const float *>(G_LNP_W), e->g<const float *>(G_LNP_B), out_dev,
+                     e->meta + 2 * n_clips};
+    LAUNCH(q2a_launch_pool_ln(pa, s));
+    return Q2A_OK;
+}
+
+int q2a_test_fc1_path(q2a_engine * e, int path) {
+    if (!e || path < 0 || path > 2) return Q2A_ERR_ARG;
+    e->fc1_path = path;
+    return Q2A_OK;
+}
+
 int q2a_test_attention(q2a_engine * e, const float * q, const float * k, const float * v, int n_clips, float * out,
                        void * stream) {
     if (!e || n_clips <= 0) return Q2A_ERR_ARG;
@@ -1219,11 +1364,12 @@ int q2a_test_attention(q2a_engine * e, const float * q, const float * k, const f
     const dims & d = e->d;
     const int64_t n = (int64_t) n_clips * d.T * d.D;
     const dim3 g((unsigned) ((n + 255) / 256)), b(256);
-    hipLaunchKernelGGL(k_split_hilo, g, b, 0, s, q, e->qh, e->ql, n);
-    hipLaunchKernelGGL(k_split_hilo, g, b, 0, s, k, e->kh, e->kl, n);
-    hipLaunchKernelGGL(k_to_vt, g, b, 0, s, v, e->vt, n_clips, d.T, d.H, e->TP);
+    hipLaunchKernelGGL(k_split_hilo, g, b, 0, s, q, e->qh, e->ql, n, Q2A_LOG2E);   // the kernel's log2 units
+    hipLaunchKernelGGL(k_split_hilo, g, b, 0, s, k, e->kh, e->kl, n, 1.0f);
+    hipLaunchKernelGGL(k_to_vt, g, b, 0, s, v, e->vt, e->vtl, n_clips, d.T, d.H, e->TP);
     LAUNCH(hipGetLastError());
     q2a_attn_args at{e->qh, e->ql, e->kh, e->kl, e->vt, n_clips, d.T, d.D, d.H, e->TP, nullptr, out};
+    at.vtl = e->vtl;
     LAUNCH(q2a_launch_attention(at, s));
     return Q2A_OK;
 }

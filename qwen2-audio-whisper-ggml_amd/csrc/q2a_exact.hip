@@ -403,6 +403,10 @@ __global__ __launch_bounds__(GQ_THREADS) void k_gelu_quant_q8k_h16(const q2a_hal
         asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(h1) : "v"(a));
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(h0), "+v"(h1) :: "memory");
         dma(t + 1);                                          // the buffer's next fill (its data is in registers)
+        // the vmcnt(3) at the top of the next iteration counts on this DMA being issued BEFORE this iteration's 3
+        // stores: pin the order (no IR motion of memory ops across the fence, no machine scheduling across the barrier)
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
         int r0, bf;
         place(t, r0, bf);
         wait_all = r0 + 4 > M;
@@ -527,6 +531,11 @@ hipError_t q2a_launch_mel(const q2a_mel_args & a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Q2A_QUANT_V1 (diagnostic builds only): the round-1 one-row-per-wave LN+Q8_K and fp16-input Q8_K kernels instead of
+// the 8-rows-per-workgroup / 16-block forms (identical codes)
+#ifndef Q2A_QUANT_V1
+#define Q2A_QUANT_V1 0
+#endif
 hipError_t q2a_launch_layernorm(const q2a_ln_args & a, hipStream_t s) {
     if (a.D % 4 != 0 || a.D > 2048) return hipErrorInvalidValue;
     if (a.mode == 1 && a.D % 256) return hipErrorInvalidValue;
@@ -535,7 +544,7 @@ hipError_t q2a_launch_layernorm(const q2a_ln_args & a, hipStream_t s) {
     if (a.mode == 0) hipLaunchKernelGGL((k_rownorm<0, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else if (a.mode == 3) hipLaunchKernelGGL((k_rownorm<3, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else if (a.mode == 4) hipLaunchKernelGGL((k_rownorm<4, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
-    else if (a.mode == 1 && a.D == 1280 && !getenv("Q2A_QUANT_V1"))
+    else if (a.mode == 1 && a.D == 1280 && !Q2A_QUANT_V1)
         hipLaunchKernelGGL((k_rownorm<1, true, false, 5>), dim3((a.M + 7) / 8), dim3(512), 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy,
                            a.aext, 1, a.dy_ld);
     else if (a.mode == 1) hipLaunchKernelGGL((k_rownorm<1, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
@@ -563,7 +572,7 @@ hipError_t q2a_launch_quant_act(const q2a_quant_args & a, hipStream_t s) {
     const dim3 grid((a.M * nseg + 3) / 4), blk(256);
     // view X as [M*nseg][seg]: contiguous, and the block structure (256 / 32) never straddles a segment
     const float * X = a.XH ? (const float *) a.XH : a.X;
-    if (a.mode == 1 && a.XH && !getenv("Q2A_QUANT_V1")) {
+    if (a.mode == 1 && a.XH && !Q2A_QUANT_V1) {
         const int64_t nb = (int64_t) a.M * (a.K / 256);
         hipLaunchKernelGGL(k_quant_q8k_h16, dim3((unsigned) ((nb + 15) / 16)), dim3(256), 0, s, a.XH, nb, a.K / 256, a.outH,
                            a.dy, a.aext, a.dy_ld);

@@ -969,38 +969,121 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
         return odd ? make_uint4(recv.x, recv.y, ub.x, ub.y) : make_uint4(ua.x, ua.y, recv.x, recv.y);
     };
     const int pcol = 16 * (q & 1) + 8 * (q >> 1);    // column of this lane's 16-B piece within a 32-column pair
-    if (EPI == Q2A_EPI_QKV && part == 2) {
+    if (PIPE == 1 && (EPI == Q2A_EPI_PRE_H || (EPI == Q2A_EPI_QKV && part < 2))) {
+      if constexpr (PIPE == 1 && (EPI == Q2A_EPI_PRE_H || EPI == Q2A_EPI_QKV)) {
+        // fp16 outputs of the 8-phase tile (fc1's pre-activation; Q / K hi and lo), staged through LDS so every store
+        // instruction writes two WHOLE 512-B output rows: all 8 waves write the tile [256 rows][256 cols] into the idle
+        // operand images (16-B granules XOR-swizzled by row: conflict-free 8-B writes of 16 rows and 16-B reads of
+        // one row), then each wave stores 32 rows. The register layout's natural store was 16 rows x 64 B per
+        // instruction (and a lane exchange per pair of column tiles): the fc1 epilogue cost ~0.3 ms per launch.
+        static_assert(BM == 256 && BN == 256 && NW == 8, "staged fp16 epilogue layout");
+        constexpr int NPASS = (EPI == Q2A_EPI_QKV && !BF) ? 2 : 1;   // Q / K: the hi image, then the lo image
+        constexpr int RB = 256 * 2;                                 // staged row bytes
+        char * stg = lds_raw;                                       // 256 x 512 B = 128 KiB (operand images)
+        const int orq = EPI == Q2A_EPI_PRE_H && p.o_rpg < p.M;      // a real output-row remap (conv paths only)
+        h4v lo[NPASS == 2 ? MI : 1][NPASS == 2 ? NJ : 1];          // the lo image, packed (the accumulators die)
+#pragma unroll
+        for (int pass = 0; pass < NPASS; ++pass) {
+            __syncthreads();   // every wave done with the operand images / the previous pass's staged rows
+#pragma unroll
+            for (int i = 0; i < MI; ++i) {
+                const int row = wm * WR + i * 16 + l16;
+#pragma unroll
+                for (int j = 0; j < NJ; ++j) {
+                    const int col = wn * WC + j * 16 + 4 * q;       // 4 consecutive fp16 columns
+                    h4v hv;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        if constexpr (EPI == Q2A_EPI_PRE_H) {       // pre-activation; x <= -10 marked -inf (GELU = 0)
+                            const float v = val(i, j, r);
+                            hv[r] = v <= -10.0f ? (_Float16) -INFINITY : (_Float16) v;
+                        } else if (pass == 0) {                     // hi, and the exact remainder's fp16 (lo)
+                            const float v = val(i, j, r);
+                            const _Float16 h = to16<BF>(v);
+                            hv[r] = h;
+                            if constexpr (NPASS == 2) lo[i][j][r] = (_Float16) (v - (float) h);
+                        } else {
+                            if constexpr (NPASS == 2) hv[r] = lo[i][j][r];
+                        }
+                    }
+                    *(h4v *) (stg + row * RB + (((col >> 3) ^ (row & 31)) << 4) + ((col & 4) << 1)) = hv;
+                }
+            }
+            __syncthreads();
+            const int g = lane & 31;
+#pragma unroll 4
+            for (int k = 0; k < 16; ++k) {
+                const int row = wave * 32 + 2 * k + (lane >> 5), m = m0 + row;
+                const uint4 v = *(const uint4 *) (stg + row * RB + ((g ^ (row & 31)) << 4));
+                if (m >= p.M || !Q2A_ST) continue;
+                if constexpr (EPI == Q2A_EPI_PRE_H) {
+                    const int64_t orow = orq ? (int64_t) (m / p.o_rpg) * p.o_gstride + m % p.o_rpg + p.o_off : (int64_t) m + p.o_off;
+                    q2a_st(v, (uint4 *) (p.outH + orow * p.ldo + n0 + g * 8));
+                    if (p.o_dup) *(uint4 *) (p.outH + orow * p.ldo + n0 + g * 8 + p.o_dup) = v;
+                } else {
+                    q2a_half * dst = pass == 0 ? (part == 0 ? p.qh : p.kh) : (part == 0 ? p.ql : p.kl);
+                    q2a_st(v, (uint4 *) (dst + (int64_t) m * p.D + n0 - part * p.D + g * 8));
+                }
+            }
+        }
+      }
+    } else if (EPI == Q2A_EPI_QKV && part == 2) {
       if constexpr (EPI == Q2A_EPI_QKV) {
             // V^T [clip][head][d][TP]: the wave's WR rows (t) of its 64 columns (d, one head) staged [d][t] in its own LDS
             // region, then stored two d-rows per instruction, 32 lanes x 8 B (4 t) = 256 contiguous bytes per row. (Per
             // 32-row pass with one lane per d-row, every store instruction touched 64 rows of 8 B: 3.5 ms/step more than
             // the bytes cost.) T % 4 == 0, so a 4-t group never straddles a clip boundary.
             constexpr int VS = WR + 4;                       // halfs per staged d-row
-            static_assert(64 * VS * 2 <= EPI_WREG, "epilogue staging layout");
-            _Float16 * wl = (_Float16 *) (lds_raw + EPI_OFF + wave * EPI_WREG);
-            __syncthreads();
-    #pragma unroll
-            for (int i = 0; i < MI; ++i)
-    #pragma unroll
-                for (int j = 0; j < NJ; ++j)
-    #pragma unroll
-                    for (int r = 0; r < 4; ++r) wl[(j * 16 + 4 * q + r) * VS + i * 16 + l16] = to16<BF>(val(i, j, r));
-            // wave-private region: the wave's LDS writes are ordered before its reads
+            static_assert(64 * VS * 2 <= EPI_WREG && WM == 2, "epilogue staging layout");
             const int h = (cbase - 2 * p.D) >> 6;
             const int clip0 = rbase / p.T, t0 = rbase - clip0 * p.T;   // WR <= T: at most one wrap
             const int tg = lane & 31;
+            // F32-class P.V (vtl set): the lo image fp16(v - fp16(v)) too. Both images of a wave are staged at once
+            // (2 x EPI_WREG), so the two M-halves of the tile take turns over the staging LDS (waves wm == half write
+            // and store, the others wait at the barriers holding only their accumulators): staging hi, storing it and
+            // then restaging lo would keep the lo values in registers across the store loop (spills)
+            const bool two = !BF && p.vtl;
+            auto vt_epi = [&](char * region) {
+                _Float16 * wl = (_Float16 *) region;
+                _Float16 * wlo = wl + EPI_WREG / 2;
     #pragma unroll
-            for (int dd = 0; dd < 64; dd += 2) {
-                const int d = dd + (lane >> 5);
+                for (int i = 0; i < MI; ++i)
     #pragma unroll
-                for (int a = tg; a < WR / 4; a += 32) {
-                    const int m = rbase + 4 * a;
-                    if (m >= p.M) continue;
-                    const bool wrap = t0 + 4 * a >= p.T;
-                    const int clip = clip0 + (wrap ? 1 : 0), t = t0 + 4 * a - (wrap ? p.T : 0);
-                    const uint2 v = *(const uint2 *) (wl + d * VS + 4 * a);
-                    if (Q2A_ST && Q2A_ST_VT) q2a_st(v, (uint2 *) (p.vt + (((int64_t) clip * p.H + h) * 64 + d) * p.TP + t));
+                    for (int j = 0; j < NJ; ++j)
+    #pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            const float v = val(i, j, r);
+                            const _Float16 vh = to16<BF>(v);
+                            const int o = (j * 16 + 4 * q + r) * VS + i * 16 + l16;
+                            wl[o] = vh;
+                            if (two) wlo[o] = (_Float16) (v - (float) vh);
+                        }
+                // wave-private region: the wave's LDS writes are ordered before its reads
+                for (int img = 0; img < (two ? 2 : 1); ++img) {
+                    const _Float16 * src = img ? wlo : wl;
+                    q2a_half * vdst = img ? p.vtl : p.vt;
+    #pragma unroll
+                    for (int dd = 0; dd < 64; dd += 2) {
+                        const int d = dd + (lane >> 5);
+    #pragma unroll
+                        for (int a = tg; a < WR / 4; a += 32) {
+                            const int m = rbase + 4 * a;
+                            if (m >= p.M) continue;
+                            const bool wrap = t0 + 4 * a >= p.T;
+                            const int clip = clip0 + (wrap ? 1 : 0), t = t0 + 4 * a - (wrap ? p.T : 0);
+                            const uint2 v = *(const uint2 *) (src + d * VS + 4 * a);
+                            if (Q2A_ST && Q2A_ST_VT) q2a_st(v, (uint2 *) (vdst + (((int64_t) clip * p.H + h) * 64 + d) * p.TP + t));
+                        }
+                    }
                 }
+            };
+            __syncthreads();
+            if (!two) {
+                vt_epi(lds_raw + EPI_OFF + wave * EPI_WREG);
+            } else {
+                if (wm == 0) vt_epi(lds_raw + EPI_OFF + 2 * wn * EPI_WREG);
+                __syncthreads();
+                if (wm == 1) vt_epi(lds_raw + EPI_OFF + 2 * wn * EPI_WREG);
             }
       }
     } else if (EPI == Q2A_EPI_QKV || EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_PRE_H) {
@@ -1261,27 +1344,47 @@ hipError_t launch_cfg(const q2a_gemm_args & a, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Tile-regime selection is fixed at compile time (every regime sums K in the same order, so these change speed, not
+// results). Diagnostic builds (diag/build_variant.sh) may override: Q2A_GEMM_NO_NARROW / Q2A_GEMM_NARROW_ALL (64-row
+// tiles never / for every small-M GEMM), Q2A_GEMM_TILE (1 force 256-wide, 2 force 128-wide), Q2A_GEMM_PIPE (0 = no
+// 8-phase kernel), Q2A_GEMM_GROUP_M (rasterisation group), Q2A_GEMM_STAGGER_NS / _G (first-round CU stagger).
+#ifndef Q2A_GEMM_NO_NARROW
+#define Q2A_GEMM_NO_NARROW 0
+#endif
+#ifndef Q2A_GEMM_NARROW_ALL
+#define Q2A_GEMM_NARROW_ALL 0
+#endif
+#ifndef Q2A_GEMM_TILE
+#define Q2A_GEMM_TILE 0
+#endif
+#ifndef Q2A_GEMM_PIPE
+#define Q2A_GEMM_PIPE 1
+#endif
+#ifndef Q2A_GEMM_GROUP_M
+#define Q2A_GEMM_GROUP_M 0
+#endif
+#ifndef Q2A_GEMM_STAGGER_NS
+#define Q2A_GEMM_STAGGER_NS 0
+#endif
+#ifndef Q2A_GEMM_STAGGER_G
+#define Q2A_GEMM_STAGGER_G 2
+#endif
+
 // small M (one or a few clips): 64-row tiles when 128x128 tiles would leave CUs idle
 bool narrow_tiles(int M, int N) {
-    static const int off = [] { const char * v = getenv("Q2A_GEMM_NO_NARROW"); return v ? atoi(v) : 0; }();
-    static const int all = [] { const char * v = getenv("Q2A_GEMM_NARROW_ALL"); return v ? atoi(v) : 0; }();
-    return !off && (all || (int64_t) ((M + 127) / 128) * (N / 128) < 256);
+    return !Q2A_GEMM_NO_NARROW && (Q2A_GEMM_NARROW_ALL || (int64_t) ((M + 127) / 128) * (N / 128) < 256);
 }
 
 bool wide_tiles(int M, int N) {
     // big M: 256-wide tiles on 8 waves (k-quant variants keep 128 rows: the per-block accumulators double the
     // register footprint); small M (a single clip): 128x128 on 4 waves so the grid still covers the 256 CUs
-    static const int force = [] { const char * v = getenv("Q2A_GEMM_TILE"); return v ? atoi(v) : 0; }();  // 1 big, 2 small
     bool big = (int64_t) ((M + 255) / 256) * (N / 256) >= 512 && N % 256 == 0;
-    if (force == 1 && N % 256 == 0) big = true;
-    if (force == 2) big = false;
+    if (Q2A_GEMM_TILE == 1 && N % 256 == 0) big = true;
+    if (Q2A_GEMM_TILE == 2) big = false;
     return big;
 }
 
-bool pipe8_enabled() {
-    static const bool on = [] { const char * v = getenv("Q2A_GEMM_PIPE"); return v ? atoi(v) != 0 : true; }();
-    return on;
-}
+bool pipe8_enabled() { return Q2A_GEMM_PIPE != 0; }
 
 // the 8-phase kernels: 256x256 tiles, 32-bit operand offsets, K-steps in pairs (fp16) or whole Q4_K blocks
 bool pipe8_ok(const q2a_gemm_args & a, int blk) {
@@ -1334,13 +1437,14 @@ hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
 
 }  // namespace
 
-// Split-K of the small-tile residual GEMMs: OFF by default (opt-in Q2A_GEMM_SPLITK=1). Partial sums combined
-// across splits change the fp32 summation order, so a clip's output would depend on whether its batch took the
-// small-tile or the 8-phase regime; without it every regime sums K identically (batch invariance).
-static bool splitk_on() {
-    static const int on = [] { const char * v = getenv("Q2A_GEMM_SPLITK"); return v ? atoi(v) : 0; }();
-    return on != 0;
-}
+// Split-K of the small-tile residual GEMMs: compiled out of the product library (diagnostic builds only:
+// -DQ2A_GEMM_SPLITK=1). Partial sums combined across splits change the fp32 summation order, so a clip's output would
+// depend on whether its batch took the small-tile or the 8-phase regime; without it every regime sums K identically
+// (batch invariance).
+#ifndef Q2A_GEMM_SPLITK
+#define Q2A_GEMM_SPLITK 0
+#endif
+static bool splitk_on() { return Q2A_GEMM_SPLITK != 0; }
 
 int q2a_gemm_resid_ksplit(int M, int N, int K, int blk) {
     if (!splitk_on() || !(blk == 0 || blk == Q2A_BLK_BF16) || wide_tiles(M, N) || N % 128) return 0;
@@ -1360,12 +1464,9 @@ int q2a_gemm_kq_ksplit(int M, int N, int K, int blk) {
 }
 
 hipError_t q2a_launch_gemm(const q2a_gemm_args & a_in, int epi, int blk, hipStream_t s) {
-    static const int st_ns = [] { const char * v = getenv("Q2A_GEMM_STAGGER_NS"); return v ? atoi(v) : 0; }();
-    static const int st_g = [] { const char * v = getenv("Q2A_GEMM_STAGGER_G"); return v ? std::max(1, atoi(v)) : 2; }();
-    static const int grp = [] { const char * v = getenv("Q2A_GEMM_GROUP_M"); return v ? atoi(v) : 0; }();
     q2a_gemm_args a = a_in;
-    a.stagger_ns = st_ns; a.stagger_g = st_g;
-    a.group_m = grp;
+    a.stagger_ns = Q2A_GEMM_STAGGER_NS; a.stagger_g = std::max(1, Q2A_GEMM_STAGGER_G);
+    a.group_m = Q2A_GEMM_GROUP_M;
     if (a.ngroup == 2 && (epi != Q2A_EPI_STORE_F || (blk != 0 && blk != 256) || wide_tiles(a.M, a.N))) return hipErrorInvalidValue;
     if (a.ngroup == 2 && blk == 256 && (!a.dx2 || !a.beta2 || !a.gamma2 || !a.wext2)) return hipErrorInvalidValue;
     if (!(epi == Q2A_EPI_RESID || (epi == Q2A_EPI_STORE_F && a.split_store)) || !a.part || a.ldo != a.N || a.ngroup == 2)

@@ -90,6 +90,7 @@ struct q2a_gemm_args {
     const float * gamma2;
     const q2a_half * wext2;
     int split_kq;                     // allow the small-tile split-K for k-quant / Q8_0 / Q4_0 weights (q2a_gemm_kq_ksplit)
+    q2a_half * vtl;                   // Q2A_EPI_QKV: V^T lo image fp16(v - fp16(v)), same layout as vt (null = not written)
 };
 
 // the launcher's split factor for a small-tile Q2A_EPI_RESID GEMM (0 = none): a function of K only, so every batch
@@ -113,8 +114,15 @@ struct q2a_attn_args {
     q2a_half * outH;     // [clips*T][D] fp16 (F16 path) or
     float * outF;        // [clips*T][D] f32  (quantized paths)
     int bf16;            // bf16-activation mode: qh/kh/vt and outH hold bf16, ql/kl unused, one MFMA per QK^T step
+    const q2a_half * vtl;   // V^T lo image (v - fp16(v)) when q2a_attention_wants_vlo(), else unused
 };
+// Reference contract (bf16 == 0): qh/ql hold Q * Q2A_LOG2E (after the 1/sqrt(dh) scale), split hi/lo — the kernel
+// works in log2 units (P = exp2(S' - m')); every producer (QKV epilogue qscale, ggml backend prep, test entry) folds it.
+// bf16 contract: qh holds Q scaled by 1/sqrt(dh) only.
+constexpr float Q2A_LOG2E = 1.4426950408889634f;
 hipError_t q2a_launch_attention(const q2a_attn_args & a, hipStream_t s);
+// true when this build's reference-contract attention reads a V^T lo image (the QKV epilogue must then write it)
+bool q2a_attention_wants_vlo();
 
 // ---- exact-order kernels (q2a_exact.hip, compiled with -ffp-contract=off)
 struct q2a_mel_args {

@@ -18,7 +18,8 @@ TOOL_PATH = os.path.join(PKG_DIR, "bin", "q2a_tool")
 EXPORTS = (
     "q2a_last_error", "q2a_open", "q2a_pack_model", "q2a_free_host_blob", "q2a_open_device_blob", "q2a_close",
     "q2a_get_info", "q2a_reserve", "q2a_encode_device", "q2a_encode_host", "q2a_pcm_to_mel",
-    "q2a_test_linear", "q2a_test_block", "q2a_test_block_taps", "q2a_test_attention",
+    "q2a_test_linear", "q2a_test_block", "q2a_test_block_taps", "q2a_test_attention", "q2a_test_fc1_path",
+    "q2a_test_frontend", "q2a_test_pool_ln",
     "q2a_projector_open", "q2a_projector_close", "q2a_projector_get_dims", "q2a_projector_apply",
 )
 
@@ -74,6 +75,12 @@ def lib() -> C.CDLL:
         L.q2a_test_block.argtypes = [vp, C.c_int, vp, C.c_int, vp]
         L.q2a_test_block_taps.argtypes = [vp, C.c_int, vp, C.c_int, C.POINTER(vp), vp]
         L.q2a_test_attention.argtypes = [vp, vp, vp, vp, C.c_int, vp, vp]
+        # test hooks added in round 3: optional, so a diagnostic library of an earlier revision (diag/build_rev_lib.sh,
+        # A/B runs) still loads; the shipped library exports them (tests/test_library_abi.py checks EXPORTS)
+        for name, at in (("q2a_test_fc1_path", [vp, C.c_int]), ("q2a_test_frontend", [vp, vp, C.c_int64, i32p, C.c_int, vp, vp]),
+                         ("q2a_test_pool_ln", [vp, vp, C.c_int, vp, vp])):
+            if hasattr(L, name):
+                getattr(L, name).argtypes = at
         L.q2a_projector_open.restype = vp
         L.q2a_projector_open.argtypes = [C.c_char_p, C.c_int]
         L.q2a_projector_close.argtypes = [vp]
@@ -167,6 +174,19 @@ class Engine:
         arr = (C.c_void_p * 4)(*[C.c_void_p(t) if t else None for t in tap_ptrs])
         _check(lib().q2a_test_block_taps(self.h, layer, C.c_void_p(x_ptr), n_clips, arr,
                                          C.c_void_p(stream) if stream else None))
+
+    def test_frontend(self, pcm_ptr, pcm_stride, n_samples, x_ptr, stream=None):
+        ns = np.ascontiguousarray(n_samples, dtype=np.int32)
+        _check(lib().q2a_test_frontend(self.h, C.c_void_p(pcm_ptr), C.c_int64(pcm_stride),
+                                       ns.ctypes.data_as(C.POINTER(C.c_int32)), len(ns), C.c_void_p(x_ptr),
+                                       C.c_void_p(stream) if stream else None))
+
+    def test_pool_ln(self, x_ptr, n_clips, out_ptr, stream=None):
+        _check(lib().q2a_test_pool_ln(self.h, C.c_void_p(x_ptr), n_clips, C.c_void_p(out_ptr),
+                                      C.c_void_p(stream) if stream else None))
+
+    def test_fc1_path(self, path):
+        _check(lib().q2a_test_fc1_path(self.h, path))
 
     def test_attention(self, q_ptr, k_ptr, v_ptr, n_clips, out_ptr, stream=None):
         _check(lib().q2a_test_attention(self.h, C.c_void_p(q_ptr), C.c_void_p(k_ptr), C.c_void_p(v_ptr), n_clips,

@@ -1,6 +1,6 @@
 """One attention-kernel variant on the GPU (tests/test_gpu_attention_variants.py): the engine's q2a_test_attention on
-seeded random Q/K/V with whichever kernel the Q2A_ATTN_* environment of this process selects (the launcher reads it
-once per process). Writes the output to OUT.npy.    python tests/attn_variant_worker.py MODEL OUT.npy"""
+seeded random Q/K/V, through whichever library Q2A_LIB_PATH names (a diag/ variant build, or the shipped library when
+unset). Writes the output to OUT.npy.    python tests/attn_variant_worker.py MODEL OUT.npy"""
 import os
 import sys
 

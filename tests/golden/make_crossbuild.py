@@ -14,7 +14,11 @@ Runs only in the build container (needs /root/reference compiled by `make -C ora
 tests/golden/crossbuild.json (small, committed). Inputs come from bin/q2a_tool (same generator / quantizer / clip
 bytes as every other fixture; SHA-256 checked against golden.json).
 
-usage: python tests/golden/make_crossbuild.py [--workdir DIR] [--types q4_k,q8_0,f16] [--builds x86-64,avx512]
+With --tiny it does the same for the TINY model (L=2, D=256; F16 / Q4_K / Q8_0 / Q4_0 files, clip 0), recording the
+pair statistics on the full output and on the rows the tiny golden samples (rows_stride5) under "tiny_<wt>": the
+evidence for the tiny-model parity bars (tests/test_gpu_parity.py, tests/test_gpu_ggml_backend.py).
+
+usage: python tests/golden/make_crossbuild.py [--workdir DIR] [--types q4_k,q8_0,f16] [--builds x86-64,avx512] [--tiny]
 """
 from __future__ import annotations
 
@@ -109,6 +113,36 @@ def node(dump, idx):
     return np.fromfile(f[0], dtype=np.float32)
 
 
+def tiny(args, gmeta, gold, result, clip):
+    """Cross-build spread of the tiny model (no per-layer dumps): every pair of builds, full output + sampled rows."""
+    base = os.path.join(args.workdir, "tiny-f16.bin")
+    if not os.path.exists(base):
+        subprocess.check_call([TOOL, "gen-model", base, "tiny", "f16", "0x51A2", str(args.threads)])
+    rows = gold["rows_stride5"]
+    for wt in args.types.split(","):
+        model = base if wt == "f16" else os.path.join(args.workdir, f"tiny-{wt}.bin")
+        if not os.path.exists(model):
+            subprocess.check_call([TOOL, "quantize", base, model, wt, str(args.threads)])
+        assert sha(model) == gmeta["models"][f"tiny-{wt}"]["sha256"], wt
+        finals = {}
+        for b in ["avx2"] + args.builds.split(","):
+            exe = os.path.join(ROOT, "oracle", BUILDS[b], "ref_harness")
+            out = os.path.join(args.workdir, f"tiny-{wt}-{b}.out")
+            subprocess.run([exe, "encode", model, clip, out, str(args.threads), "1"], check=True, capture_output=True)
+            finals[b] = np.fromfile(out, dtype=np.float32).reshape(750, -1)
+        names = list(finals)
+        ent = {"pairs": {}}
+        for i, a in enumerate(names):
+            for c in names[i + 1:]:
+                mx, l2 = relerr(finals[c], finals[a])
+                rmx, rl2 = relerr(finals[c][rows], finals[a][rows])
+                ent["pairs"][f"{a}_vs_{c}"] = {"max_rel": mx, "rel_l2": l2, "rows_max_rel": rmx, "rows_rel_l2": rl2}
+        ref_rows = gold["tiny_f16_c0"][rows] if wt == "f16" else gold[f"tiny_{wt}_c0_rows"]
+        ent["avx2_matches_golden_rows"] = bool(np.array_equal(finals["avx2"][rows], ref_rows))
+        result[f"tiny_{wt}"] = ent
+        print("tiny", wt, json.dumps(ent), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workdir", default="/tmp/q2a_crossbuild")
@@ -116,6 +150,7 @@ def main():
     ap.add_argument("--builds", default="x86-64,avx512")
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
     ap.add_argument("--summarize-only", action="store_true", help="recompute pair statistics from existing outputs")
+    ap.add_argument("--tiny", action="store_true", help="the tiny model's spread (F16 / Q4_K / Q8_0 / Q4_0)")
     args = ap.parse_args()
     os.makedirs(args.workdir, exist_ok=True)
     with open(os.path.join(HERE, "golden.json")) as f:
@@ -128,10 +163,16 @@ def main():
     if not os.path.exists(clip):
         subprocess.check_call([TOOL, "synth-clip", clip, "480000", "0"])
     assert sha(clip) == gmeta["clips"]["0"]["sha256"]
+    gold = dict(np.load(os.path.join(HERE, "golden.npz"), allow_pickle=False))
+    if args.tiny:
+        tiny(args, gmeta, gold, result, clip)
+        with open(outp, "w") as f:
+            json.dump(result, f, indent=1, sort_keys=True)
+        print("wrote", outp)
+        return
     base = os.path.join(args.workdir, "full-f16.bin")
     if not os.path.exists(base):
         subprocess.check_call([TOOL, "gen-model", base, "full", "f16", "0x51A2", str(args.threads)])
-    gold = dict(np.load(os.path.join(HERE, "golden.npz"), allow_pickle=False))
     if args.summarize_only:
         for wt in args.types.split(","):
             finals = {b: np.fromfile(os.path.join(args.workdir, f"{wt}-{b}.out"), dtype=np.float32)

@@ -1,0 +1,56 @@
+"""The multi-GPU launch glue of bench.py: `--gpus N` starts N ranks under torch.distributed.run
+as a child process, a WORLD_SIZE that disagrees with --gpus exits 2 instead of reporting a mislabelled run, and a
+2-rank run returns ONE JSON line labelled n_gpus 2 / dp2. The RCCL path itself needs an 8-GPU node (the driver's
+SCALE run); on a 1-GPU box the 2 ranks are rehearsed on device 0 with gloo collectives (Q2A_BENCH_REHEARSE=1)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**kw):
+    e = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "Q2A_BENCH_REHEARSE")}
+    e.update(kw)
+    return e
+
+
+def test_world_size_mismatch_exits_2():
+    """A torchrun environment of 2 ranks with --gpus 1: refused before any GPU work (CPU-only check)."""
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "1", "--no-cpu-baseline"], capture_output=True, text=True,
+                       timeout=120, env=_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
+    assert r.returncode == 2, (r.returncode, r.stderr[-500:])
+    assert "WORLD_SIZE=2 but --gpus 1" in r.stderr
+    assert r.stdout.strip() == ""
+
+
+def test_more_gpus_than_visible_exits_2():
+    """--gpus 2 on a host without 2 visible devices (and no rehearsal): exit 2, no ranks started."""
+    import torch
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("host has >= 2 GPUs")
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--no-cpu-baseline"], capture_output=True, text=True,
+                       timeout=120, env=_env())
+    assert r.returncode == 2, (r.returncode, r.stderr[-500:])
+    assert "only" in r.stderr and "visible" in r.stderr
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_rehearsal(tmp_path):
+    """`python bench.py --gpus 2` (2 ranks, every rank on device 0, gloo) -> one JSON line, n_gpus 2, dp2, weak
+    scaling over the 2 x 2 clips, setup timing of the blob broadcast present."""
+    r = subprocess.run([sys.executable, "-u", BENCH, "--gpus", "2", "--steps", "2", "--warmup", "1", "--clips", "2",
+                        "--config", "f16x1", "--no-cpu-baseline", "--workdir", str(tmp_path)],
+                       capture_output=True, text=True, timeout=600, env=_env(Q2A_BENCH_REHEARSE="1"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2"
+    assert res["config"]["global_batch"] == 4 and res["scaling"] == "weak"
+    assert res["value"] > 0 and res["steps"] == 2
+    assert res["setup_s"]["weight_h2d_plus_rccl_broadcast"] > 0

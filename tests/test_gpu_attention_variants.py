@@ -1,9 +1,10 @@
-"""The opt-in F32-class attention schedules against the default kernel and an fp64 reference, each in its
-own process (the launcher reads Q2A_ATTN_* once per process): k_attn_g32 (32-key tiles), k_attn_p32 (QK^T of the next
-tile interleaved with the softmax) and k_attn_pp32 (8-wave ping-pong over three LDS-DMA stages) share one per-element
-operation sequence, so they must agree BIT FOR BIT — a missing barrier or an early read of a DMA'd stage shows up
-here as a mismatch; every variant, and the register-staged k_attn, must meet the attention bar of
-test_gpu_parity.py against float64."""
+"""The F32-class attention schedules measured and not adopted against an fp64 reference. They live in
+diag/attn_variants.hip and are built only into diagnostic libraries (diag/Makefile, made by __graft_entry__.build()),
+each loaded in its own process through Q2A_LIB_PATH — the shipped lib/libq2a.so carries none of them and reads no
+kernel-selecting environment variable. k_attn_g32 (32-key tiles), k_attn_p32 (QK^T of the next tile interleaved with
+the softmax) and k_attn_pp32 (8-wave ping-pong over three LDS-DMA stages) share one per-element operation sequence, so
+they must agree BIT FOR BIT — a missing barrier or an early read of a DMA'd stage shows up here as a mismatch; every
+variant, the register-staged k_attn and the shipped kernel must meet the attention bar against float64."""
 import os
 import subprocess
 import sys
@@ -18,8 +19,9 @@ sys.path.insert(0, HERE)
 from attn_variant_worker import B, D, T, inputs  # noqa: E402
 from conftest import rel_errors  # noqa: E402
 
-VARIANTS = {"default": {}, "k_attn": {"Q2A_ATTN_G": "0"}, "g32": {"Q2A_ATTN_G32": "1"}, "p32": {"Q2A_ATTN_P32": "1"},
-            "pp32": {"Q2A_ATTN_PP32": "1"}}
+ROOT = os.path.dirname(HERE)
+VARIANTS = {"default": None, "k_attn": "diag/attnv_k_attn/libq2a.so", "g32": "diag/attnv_g32/libq2a.so",
+            "p32": "diag/attnv_p32/libq2a.so", "pp32": "diag/attnv_pp32/libq2a.so"}
 
 
 @pytest.fixture(scope="module")
@@ -27,10 +29,12 @@ def outputs(make_model, tmp_path_factory):
     model = make_model("tiny", "f16")
     d = tmp_path_factory.mktemp("attn_variants")
     res = {}
-    for name, env in VARIANTS.items():
+    for name, lib in VARIANTS.items():
         path = str(d / f"{name}.npy")
-        e = {k: v for k, v in os.environ.items() if not k.startswith("Q2A_ATTN_")}
-        e.update(env)
+        e = {k: v for k, v in os.environ.items() if k != "Q2A_LIB_PATH"}
+        if lib:
+            assert os.path.exists(os.path.join(ROOT, lib)), f"{lib} not built (make -C diag test-variants)"
+            e["Q2A_LIB_PATH"] = os.path.join(ROOT, lib)
         subprocess.run([sys.executable, os.path.join(HERE, "attn_variant_worker.py"), model, path], env=e, check=True,
                        timeout=240)
         res[name] = np.load(path)

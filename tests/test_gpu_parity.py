@@ -263,19 +263,21 @@ def test_block_batched_matches_oracle_layer0(engines, make_model, make_clip, wt,
 
 # ---------------------------------------------------------------- deferred GELU (Q4_K fc1 -> Q8_K quantizer)
 @pytest.mark.parametrize("n_clips", [1, 30])
-def test_deferred_gelu_equals_epilogue_gelu(make_model, make_clip, n_clips, monkeypatch):
+def test_deferred_gelu_equals_epilogue_gelu(make_model, make_clip, n_clips):
     """Q4_K fc1 writes its fp16 pre-activation (Q2A_EPI_PRE_H) and the Q8_K quantizer applies the GELU table; the
-    codes, hence every output bit, must equal the GELU-epilogue + quantizer path (Q2A_GELU_IN_EPI=1)."""
+    codes, hence every output bit, must equal the GELU-epilogue + quantizer path (q2a_test_fc1_path 1) and, at the
+    8-phase batch shapes, the fused GELU + Q8_K fc1 epilogue (path 2)."""
     import q2a
     path = make_model("tiny", "q4_k")
     clips = [make_clip(0)] * n_clips
-    monkeypatch.setenv("Q2A_GELU_IN_EPI", "1")
-    e1 = q2a.Engine(path, device=0)
-    monkeypatch.setenv("Q2A_GELU_IN_EPI", "0")
-    e0 = q2a.Engine(path, device=0)
+    engines = [q2a.Engine(path, device=0) for _ in range(3)]
     try:
-        o1, _ = e1.encode_host(clips)
-        o0, _ = e0.encode_host(clips)
-        assert np.array_equal(o0, o1)
+        outs = []
+        for k, e in enumerate(engines):
+            e.test_fc1_path(k)
+            outs.append(e.encode_host(clips)[0])
+        assert np.array_equal(outs[0], outs[1])
+        assert np.array_equal(outs[0], outs[2])
     finally:
-        e0.close(); e1.close()
+        for e in engines:
+            e.close()

@@ -69,3 +69,19 @@ def test_unknown_activation_contract_is_rejected(make_model):
     assert L.q2a_pack_model_ex(path.encode(), 7, C.byref(p)) < 0
     with pytest.raises(q2a.Q2AError):
         q2a.pack_model(path, 7)
+
+
+def test_blob_version_tracks_the_q4k_layout(make_model):
+    """Blob version 3 = Q4_K gamma stored negated (-(dmin/dx)); the Q4_K gamma section of a packed blob must be
+    <= 0 everywhere, and the header must say 3 so an older build's blob (positive gamma) is refused on open."""
+    import q2a
+    path = make_model("tiny", "q4_k")
+    blob = q2a.pack_model(path)
+    magic, version = struct.unpack_from("<II", blob, 0)
+    assert magic == 0x42413251 and version == 3
+    _, blk, _, _, loff0 = header(blob)
+    assert blk == 256
+    A_GAMMA = 5
+    off = loff0[L_MAT0 + A_GAMMA]
+    gamma = np.frombuffer(blob, dtype=np.float32, count=(256 // 256) * 3 * 256, offset=off)
+    assert np.all(gamma <= 0) and np.any(gamma < 0)
