@@ -59,6 +59,11 @@ __device__ __forceinline__ void q2a_st(const V & v, V * ptr) {
 #endif
 }
 
+// fp16 outputs of the 8-phase tile through the LDS-staged row-contiguous store (diagnostic builds: 0 = register path)
+#ifndef Q2A_GEMM_STAGED_EPI
+#define Q2A_GEMM_STAGED_EPI 1
+#endif
+
 constexpr int BK = 64;
 constexpr int ROWB = BK * 2;   // bytes per LDS row (64 halves)
 constexpr int GROUP_M = 4;   // swept 2..32 at the batched shapes (Q2A_GEMM_GROUP_M): 4 best by ~1 %
@@ -946,7 +951,10 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     const float vscale = (EPI == Q2A_EPI_QKV && part == 0) ? p.qscale : 1.0f;
     const uint16_t * lut = (const uint16_t *) lds_raw;
     // per-element value before the store: bias, GELU (LDS table when staged), Q scale
+    // (no FMA contraction across the value: a later hi/lo split v - fp16(v) must see the ROUNDED v in every tile
+    // regime — contracted into fma(acc + bias, qscale, -hi) it would not, and the regimes would differ in Q lo)
     auto val = [&](int i, int j, int r) -> float {
+#pragma clang fp contract(off)
         float v = acc[i][j][r];
         if (EPI != Q2A_EPI_STORE_F || p.store_bias) v = v + bias4[j][r];
         if (LUT_EPI && EPI != Q2A_EPI_GELU_H) v = gelu_lut_c(v, lut);
@@ -969,7 +977,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
         return odd ? make_uint4(recv.x, recv.y, ub.x, ub.y) : make_uint4(ua.x, ua.y, recv.x, recv.y);
     };
     const int pcol = 16 * (q & 1) + 8 * (q >> 1);    // column of this lane's 16-B piece within a 32-column pair
-    if (PIPE == 1 && (EPI == Q2A_EPI_PRE_H || (EPI == Q2A_EPI_QKV && part < 2))) {
+    if (Q2A_GEMM_STAGED_EPI && PIPE == 1 && (EPI == Q2A_EPI_PRE_H || (EPI == Q2A_EPI_QKV && part < 2))) {
       if constexpr (PIPE == 1 && (EPI == Q2A_EPI_PRE_H || EPI == Q2A_EPI_QKV)) {
         // fp16 outputs of the 8-phase tile (fc1's pre-activation; Q / K hi and lo), staged through LDS so every store
         // instruction writes two WHOLE 512-B output rows: all 8 waves write the tile [256 rows][256 cols] into the idle

@@ -36,7 +36,8 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 TOOL = os.path.join(ROOT, "qwen2-audio-whisper-ggml_amd", "bin", "q2a_tool")
-BUILDS = {"avx2": "_ref", "x86-64": "_ref_x86-64", "avx512": "_ref_avx512"}
+BUILDS = {"avx2": "_ref", "x86-64": "_ref_x86-64", "avx512": "_ref_avx512", "sse42": "_ref_v2", "avx2-fma": "_ref_fma",
+          "shipped-o0": "_ref_o0"}
 T, D, F, L = 1500, 1280, 5120, 32
 POINTS = {"ln1": 3, "attn": 21, "ln2": 27, "gelu": 30}   # node offsets within a layer (oracle/ref_harness.cpp)
 
@@ -96,11 +97,14 @@ def pair_stats(y, ref, idx):
 
 def run_ref(build, model, clip, out, dump, nthreads):
     exe = os.path.join(ROOT, "oracle", BUILDS[build], "ref_harness")
-    if os.path.exists(dump):
-        shutil.rmtree(dump)
-    os.makedirs(dump)
+    extra = []
+    if dump is not None:
+        if os.path.exists(dump):
+            shutil.rmtree(dump)
+        os.makedirs(dump)
+        extra = [dump, "-1"]
     t0 = time.time()
-    res = subprocess.run([exe, "encode", model, clip, out, str(nthreads), "1", dump, "-1"], check=True,
+    res = subprocess.run([exe, "encode", model, clip, out, str(nthreads), "1"] + extra, check=True,
                          capture_output=True, text=True).stdout
     info = json.loads(res.strip().splitlines()[-1])
     info["wall_s"] = time.time() - t0
@@ -143,6 +147,67 @@ def tiny(args, gmeta, gold, result, clip):
         print("tiny", wt, json.dumps(ent), flush=True)
 
 
+def frontend(args, gmeta, result, clip):
+    """Cross-build spread of the FRONT END alone (log-mel -> conv1 + GELU -> conv2 + GELU -> + positions: encoder
+    node 3, the first block's input), F16 tiny and full-size files: the evidence for tests/test_gpu_isolated.py."""
+    for cfg in ("tiny", "full"):
+        model = os.path.join(args.workdir, f"{cfg}-f16.bin")
+        if not os.path.exists(model):
+            subprocess.check_call([TOOL, "gen-model", model, cfg, "f16", "0x51A2", str(args.threads)])
+        assert sha(model) == gmeta["models"][f"{cfg}-f16"]["sha256"], cfg
+        x = {}
+        for b in ["avx2"] + args.builds.split(","):
+            exe = os.path.join(ROOT, "oracle", BUILDS[b], "ref_harness")
+            dump = os.path.join(args.workdir, f"fe-{cfg}-{b}")
+            if os.path.exists(dump):
+                shutil.rmtree(dump)
+            os.makedirs(dump)
+            subprocess.run([exe, "encode", model, clip, os.path.join(dump, "out.f32"), str(args.threads), "1", dump, "4"],
+                           check=True, capture_output=True)
+            x[b] = node(dump, 3)
+            shutil.rmtree(dump)
+        names = list(x)
+        ent = {"pairs": {}}
+        for i, a in enumerate(names):
+            for c in names[i + 1:]:
+                mx, l2 = relerr(x[c], x[a])
+                ent["pairs"][f"{a}_vs_{c}"] = {"max_rel": mx, "rel_l2": l2}
+        result[f"frontend_{cfg}"] = ent
+        print("frontend", cfg, json.dumps(ent), flush=True)
+
+
+def more_clips(args, gmeta, gold, result):
+    """Full-size spread on further 30 s clips (ids from --clip-ids, no per-layer dumps): per (weight type, clip) the
+    pair statistics on the golden's 8 192 sampled indices, and the AVX2 (golden) build's sampled values into
+    tests/golden/xclips.npz, so the GPU test can average the engine's distance over several clips."""
+    base = os.path.join(args.workdir, "full-f16.bin")
+    if not os.path.exists(base):
+        subprocess.check_call([TOOL, "gen-model", base, "full", "f16", "0x51A2", str(args.threads)])
+    npz = os.path.join(HERE, "xclips.npz")
+    store = dict(np.load(npz, allow_pickle=False)) if os.path.exists(npz) else {}
+    for c in [int(v) for v in args.clip_ids.split(",")]:
+        clip = os.path.join(args.workdir, f"clip{c}.f32")
+        if not os.path.exists(clip):
+            subprocess.check_call([TOOL, "synth-clip", clip, "480000", str(c)])
+        for wt in args.types.split(","):
+            model = base if wt == "f16" else os.path.join(args.workdir, f"full-{wt}.bin")
+            if not os.path.exists(model):
+                subprocess.check_call([TOOL, "quantize", base, model, wt, str(args.threads)])
+            idx = gold[f"full_{wt}_c0_idx"]
+            finals = {}
+            for b in ["avx2"] + args.builds.split(","):
+                y, info = run_ref(b, model, clip, os.path.join(args.workdir, f"{wt}-{b}-c{c}.out"), None, args.threads)
+                finals[b] = y
+                print(wt, c, b, f"{info['wall_s']:.1f} s", flush=True)
+            names = list(finals)
+            result[f"{wt}_clip{c}"] = {"pairs": {f"{a}_vs_{d}": pair_stats(finals[d], finals[a], idx)
+                                                 for i, a in enumerate(names) for d in names[i + 1:]}}
+            store[f"full_{wt}_c{c}_val"] = finals["avx2"].reshape(-1)[idx]
+            np.savez_compressed(npz, **store)
+            with open(os.path.join(HERE, "crossbuild.json"), "w") as f:
+                json.dump(result, f, indent=1, sort_keys=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workdir", default="/tmp/q2a_crossbuild")
@@ -151,6 +216,9 @@ def main():
     ap.add_argument("--threads", type=int, default=os.cpu_count() or 8)
     ap.add_argument("--summarize-only", action="store_true", help="recompute pair statistics from existing outputs")
     ap.add_argument("--tiny", action="store_true", help="the tiny model's spread (F16 / Q4_K / Q8_0 / Q4_0)")
+    ap.add_argument("--frontend", action="store_true", help="the front end's (first block input) spread, F16 files")
+    ap.add_argument("--clip-ids", default="", help="further 30 s clip ids for the full-size spread (no layer traces)")
+    ap.add_argument("--layers-for", default="x86-64,avx512", help="builds whose per-layer code flips are traced")
     args = ap.parse_args()
     os.makedirs(args.workdir, exist_ok=True)
     with open(os.path.join(HERE, "golden.json")) as f:
@@ -164,8 +232,12 @@ def main():
         subprocess.check_call([TOOL, "synth-clip", clip, "480000", "0"])
     assert sha(clip) == gmeta["clips"]["0"]["sha256"]
     gold = dict(np.load(os.path.join(HERE, "golden.npz"), allow_pickle=False))
-    if args.tiny:
-        tiny(args, gmeta, gold, result, clip)
+    if args.clip_ids:
+        more_clips(args, gmeta, gold, result)
+        print("wrote", outp)
+        return
+    if args.tiny or args.frontend:
+        (tiny if args.tiny else frontend)(args, gmeta, gold, result, clip) if args.tiny else frontend(args, gmeta, result, clip)
         with open(outp, "w") as f:
             json.dump(result, f, indent=1, sort_keys=True)
         print("wrote", outp)
@@ -196,10 +268,14 @@ def main():
                "seconds": {"avx2": iref["wall_s"]}, "pairs": {}, "layers": {}}
         finals = {"avx2": yref}
         for b in args.builds.split(","):
-            dother = os.path.join(args.workdir, f"dump-{wt}-{b}")
+            traced = b in args.layers_for.split(",")
+            dother = os.path.join(args.workdir, f"dump-{wt}-{b}") if traced else None
             y, info = run_ref(b, model, clip, os.path.join(args.workdir, f"{wt}-{b}.out"), dother, args.threads)
             finals[b] = y
             ent["seconds"][b] = info["wall_s"]
+            print(wt, b, f"{info['wall_s']:.1f} s", flush=True)
+            if not traced:
+                continue
             codes = CODES[wt]
             rows = []
             for l in range(L):

@@ -47,7 +47,8 @@ def test_bench_two_ranks_rehearsal(tmp_path):
                         "--config", "f16x1", "--no-cpu-baseline", "--workdir", str(tmp_path)],
                        capture_output=True, text=True, timeout=600, env=_env(Q2A_BENCH_REHEARSE="1"))
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    # (gloo prints its rendezvous notes to stdout; the bench's result is the one JSON line)
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
     assert len(lines) == 1, r.stdout
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2"

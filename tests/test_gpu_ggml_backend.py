@@ -43,7 +43,7 @@ def run(harness, model, pcm, tmp_path, env_extra=None, reps=1):
 
 
 @pytest.mark.parametrize("wt", ["f16", "q4_k", "q8_0", "q4_0"])
-def test_reference_whisper_full_on_backend_tiny(harness, make_model, make_clip, golden, wt, tmp_path):
+def test_reference_whisper_full_on_backend_tiny(harness, make_model, make_clip, golden, tiny_bar, wt, tmp_path):
     _, g = golden
     emb, info = run(harness, make_model("tiny", wt), make_clip(0), tmp_path)
     assert info["backend"] == "Q2A0" and info["embd_buffer"] == "Q2A0", info
@@ -53,12 +53,13 @@ def test_reference_whisper_full_on_backend_tiny(harness, make_model, make_clip, 
     assert info["n_splits_encode"] == 1, info
     # weights were packed as the loader uploaded them (ggml-q2a.hip prepack), not at the first MUL_MAT
     assert info["repack_lazy"] == 0, info
+    # within the reference's own widest cross-build disagreement (tiny_bar, x1.0; tests/golden/crossbuild.json)
+    bar = tiny_bar(wt)
     if wt == "f16":
         mx, l2 = rel_errors(emb, g["tiny_f16_c0"])
-        assert mx < 1e-3 and l2 < 1e-4, (mx, l2)
     else:
         mx, l2 = rel_errors(emb[g["rows_stride5"]], g[f"tiny_{wt}_c0_rows"])
-        assert l2 < 1e-3 and mx < 5e-3, (mx, l2)
+    assert mx <= bar["max_rel"] and l2 <= bar["rel_l2"], (mx, l2, bar)
 
 
 def test_backend_unfused_attention_path(harness, make_model, make_clip, golden, tmp_path):
@@ -80,7 +81,7 @@ def test_reference_whisper_full_on_backend_full_size(harness, make_model, make_c
     rn = np.linalg.norm(emb.astype(np.float64), axis=1)
     rnerr = np.abs(rn - g[f"full_{wt}_c0_rownorm"]).max() / g[f"full_{wt}_c0_rownorm"].max()
     bar = xbuild_bar(wt)   # the reference's own cross-build spread
-    assert mxs < bar["max_rel"] and l2s < bar["rel_l2"] and rnerr < 20 * bar["rownorm_rel"], (mxs, l2s, rnerr, bar)
+    assert mxs <= bar["max_rel"] and l2s <= bar["rel_l2"] and rnerr < 20 * bar["rownorm_rel"], (mxs, l2s, rnerr, bar)
     if wt == "f16":
         assert mxs < 1e-3 and l2s < 1e-3
 

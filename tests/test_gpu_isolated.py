@@ -43,22 +43,25 @@ def frontend(make_model, make_clip):
 
 
 @pytest.mark.parametrize("cfg", ["tiny", "full"])
-def test_frontend_matches_oracle(frontend, cfg):
+def test_frontend_matches_oracle(frontend, frontend_bar, cfg):
     """mel bit-exact, conv operands exact (mel hi|lo x fp16 kernel, fp32 accumulation), ggml's fp16 GELU table: only
-    the fp32 summation order differs, so the first block's input agrees to F32 rounding — the reference's own builds
-    differ by 4.6e-6 here."""
+    the fp32 summation order differs — but a 1-ulp f32 difference at a GELU input rounds to the neighbouring fp16 table
+    entry now and then (1 fp16 ulp of that element: the max-rel), exactly as between two builds of the reference. Bar:
+    the reference's own widest cross-build disagreement on this output (frontend_bar, x1.0)."""
     x, ref, _, _ = frontend(cfg)
     mx, l2 = rel_errors(x, ref)
-    assert mx < 1e-5 and l2 < 1e-6, (cfg, mx, l2)
+    bar = frontend_bar(cfg)
+    assert mx <= bar["max_rel"] and l2 <= bar["rel_l2"], (cfg, mx, l2, bar)
 
 
-def test_frontend_matches_reference_samples(frontend, golden):
+def test_frontend_matches_reference_samples(frontend, frontend_bar, golden):
     """The same output against samples of the REFERENCE's own layer-0 input (tiny F16 model, clip 0)."""
     _, g = golden
     x, _, _, _ = frontend("tiny")
     idx, val = g["tiny_f16_l0_conv_out_idx"], g["tiny_f16_l0_conv_out_val"]
     mx, l2 = rel_errors(x.reshape(-1)[idx], val)
-    assert mx < 1e-5 and l2 < 1e-6, (mx, l2)
+    bar = frontend_bar("tiny")
+    assert mx <= bar["max_rel"] and l2 <= bar["rel_l2"], (mx, l2, bar)
 
 
 @pytest.mark.parametrize("cfg", ["tiny", "full"])

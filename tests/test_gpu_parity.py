@@ -105,23 +105,30 @@ def _encode(e, clips):
     return out, st
 
 
-def test_encoder_tiny_f16_vs_reference(engines, make_clip, golden):
+def test_encoder_tiny_f16_vs_reference(engines, make_clip, golden, tiny_bar):
+    """Tiny F16 model against the reference (golden AVX2 build): within the reference's own widest cross-build
+    disagreement (tiny_bar, x1.0) — the tiny model is not saturated by re-quantization chaos, so this is where an
+    implementation's own rounding shows (the fp16 P.V of round 2 sat at 1.8x this bar)."""
     _, g = golden
     e = engines("tiny", "f16")
     out, st = _encode(e, [make_clip(0)])
     assert st[0] == 0
     mx, l2 = rel_errors(out[0], g["tiny_f16_c0"])
-    assert mx < 1e-3 and l2 < 1e-4, (mx, l2)
+    bar = tiny_bar("f16")
+    assert mx <= bar["max_rel"] and l2 <= bar["rel_l2"], (mx, l2, bar)
+    assert mx < 1e-3 and l2 < 1e-4, (mx, l2)   # north-star 1e-3
 
 
 @pytest.mark.parametrize("wt", ["q4_k", "q8_0", "q4_0"])
-def test_encoder_tiny_quantized_vs_reference(engines, make_clip, golden, wt):
+def test_encoder_tiny_quantized_vs_reference(engines, make_clip, golden, tiny_bar, wt):
+    """Tiny quantized models: activation re-quantization makes single int8 flips unavoidable, for the reference's
+    own builds too; the bar is their widest disagreement on the golden's sampled rows (tiny_bar, x1.0)."""
     meta, g = golden
     e = engines("tiny", wt)
     out, st = _encode(e, [make_clip(0)])
     mx, l2 = rel_errors(out[0][g["rows_stride5"]], g[f"tiny_{wt}_c0_rows"])
-    # activation re-quantization makes single int8 flips unavoidable (see test_oracle_golden)
-    assert l2 < 1e-3 and mx < 5e-3, (mx, l2)
+    bar = tiny_bar(wt)
+    assert mx <= bar["max_rel"] and l2 <= bar["rel_l2"], (mx, l2, bar)
 
 
 def test_batch_equals_single_and_edge_clips(engines, make_clip, golden):
