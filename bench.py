@@ -220,6 +220,8 @@ def main():
     ap.add_argument("--config", default="q4k64", choices=sorted(CONFIGS))
     ap.add_argument("--clips", type=int, default=0, help="override clips per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-legs", action="store_true",
+                    help="skip the PCIe-inclusive and host-API legs (profiles/collect.sh: every launch is then the workload's own batch)")
     ap.add_argument("--cpu-reps", type=int, default=2)   # ~7 s of reference CPU work on 16 threads (+ legs)
     ap.add_argument("--workdir", default=os.environ.get("Q2A_BENCH_DIR", os.path.join(tempfile.gettempdir(), "q2a_bench")))
     args = ap.parse_args()
@@ -325,7 +327,7 @@ def main():
     # PCIe-inclusive rate (outside `value`): a serving loop over consecutive batches from pinned host memory, double
     # buffered — batch i+1's PCM goes host -> HBM and batch i-1's embd_enc HBM -> host on a copy stream while batch i
     # encodes (events order each buffer's reuse); the first upload and the last download are exposed
-    pcie_steps = 4
+    pcie_steps = 0 if args.no_host_legs else 4
     pcm_host = pcm.cpu().pin_memory()
     out_host = [torch.empty(out.shape, dtype=out.dtype).pin_memory() for _ in range(2)]
     pcm_d, out_d = [pcm, torch.empty_like(pcm)], [out, torch.empty_like(out)]
@@ -351,11 +353,11 @@ def main():
             ev["d2h"][b].record(cps)
     torch.cuda.synchronize()
     pcie_rate = qd.max_over_ranks(dist, time.perf_counter() - tp, coll_dev)
-    pcie_rate = pcie_steps * clips_per_gpu * ws * T_MEL / pcie_rate
+    pcie_rate = pcie_steps * clips_per_gpu * ws * T_MEL / pcie_rate if pcie_steps else None
     del pcm_d, out_d
     # the C host API itself (q2a_encode_host: pageable caller arrays, chunked + double-buffered inside), one call
     host_rate = None
-    if clips_per_gpu >= 2:
+    if clips_per_gpu >= 2 and not args.no_host_legs:
         pcm_np = [pcm_host[c].numpy() for c in range(clips_per_gpu)]
         out_np = np.empty((clips_per_gpu,) + eng.out_shape, dtype=np.float32)
         eng.encode_host(pcm_np, out=out_np)   # staging buffers allocated (and the output pages touched) here
@@ -437,7 +439,7 @@ def main():
                      "all_weight_gemms_tflops": round(gemm_tf, 1),
                      "mfma_busy_frac": mfma_busy, "mfma_busy_source": mfma_src},
         "cpu_baseline": cpu,
-        "pcie_inclusive_frames_per_s": round(pcie_rate, 1),
+        "pcie_inclusive_frames_per_s": round(pcie_rate, 1) if pcie_rate else None,
         "pcie_inclusive_source": f"{pcie_steps} batches from pinned host memory, H2D / D2H double-buffered on a copy stream",
         "host_api_frames_per_s": round(host_rate, 1) if host_rate else None,
         "per_kernel": per_kernel,

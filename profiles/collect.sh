@@ -11,7 +11,7 @@ mkdir -p $O
 export Q2A_BENCH_DIR=/tmp/q2ab
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 400 python3 $R/bench.py --config $CFG --steps 1 --warmup 1 --no-cpu-baseline > $O/warm.json 2> $O/warm.err
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline > $O/bench_traced.json 2> $O/trace.err
-timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_gemm|k_attn" -d $O/fetch -o run --output-format csv -- python3 $R/bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> $O/fetch.err
-timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_gemm|k_attn" -d $O/write -o run --output-format csv -- python3 $R/bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline > /dev/null 2> $O/write.err
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 $R/bench.py --config $CFG --steps 5 --warmup 1 --no-cpu-baseline --no-host-legs > $O/bench_traced.json 2> $O/trace.err
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "k_gemm|k_attn" -d $O/fetch -o run --output-format csv -- python3 $R/bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline --no-host-legs > /dev/null 2> $O/fetch.err
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "k_gemm|k_attn" -d $O/write -o run --output-format csv -- python3 $R/bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline --no-host-legs > /dev/null 2> $O/write.err
 find $O -name "*.csv" | head -20

@@ -94,9 +94,9 @@ __device__ __forceinline__ float max_lane32(float x) {
 #ifndef Q2A_ATTN_VHL
 #define Q2A_ATTN_VHL 1
 #endif
-// lazy re-basing threshold of the softmax reference point (log2 units): it moves only when a score exceeds it by more
-// than this, so P <= 2^7 stays well inside fp16 between moves
-constexpr float TAU2 = 7.0f;
+// lazy re-basing threshold of the softmax reference point (k_attn_g): a lane re-bases when the 32 P of its tile sum to
+// more than this (so each P <= 2^15 < 65504, inside fp16, between moves)
+constexpr float PLIM = 32768.0f;
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ half2_t pk_rtz(float a, float b) {
     return __builtin_bit_cast(half2_t, __builtin_amdgcn_cvt_pkrtz(a, b));
@@ -182,9 +182,16 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
     // Online softmax in log2 units: Q arrives pre-multiplied by log2(e) (the QKV epilogue folds it into the 1/8
-    // scale), so S' = log2(e)·S and P = exp2(S' - m'): one subtraction per score feeds v_exp_f32. The reference point
-    // m' of the lane's query moves (lazily) only when a score exceeds it by more than TAU2, or on the first tile.
+    // scale), so S' = log2(e)·S and P = exp2(S' - m'). The reference point m' of the lane's query enters the QK^T
+    // MFMAs as their initial accumulator (negm = -m' in all 16 C registers of each chain's first MFMA), so the
+    // accumulators hold S' - m' and feed v_exp_f32 directly: no subtraction per score. m' is set on the first tile (its
+    // max) and moves (lazily) only when a tile's P would leave the range the fp16 P halves hold: a lane whose 32 P of
+    // the tile sum to more than PLIM (then every one of them is <= PLIM < 65504) re-bases to the tile's max, so the
+    // common path needs no per-score max either.
     float m_run = 0.f, l_run = 0.f;
+    f16v negm;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) negm[r] = 0.f;
     const int ntiles = (T + KT - 1) / KT;
 
     // P of the current tile, packed two per register (truncated to fp16); PHL: plus the truncated remainders
@@ -211,73 +218,101 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
     auto qk_softmax = [&](const char * kh_img, int t) {
         const char * kl_img = kh_img + KIMG;
         f16v sc[2];
-        // S'^T for both 32-key halves of the tile (24 MFMAs, the two chains interleaved per 16-deep step); the K
-        // fragments of step st+1 are read before the MFMAs of step st, so each MFMA group waits only for its own reads
+        // S'^T - m' for both 32-key halves of the tile (24 MFMAs, the two chains interleaved per 16-deep step, each
+        // starting from negm); the K fragments of step st+1 are read before the MFMAs of step st, so each MFMA group
+        // waits only for its own reads
+        auto qk = [&]() {
+            half8 fh[2], fl[2];
+            launder_ofs();
+            auto rdk = [&](int st, int kb, half8 & hh, half8 & ll) {
+                const uint32_t off = kofs[st] + kb * 32 * KROW;   // (krow >> 1) & 7 does not depend on kb
+                hh = *(const half8 *) (kh_img + off);
+                ll = *(const half8 *) (kl_img + off);
+            };
+            rdk(0, 0, fh[0], fl[0]);
+            rdk(0, 1, fh[1], fl[1]);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) { sc[0][r] = 0.f; sc[1][r] = 0.f; }
-        half8 fh[2], fl[2];
-        launder_ofs();
-        auto rdk = [&](int st, int kb, half8 & hh, half8 & ll) {
-            const uint32_t off = kofs[st] + kb * 32 * KROW;   // (krow >> 1) & 7 does not depend on kb
-            hh = *(const half8 *) (kh_img + off);
-            ll = *(const half8 *) (kl_img + off);
-        };
-        rdk(0, 0, fh[0], fl[0]);
-        rdk(0, 1, fh[1], fl[1]);
+            for (int st = 0; st < 4; ++st) {
+                half8 nh[2], nl[2];
+                if (st < 3) { rdk(st + 1, 0, nh[0], nl[0]); rdk(st + 1, 1, nh[1], nl[1]); }
 #pragma unroll
-        for (int st = 0; st < 4; ++st) {
-            half8 nh[2], nl[2];
-            if (st < 3) { rdk(st + 1, 0, nh[0], nl[0]); rdk(st + 1, 1, nh[1], nl[1]); }
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb) {
-                sc[kb] = mma32<false>(fh[kb], qh[st], sc[kb]);
-                sc[kb] = mma32<false>(fl[kb], qh[st], sc[kb]);
-                sc[kb] = mma32<false>(fh[kb], ql[st], sc[kb]);
+                for (int kb = 0; kb < 2; ++kb) {
+                    sc[kb] = mma32<false>(fh[kb], qh[st], st == 0 ? negm : sc[kb]);
+                    sc[kb] = mma32<false>(fl[kb], qh[st], sc[kb]);
+                    sc[kb] = mma32<false>(fh[kb], ql[st], sc[kb]);
+                }
+                if (st < 3) { fh[0] = nh[0]; fh[1] = nh[1]; fl[0] = nl[0]; fl[1] = nl[1]; }
             }
-            if (st < 3) { fh[0] = nh[0]; fh[1] = nh[1]; fl[0] = nl[0]; fl[1] = nl[1]; }
-        }
-        if (t == ntiles - 1) {   // keys >= T exist only in the last tile (key of reg r: 16(r>>3) + 8hi + (r&7))
+            if (t == ntiles - 1) {   // keys >= T exist only in the last tile (key of reg r: 16(r>>3) + 8hi + (r&7))
 #pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
+                for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-                for (int r = 0; r < 16; ++r)
-                    if (t * KT + kb * 32 + 16 * (r >> 3) + 8 * hi + (r & 7) >= T) sc[kb][r] = -1e30f;
-        }
-        float mx = fmaxf(sc[0][0], sc[1][0]);
+                    for (int r = 0; r < 16; ++r)
+                        if (t * KT + kb * 32 + 16 * (r >> 3) + 8 * hi + (r & 7) >= T) sc[kb][r] = -1e30f;
+            }
+        };
+        // re-base to the tile's max (per query: both lane halves): on the first tile m' := that max (O and l are 0);
+        // later only for queries whose max exceeds m' (alpha = 1 for the others)
+        auto rebase = [&](bool first) {
+            float mx = fmaxf(sc[0][0], sc[1][0]);
 #pragma unroll
-        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(sc[0][r], sc[1][r]));   // (v_max3_f32; -fno-honor-nans)
-        mx = max_lane32(mx);
-        // re-base: on the first tile (m' := its max) or when some score exceeds m' by more than TAU2 (P <= 2^TAU2 in
-        // between, well inside fp16); rare after the first tiles
-        if (t == 0 || __any(mx > m_run + TAU2)) {
-            const float m_new = t == 0 ? mx : fmaxf(mx, m_run);
-            if (t != 0) {
-                const float alpha = __builtin_amdgcn_exp2f(m_run - m_new);
+            for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(sc[0][r], sc[1][r]));   // (v_max3_f32; -fno-honor-nans)
+            mx = max_lane32(mx);
+            const float sh = first ? mx : fmaxf(mx, 0.f);
+            if (!first) {
+                const float alpha = __builtin_amdgcn_exp2f(-sh);
                 l_run *= alpha;
 #pragma unroll
                 for (int dt = 0; dt < 2; ++dt)
 #pragma unroll
                     for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
             }
-            m_run = m_new;
-        }
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) sc[kb][r] -= sh;
+            m_run += sh;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) negm[r] = -m_run;
+        };
+        // P = exp2(S' - m') in place of the scores, and the lane's f32 sum of them
         float ls = 0.f;
+        auto exps = [&]() {
+            ls = 0.f;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    sc[kb][r] = __builtin_amdgcn_exp2f(sc[kb][r]);
+                    ls += sc[kb][r];
+                }
+        };
+        qk();
+        if (t == 0) rebase(true);
+        exps();
+        if (t != 0 && __any(ls > PLIM)) {   // rare: some P of the tile may not fit fp16; the scores again (the K stage
+            qk();                           // is still in place), re-based, and their P
+            rebase(false);
+            exps();
+        }
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int r = 0; r < 16; r += 2) {
-                const float p0 = __builtin_amdgcn_exp2f(sc[kb][r] - m_run);
-                const float p1 = __builtin_amdgcn_exp2f(sc[kb][r + 1] - m_run);
+                const float p0 = sc[kb][r], p1 = sc[kb][r + 1];
                 const half2_t hp = pk_rtz(p0, p1);
                 ph[kb][r >> 1] = hp;
                 if (PHL) {   // exact remainders p - fp16(p) (one v_fma_mix each: the fp16 operand read in place)
                     pl[kb][r >> 1] = pk_rtz(sub_half<0>(p0, hp), sub_half<1>(p1, hp));
-                    ls += p0;
-                    ls += p1;
-                } else {
-                    ls = __builtin_amdgcn_fdot2(hp, half2_t{(_Float16) 1.0f, (_Float16) 1.0f}, ls, false);
                 }
             }
+        if (!PHL) {   // the denominator of fp16 P: the sum of exactly those fp16 values
+            ls = 0.f;
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                for (int r = 0; r < 8; ++r) ls = __builtin_amdgcn_fdot2(ph[kb][r], half2_t{(_Float16) 1.0f, (_Float16) 1.0f}, ls, false);
+        }
         l_run += ls;
     };
     // O^T[d][q] += V^T[d][keys] . P^T[keys][q] for the tile whose V^T (hi [| lo]) image is at vt_img

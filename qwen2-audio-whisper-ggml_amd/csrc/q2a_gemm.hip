@@ -509,8 +509,10 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     constexpr bool LUT_EPI = PIPE && (EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_GELU_F || EPI == Q2A_EPI_CONV2 ||
                                       EPI == Q2A_EPI_GELU_Q8K);
     constexpr int EPI_OFF = LUT_EPI ? Q2A_GELU_C_BYTES : 0;
-    // per-wave epilogue staging: V^T [64 d][WR + 4 t] fp16 (QKV); the other epilogues keep their 32-row budget
-    constexpr int EPI_WREG = EPI == Q2A_EPI_QKV ? 64 * (BM / WM + 4) * 2 : 2 * 32 * (BN / WN + 8) * 2;
+    // per-wave epilogue staging: V^T [64 d][WR + 4 t] fp16 (QKV), or with the lo image the hi | lo pair of [64 d][WR/2
+    // + 4 t] (half the wave's rows at a time); the other epilogues keep their 32-row budget
+    constexpr int EPI_WREG = EPI == Q2A_EPI_QKV ? std::max(64 * (BM / WM + 4) * 2, 2 * 64 * (BM / WM / 2 + 4) * 2)
+                                                : 2 * 32 * (BN / WN + 8) * 2;
     // small-tile kernels: NS operand stages (NS - 1 K-steps of loads in flight, counted vmcnt, raw barriers) within
     // ~150 KiB of LDS. Q4_K: block b+1's scales arrive by glds in 1 KiB pieces (SBP per block, one per wave on the
     // first SP K-steps of block b) into the other of two buffers, plus one pad piece per wave for the dummy pieces
@@ -1041,57 +1043,64 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
             // region, then stored two d-rows per instruction, 32 lanes x 8 B (4 t) = 256 contiguous bytes per row. (Per
             // 32-row pass with one lane per d-row, every store instruction touched 64 rows of 8 B: 3.5 ms/step more than
             // the bytes cost.) T % 4 == 0, so a 4-t group never straddles a clip boundary.
-            constexpr int VS = WR + 4;                       // halfs per staged d-row
-            static_assert(64 * VS * 2 <= EPI_WREG && WM == 2, "epilogue staging layout");
             const int h = (cbase - 2 * p.D) >> 6;
             const int clip0 = rbase / p.T, t0 = rbase - clip0 * p.T;   // WR <= T: at most one wrap
-            const int tg = lane & 31;
-            // F32-class P.V (vtl set): the lo image fp16(v - fp16(v)) too. Both images of a wave are staged at once
-            // (2 x EPI_WREG), so the two M-halves of the tile take turns over the staging LDS (waves wm == half write
-            // and store, the others wait at the barriers holding only their accumulators): staging hi, storing it and
-            // then restaging lo would keep the lo values in registers across the store loop (spills)
+            // F32-class P.V (vtl set): the lo image fp16(v - fp16(v)) too. Every wave stages its hi | lo pair for
+            // half of its rows at a time in its own region (8 x 17 KiB for the 256-row tile), stores both, then the
+            // other half: no wave waits for another (one image at a time for the whole WR rows would keep the lo
+            // values in registers across the store loop; the whole pair at once does not fit 8 regions)
             const bool two = !BF && p.vtl;
-            auto vt_epi = [&](char * region) {
+            // stage row blocks [i0, i0 + NI) of the wave's WR rows (t) as [d][t] images with VS halves per d-row, then
+            // store them: two d-rows per instruction, 32 lanes x 8 B (4 t) each
+            auto vt_epi = [&](char * region, auto i0c, auto nic, auto vsc, bool lo) {
+                constexpr int I0 = decltype(i0c)::value, NI = decltype(nic)::value, VS = decltype(vsc)::value;
+                static_assert(64 * VS * 2 * 2 <= EPI_WREG || NI == MI, "epilogue staging layout");
                 _Float16 * wl = (_Float16 *) region;
-                _Float16 * wlo = wl + EPI_WREG / 2;
+                _Float16 * wlo = wl + 64 * VS;
     #pragma unroll
-                for (int i = 0; i < MI; ++i)
+                for (int i = I0; i < I0 + NI; ++i)
     #pragma unroll
                     for (int j = 0; j < NJ; ++j)
     #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             const float v = val(i, j, r);
                             const _Float16 vh = to16<BF>(v);
-                            const int o = (j * 16 + 4 * q + r) * VS + i * 16 + l16;
+                            const int o = (j * 16 + 4 * q + r) * VS + (i - I0) * 16 + l16;
                             wl[o] = vh;
-                            if (two) wlo[o] = (_Float16) (v - (float) vh);
+                            if (lo) wlo[o] = (_Float16) (v - (float) vh);
                         }
-                // wave-private region: the wave's LDS writes are ordered before its reads
-                for (int img = 0; img < (two ? 2 : 1); ++img) {
+                // wave-private region: the wave's LDS writes are ordered before its reads (and its reads before the
+                // next call's writes)
+                for (int img = 0; img < (lo ? 2 : 1); ++img) {
                     const _Float16 * src = img ? wlo : wl;
                     q2a_half * vdst = img ? p.vtl : p.vt;
+                    // LPR lanes per d-row (4 t = 8 B each), 64 / LPR d-rows per store instruction
+                    constexpr int LPR = NI * 4 >= 32 ? 32 : NI * 4, RPI = 64 / LPR;
     #pragma unroll
-                    for (int dd = 0; dd < 64; dd += 2) {
-                        const int d = dd + (lane >> 5);
+                    for (int dd = 0; dd < 64; dd += RPI) {
+                        const int d = dd + lane / LPR;
     #pragma unroll
-                        for (int a = tg; a < WR / 4; a += 32) {
-                            const int m = rbase + 4 * a;
+                        for (int a = lane % LPR; a < NI * 4; a += LPR) {
+                            const int ml = I0 * 16 + 4 * a, m = rbase + ml;
                             if (m >= p.M) continue;
-                            const bool wrap = t0 + 4 * a >= p.T;
-                            const int clip = clip0 + (wrap ? 1 : 0), t = t0 + 4 * a - (wrap ? p.T : 0);
+                            const bool wrap = t0 + ml >= p.T;
+                            const int clip = clip0 + (wrap ? 1 : 0), t = t0 + ml - (wrap ? p.T : 0);
                             const uint2 v = *(const uint2 *) (src + d * VS + 4 * a);
                             if (Q2A_ST && Q2A_ST_VT) q2a_st(v, (uint2 *) (vdst + (((int64_t) clip * p.H + h) * 64 + d) * p.TP + t));
                         }
                     }
                 }
             };
+            typedef std::integral_constant<int, 0> c0;
+            typedef std::integral_constant<int, MI> cmi;
+            typedef std::integral_constant<int, MI / 2> cmh;
             __syncthreads();
+            char * region = lds_raw + EPI_OFF + wave * EPI_WREG;
             if (!two) {
-                vt_epi(lds_raw + EPI_OFF + wave * EPI_WREG);
+                vt_epi(region, c0{}, cmi{}, std::integral_constant<int, WR + 4>{}, false);
             } else {
-                if (wm == 0) vt_epi(lds_raw + EPI_OFF + 2 * wn * EPI_WREG);
-                __syncthreads();
-                if (wm == 1) vt_epi(lds_raw + EPI_OFF + 2 * wn * EPI_WREG);
+                vt_epi(region, c0{}, cmh{}, std::integral_constant<int, WR / 2 + 4>{}, true);
+                vt_epi(region, cmh{}, cmh{}, std::integral_constant<int, WR / 2 + 4>{}, true);
             }
       }
     } else if (EPI == Q2A_EPI_QKV || EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_PRE_H) {
