@@ -1,0 +1,19 @@
+#!/bin/bash
+# round 3: P.V precision variants end to end (pv_parity: distance to the reference golden and ratio to the widest
+# reference build pair) and their attention time: cur = P hi/lo + V hi/lo, vhl0 = P hi/lo + V fp16, phl0 = fp16 P
+# (l = sum of those fp16 values) + V hi/lo
+cd /root/repo
+mkdir -p gpurun_out
+export Q2A_BENCH_DIR=/tmp/q2ab
+L=qwen2-audio-whisper-ggml_amd/lib/libq2a.so
+timeout -k 10 600 python3 -u diag/pv_parity.py gpurun_out/k_pv.jsonl cur=$L vhl0=diag/pv_vhl0/libq2a.so phl0=diag/pv_phl0/libq2a.so \
+    > gpurun_out/k_pv.log 2>&1 || { tail -30 gpurun_out/k_pv.log; exit 1; }
+cat gpurun_out/k_pv.jsonl
+s() { python3 -c "
+import json,sys
+d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); pk=d['per_kernel']
+print(sys.argv[1], d['ms_per_step'], 'attn', pk['attention']['ms_per_step'], 'qkv', pk['gemm_qkv']['ms_per_step'])" $1; }
+for v in cur=$L vhl0=diag/pv_vhl0/libq2a.so phl0=diag/pv_phl0/libq2a.so; do
+  n=${v%%=*}; lib=${v#*=}
+  Q2A_LIB_PATH=$PWD/$lib timeout -k 10 300 python3 bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-host-legs > gpurun_out/k_b_$n.json 2> gpurun_out/k_b_$n.err && s gpurun_out/k_b_$n.json || { tail -20 gpurun_out/k_b_$n.err; exit 1; }
+done

@@ -499,25 +499,30 @@ __global__ void k_attn_out(const float * o, tview d, int T, int H, int64_t n) {
     *(float *) (d.base + voff(d, dd, t, h, 0)) = o[(int64_t) t * H * 64 + h * 64 + dd];
 }
 
-// MUL_MAT(F32 im2col, F16 conv kernel) on the fp16 MFMA GEMM (the conv2 graph node, qwen2-whisper.cpp:1926-1931 via
-// ggml_conv_1d): every f32 activation x = hi + lo with hi = fp16(x), lo = fp16(x - hi) (22 significant bits; the
-// product with the fp16 weight and its f32 accumulation then sit at the f32 summation-order level), operand rows
-// [M][K] -> [M][2K] = hi | lo against weight rows duplicated [N][2K] = w | w
-__global__ void k_hilo_rows(const float * x, _Float16 * a, int K, int n) {
+// MUL_MAT(F32 im2col, F16 conv kernel) on the fp16 MFMA GEMM (the conv graph nodes, qwen2-whisper.cpp:1926-1931 via
+// ggml_conv_1d): every f32 activation x is written as P fp16 parts against the weight row repeated P times, operand rows
+// [M][K] -> [M][PK] against [N][PK]. P = 3 (conv_parts): hi = fp16(x), mid = fp16(x - hi), lo = fp16(x - hi - mid)
+// hold x exactly (24 bits in three 11-bit pieces), so every product is the f32 product exactly; P = 2 (hi | mid, 22
+// significant bits) where the third part would triple a large node's MFMA work for nothing (conv2: its input is the
+// GELU table's fp16 values, for which mid = lo = 0)
+__global__ void k_hilo_rows(const float * x, _Float16 * a, int K, int P, int n) {
     const int i = (int) blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int m = i / K, k = i - m * K;
     const float v = x[i];
     const _Float16 h = (_Float16) v;
-    a[(int64_t) m * 2 * K + k] = h;
-    a[(int64_t) m * 2 * K + K + k] = (_Float16) (v - (float) h);
+    const float r = v - (float) h;   // exact
+    const _Float16 md = (_Float16) r;
+    _Float16 * row = a + (int64_t) m * P * K;
+    row[k] = h;
+    row[K + k] = md;
+    if (P == 3) row[2 * K + k] = (_Float16) (r - (float) md);
 }
-__global__ void k_dup_rows(const _Float16 * w, _Float16 * o, int K, int n) {
+__global__ void k_dup_rows(const _Float16 * w, _Float16 * o, int K, int P, int n) {
     const int i = (int) blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const int r = i / K, k = i - r * K;
-    o[(int64_t) r * 2 * K + k] = w[i];
-    o[(int64_t) r * 2 * K + K + k] = w[i];
+    for (int q = 0; q < P; ++q) o[(int64_t) r * P * K + q * K + k] = w[i];
 }
 // t [R][C] -> o [C][R] (f32), 64x64 tiles through LDS
 __global__ __launch_bounds__(256) void k_transpose_f32(const float * t, float * o, int R, int C) {
@@ -960,8 +965,8 @@ bool is_weight_buffer(const ggml_tensor * w) {
     return t->buffer && ggml_backend_buffer_get_usage(t->buffer) == GGML_BACKEND_BUFFER_USAGE_WEIGHTS;
 }
 
-packed_w get_dup16(q2a_backend_ctx * b, const ggml_tensor * w, int N, int K) {
-    constexpr int DUP16 = -16;   // cache tag (not a ggml type)
+packed_w get_dup16(q2a_backend_ctx * b, const ggml_tensor * w, int N, int K, int P) {
+    const int DUP16 = -16 - P;   // cache tag (not a ggml type)
     q2a_device_ctx * d = dev_ctx(b->device);
     {
         std::lock_guard<std::mutex> lk(d->mu);
@@ -971,9 +976,9 @@ packed_w get_dup16(q2a_backend_ctx * b, const ggml_tensor * w, int N, int K) {
     packed_w p{};
     p.raw = (const char *) w->data; p.raw_bytes = ggml_nbytes(w); p.type = DUP16; p.N = N; p.K = K;
     Q2A_HIP(hipStreamSynchronize(b->stream));
-    Q2A_HIP(hipMalloc(&p.dev, (size_t) N * 2 * K * 2));
+    Q2A_HIP(hipMalloc(&p.dev, (size_t) N * P * K * 2));
     const int n = N * K;
-    hipLaunchKernelGGL(k_dup_rows, grid1(n), dim3(256), 0, b->stream, (const _Float16 *) w->data, (_Float16 *) p.dev, K, n);
+    hipLaunchKernelGGL(k_dup_rows, grid1(n), dim3(256), 0, b->stream, (const _Float16 *) w->data, (_Float16 *) p.dev, K, P, n);
     Q2A_HIP(hipStreamSynchronize(b->stream));
     std::lock_guard<std::mutex> lk(d->mu);
     d->wcache.push_back(p);
@@ -994,8 +999,12 @@ bool conv_hilo_ok(const ggml_tensor * op) {
     if (!ggml_is_contiguous(x) || !ggml_is_contiguous(w) || !ggml_is_contiguous(op)) return false;
     if (x->ne[2] != 1 || x->ne[3] != 1 || w->ne[2] != 1 || w->ne[3] != 1) return false;
     const int64_t K = x->ne[0], M = x->ne[1], N = w->ne[1];
-    return K % 32 == 0 && N % 128 == 0 && 2 * K <= 16384 && M * K < (1ll << 30) && N * K < (1ll << 30);
+    return K % 64 == 0 && N % 128 == 0 && 2 * K <= 16384 && M * K < (1ll << 30) && N * K < (1ll << 30);
 }
+
+// operand parts of a conv MUL_MAT: the exact three-part split where it is cheap (conv1: K = 3 x 128 mel bins), the
+// two-part one for the large conv2 node (K = 3 x 1280, fp16-exact GELU inputs)
+int conv_parts(int K) { return 3 * K <= 4096 ? 3 : 2; }
 
 // out[n][m] = sum_k x[m][k] * w[n][k] (ggml MUL_MAT with src0 = x F32, src1 = w F16): GEMM [M][N] into the scratch,
 // then one transpose into the node's [N][M] layout
@@ -1003,29 +1012,30 @@ void run_mm_conv_hilo(q2a_backend_ctx * b, ggml_tensor * op) {
     const ggml_tensor * x = op->src[0];
     const ggml_tensor * w = op->src[1];
     const int K = (int) x->ne[0], M = (int) x->ne[1], N = (int) w->ne[1];
+    const int P = conv_parts(K);
     const bool cached = is_weight_buffer(w);
-    const packed_w wd = cached ? get_dup16(b, w, N, K) : packed_w{};
-    const int S = q2a_gemm_resid_ksplit(M, N, 2 * K, 0);
-    const size_t a_bytes = ((size_t) M * 2 * K * 2 + 255) & ~size_t(255);
+    const packed_w wd = cached ? get_dup16(b, w, N, K, P) : packed_w{};
+    const int S = q2a_gemm_resid_ksplit(M, N, P * K, 0);
+    const size_t a_bytes = ((size_t) M * P * K * 2 + 255) & ~size_t(255);
     const size_t t_bytes = ((size_t) M * N * 4 + 255) & ~size_t(255);
     const size_t p_bytes = S > 1 ? ((size_t) S * M * N * 4 + 255) & ~size_t(255) : 0;
-    const size_t d_bytes = cached ? 0 : (size_t) N * 2 * K * 2;
+    const size_t d_bytes = cached ? 0 : (size_t) N * P * K * 2;
     char * s = (char *) scratch(b, a_bytes + t_bytes + p_bytes + d_bytes);
     b->quant_src = nullptr;
     const _Float16 * wdup = (const _Float16 *) wd.dev;
     if (!cached) {   // not a model weight: duplicate this call's bytes into the scratch
         _Float16 * dst = (_Float16 *) (s + a_bytes + t_bytes + p_bytes);
-        hipLaunchKernelGGL(k_dup_rows, grid1((int64_t) N * K), dim3(256), 0, b->stream, (const _Float16 *) w->data, dst, K, N * K);
+        hipLaunchKernelGGL(k_dup_rows, grid1((int64_t) N * K), dim3(256), 0, b->stream, (const _Float16 *) w->data, dst, K, P, N * K);
         wdup = dst;
     }
     _Float16 * A = (_Float16 *) s;
     float * tmp = (float *) (s + a_bytes);
     const int n = M * K;
-    hipLaunchKernelGGL(k_hilo_rows, grid1(n), dim3(256), 0, b->stream, (const float *) x->data, A, K, n);
+    hipLaunchKernelGGL(k_hilo_rows, grid1(n), dim3(256), 0, b->stream, (const float *) x->data, A, K, P, n);
     q2a_gemm_args a;
     memset(&a, 0, sizeof(a));
-    a.A = (const q2a_half *) A; a.lda = 2 * K; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
-    a.M = M; a.N = N; a.K = 2 * K; a.ldw = 2 * K;
+    a.A = (const q2a_half *) A; a.lda = P * K; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
+    a.M = M; a.N = N; a.K = P * K; a.ldw = P * K;
     a.W = (const q2a_half *) wdup;
     a.outF = tmp; a.ldo = N;
     a.gelu_tab = gelu_table(b->device);

@@ -47,7 +47,7 @@ void set_err(const char * fmt, ...) {
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t BLOB_MAGIC = 0x42413251u;   // "Q2AB"
 // version 3: the Q4_K gamma array holds -(dmin/dx) (stored negated); a version-2 blob (positive gamma) is refused
-constexpr uint32_t BLOB_VERSION = 3;
+constexpr uint32_t BLOB_VERSION = 4;   // 4: conv1 taps against the three-part mel operand
 constexpr int MAX_LAYERS = 64;
 constexpr size_t HEADER_BYTES = 32768;
 
@@ -99,7 +99,7 @@ bool plan(blob_header & h, const q2a_hparams & hp, int wtype, int act) {
     const uint64_t kx = f32 && !act ? 3 : 1;
     uint64_t off = HEADER_BYTES;
     auto take = [&](uint64_t bytes) { const uint64_t o = off; off += (bytes + 255) & ~uint64_t(255); return o; };
-    h.goff[G_CONV1_W] = take((uint64_t) d.D * 3 * (f32 ? 3 : 2) * d.M * 2);
+    h.goff[G_CONV1_W] = take((uint64_t) d.D * 3 * 3 * d.M * 2);
     h.goff[G_CONV1_B] = take((uint64_t) d.D * 4);
     h.goff[G_CONV2_W] = take((uint64_t) d.D * 3 * (f32 ? 2 : 1) * d.D * 2);
     h.goff[G_CONV2_B] = take((uint64_t) d.D * 4);
@@ -320,9 +320,9 @@ int pack(const char * path, std::vector<uint8_t> & out, int act = 0) {
             hi = q2a_fp32_to_fp16(x);
             lo = q2a_fp32_to_fp16(x - q2a_fp16_to_fp32(hi));
         };
-        // conv1: [oc][ic][k] -> k-major taps against the mel operand rows: F16 [w | w] x [mel_h | mel_l];
-        // F32 [wh | wh | wl] x [mel_h | mel_l | mel_h]
-        const int P1 = f32 ? 3 : 2;
+        // conv1: [oc][ic][k] -> k-major taps against the mel operand rows: F16 [w | w | w] x [mel_h | mel_m | mel_l]
+        // (exact); F32 [wh | wh | wl] x [mel_h | mel_l | mel_h]
+        const int P1 = 3;
         uint16_t * w = (uint16_t *) (blob + h.goff[G_CONV1_W]);
         for (int oc = 0; oc < d.D; ++oc)
             for (int ic = 0; ic < d.M; ++ic)
@@ -332,7 +332,7 @@ int pack(const char * path, std::vector<uint8_t> & out, int act = 0) {
                     uint16_t * t = w + (size_t) oc * 3 * P1 * d.M + (size_t) k * P1 * d.M + ic;
                     t[0] = hi;
                     t[d.M] = hi;
-                    if (f32) t[2 * d.M] = lo;
+                    t[2 * d.M] = f32 ? lo : hi;
                 }
         // conv2: k-major taps over three consecutive conv1 output rows: F16 [w]; F32 [wh | wl] x rows [y | y]
         const int P2 = f32 ? 2 : 1;
@@ -669,7 +669,7 @@ int reserve(q2a_engine * e, int B) {
     auto take = [&](size_t bytes) { const size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
     const size_t o_meta = take((size_t) B * 4 * 4);
     const size_t o_mel = take((size_t) B * d.M * d.TM * 4);
-    const size_t o_xc1 = take((size_t) B * (d.TM + 2) * (e->f32 ? 3 : 2) * d.M * 2);
+    const size_t o_xc1 = take((size_t) B * (d.TM + 2) * 3 * d.M * 2);
     const size_t o_y1 = take((size_t) B * (d.TM + 1) * d.D * 2 * (e->f32 ? 2 : 1));
     const size_t o_X = take((size_t) BT * d.D * 4);
     const size_t o_actD = take((size_t) BT * d.D * 2 * e->kx);
@@ -905,9 +905,9 @@ int run_frontend(q2a_engine * e, const float * pcm, int64_t stride, int B, int m
     ma.filters = e->g<const float *>(G_FILT); ma.tab = e->g<const float *>(G_TAB);
     if (int rc = ensure_frange(e, s)) return rc;
     ma.frange = e->frange;
-    ma.mel = e->mel; ma.clip_max = cmax; ma.xc1 = e->xc1; ma.xc_parts = e->f32 ? 3 : 2;
+    ma.mel = e->mel; ma.clip_max = cmax; ma.xc1 = e->xc1; ma.xc_f32 = e->f32 ? 1 : 0;
     PLAUNCH(e, s, Q2A_PROF_MEL, q2a_launch_mel(ma, s));
-    const int P1 = e->f32 ? 3 : 2, P2 = e->f32 ? 2 : 1;   // operand parts per mel row / per conv1 output row
+    const int P1 = 3, P2 = e->f32 ? 2 : 1;   // operand parts per mel row / per conv1 output row
     {   // conv1: implicit GEMM, A row t = xc1 rows t..t+2 of its clip (3 x P1 x M halves), K = 3 P1 M
         q2a_gemm_args a;
         memset(&a, 0, sizeof(a));
@@ -1205,7 +1205,7 @@ int q2a_pcm_to_mel(q2a_engine * e, const float * pcm, int n_samples, float * mel
         ma.filters = e->g<const float *>(G_FILT); ma.tab = e->g<const float *>(G_TAB);
         if (int rc = ensure_frange(e, e->stream)) return rc;
         ma.frange = e->frange;
-        ma.mel = e->mel; ma.clip_max = e->meta + 3; ma.xc1 = e->xc1; ma.xc_parts = e->f32 ? 3 : 2;
+        ma.mel = e->mel; ma.clip_max = e->meta + 3; ma.xc1 = e->xc1; ma.xc_f32 = e->f32 ? 1 : 0;
         if (q2a_launch_mel(ma, s) != hipSuccess) { rc = Q2A_ERR_HIP; break; }
         if (hipMemcpyAsync(chunk.data(), e->mel, chunk.size() * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipMemcpyAsync(&cmax, e->meta + 3, 4, hipMemcpyDeviceToHost, s) != hipSuccess ||

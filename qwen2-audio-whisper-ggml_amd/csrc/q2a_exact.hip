@@ -138,8 +138,11 @@ __global__ __launch_bounds__(256) void k_mel_frames(const q2a_mel_args p) {
     if (lane == 0) atomicMax(p.clip_max + c, f2ord(lmax));
 }
 
-// clamp to (max - 8), (x + 4) / 4 (:2633-2649), then write the conv1 operand rows [hi(128) | lo(128)] as fp16
-// (x = hi + lo to 22 bits, so the fp16 MFMA conv reproduces the F32 im2col x F32-upcast-kernel product).
+// clamp to (max - 8), (x + 4) / 4 (:2633-2649), then write the conv1 operand rows as three fp16 parts. F16 conv kernels:
+// [hi | mid | lo] with hi + mid + lo = the f32 value exactly (24 significant bits in three 11-bit pieces; pieces below
+// fp16's 2^-24 resolution are lost only for |x| < 2^-1, an absolute error < 2^-25), so the fp16 MFMA conv's products
+// are the F32 im2col x F32-upcast-kernel products exactly. F32 kernels (all-F32 files): [hi | lo | hi] against
+// [wh | wh | wl] (the product to 22 bits).
 __global__ __launch_bounds__(256) void k_mel_norm(const q2a_mel_args p) {
     __shared__ float tile[128][65];
     const int c = blockIdx.y, t0 = blockIdx.x * 64;
@@ -156,18 +159,19 @@ __global__ __launch_bounds__(256) void k_mel_norm(const q2a_mel_args p) {
         tile[j][tt] = v;
     }
     __syncthreads();
-    const int nm = p.n_mel, P = p.xc_parts;
-    q2a_half * xc = p.xc1 + (int64_t) c * (p.n_frames_win + 2) * P * nm;
+    const int nm = p.n_mel;
+    q2a_half * xc = p.xc1 + (int64_t) c * (p.n_frames_win + 2) * 3 * nm;
     for (int e = threadIdx.x; e < nm * 64; e += 256) {
         const int tt = e / nm, j = e % nm;
         if (t0 + tt >= p.n_frames_win) continue;
         const float v = tile[j][tt];
         const _Float16 h = (_Float16) v;
-        const _Float16 l = (_Float16) (v - (float) h);
-        q2a_half * row = xc + (int64_t) (t0 + tt + 1) * P * nm;
+        const float r = v - (float) h;             // exact (|r| <= ulp_fp16(v) / 2)
+        const _Float16 m = (_Float16) r;
+        q2a_half * row = xc + (int64_t) (t0 + tt + 1) * 3 * nm;
         row[j] = h;
-        row[nm + j] = l;
-        if (P == 3) row[2 * nm + j] = h;   // F32 kernel: [h | l | h] x [wh | wh | wl]
+        row[nm + j] = m;
+        row[2 * nm + j] = p.xc_f32 ? h : (_Float16) (r - (float) m);   // (r - m exact as well)
     }
 }
 

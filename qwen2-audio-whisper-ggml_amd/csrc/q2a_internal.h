@@ -139,9 +139,9 @@ struct q2a_mel_args {
     const int2 * frange;        // [n_mel] non-zero 4-aligned bin-group range per filter (q2a_launch_filter_ranges), or NULL
     float * mel;                // [clips][n_mel][n_frames_win] raw log10 values
     int32_t * clip_max;         // [clips] ordered-int encoding of the max over ALL frames
-    q2a_half * xc1;             // [clips][n_frames_win+2][parts*n_mel] conv1 operand (hi|lo or hi|lo|hi per row),
-                                //   rows 0/last = 0
-    int xc_parts;               // 2 (F16 conv kernel) or 3 (F32 conv kernel, all-F32 model files)
+    q2a_half * xc1;             // [clips][n_frames_win+2][3*n_mel] conv1 operand, rows 0/last = 0: F16 conv kernel
+                                //   hi|mid|lo (the f32 mel value exactly), F32 kernel hi|lo|hi
+    int xc_f32;                 // 1: all-F32 model files (F32 conv kernel, hi|lo|hi against wh|wh|wl)
 };
 hipError_t q2a_launch_mel(const q2a_mel_args & a, hipStream_t s);
 hipError_t q2a_launch_filter_ranges(const float * filters, int n_mel, int n_bins, int2 * out, hipStream_t s);

@@ -72,13 +72,14 @@ def test_unknown_activation_contract_is_rejected(make_model):
 
 
 def test_blob_version_tracks_the_q4k_layout(make_model):
-    """Blob version 3 = Q4_K gamma stored negated (-(dmin/dx)); the Q4_K gamma section of a packed blob must be
-    <= 0 everywhere, and the header must say 3 so an older build's blob (positive gamma) is refused on open."""
+    """Blob version 3 = Q4_K gamma stored negated (-(dmin/dx)); version 4 = conv1 taps against the three-part mel
+    operand. The Q4_K gamma section of a packed blob must be <= 0 everywhere, and the header must say 4 so an older
+    build's blob (positive gamma, two-part conv1 taps) is refused on open."""
     import q2a
     path = make_model("tiny", "q4_k")
     blob = q2a.pack_model(path)
     magic, version = struct.unpack_from("<II", blob, 0)
-    assert magic == 0x42413251 and version == 3
+    assert magic == 0x42413251 and version == 4
     _, blk, _, _, loff0 = header(blob)
     assert blk == 256
     A_GAMMA = 5
