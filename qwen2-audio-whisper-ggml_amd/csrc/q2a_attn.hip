@@ -94,6 +94,11 @@ __device__ __forceinline__ float max_lane32(float x) {
 #ifndef Q2A_ATTN_VHL
 #define Q2A_ATTN_VHL 1
 #endif
+// QK^T terms of k_attn_g (diagnostic builds only): 3 = Kh.Qh + Kl.Qh + Kh.Ql (the contract); 21 = without Kl.Qh (K as
+// fp16); 22 = without Kh.Ql (Q as fp16)
+#ifndef Q2A_ATTN_QK_TERMS
+#define Q2A_ATTN_QK_TERMS 3
+#endif
 // lazy re-basing threshold of the softmax reference point (k_attn_g): a lane re-bases when the 32 P of its tile sum to
 // more than this (so each P <= 2^15 < 65504, inside fp16, between moves)
 constexpr float PLIM = 32768.0f;
@@ -114,14 +119,20 @@ __device__ __forceinline__ float sub_half(float p, half2_t h) {
 // (16 KiB each) and ONE V^T hi | lo stage (16 KiB): 48 KiB, three workgroups per CU (a second V stage would make it
 // 64 KiB and two per CU). Tile t's V^T is DMA'd at the start of its iteration beside K(t+1), lands under QK^T(t) and
 // the softmax, and a second barrier per tile separates the P.V reads from the next overwrite.
-__global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
+#ifndef Q2A_ATTN_VDB
+#define Q2A_ATTN_VDB 0     // 1: V^T hi | lo double-buffered beside K (64 KiB, one barrier per tile; diagnostic builds)
+#endif
+#ifndef Q2A_ATTN_G_OCC
+#define Q2A_ATTN_G_OCC (Q2A_ATTN_VDB ? 2 : 3)   // workgroups per CU the register budget is sized for
+#endif
+__global__ __launch_bounds__(256, Q2A_ATTN_G_OCC) void k_attn_g(const q2a_attn_args p) {
     typedef attn_lds_g LY;
-    constexpr bool VHL = Q2A_ATTN_VHL, PHL = Q2A_ATTN_PHL;
+    constexpr bool VHL = Q2A_ATTN_VHL, PHL = Q2A_ATTN_PHL, VDB = VHL && Q2A_ATTN_VDB;
     constexpr int KROW = LY::KROW, VROW = LY::VROW;
-    constexpr int KIMG = KT * KROW, VIMG = 64 * VROW, STAGE = 2 * KIMG + (VHL ? 0 : VIMG);
+    constexpr int KIMG = KT * KROW, VIMG = 64 * VROW, STAGE = 2 * KIMG + (VHL ? (VDB ? 2 * VIMG : 0) : VIMG);
     __shared__ __attribute__((aligned(16))) char ldsA[STAGE];
     __shared__ __attribute__((aligned(16))) char ldsB[STAGE];
-    __shared__ __attribute__((aligned(16))) char ldsV[VHL ? 2 * VIMG : 16];
+    __shared__ __attribute__((aligned(16))) char ldsV[VHL && !VDB ? 2 * VIMG : 16];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int T = p.T, D = p.D;
     const int nq = (T + 127) / 128, total = (int) gridDim.x;
@@ -238,8 +249,8 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
 #pragma unroll
                 for (int kb = 0; kb < 2; ++kb) {
                     sc[kb] = mma32<false>(fh[kb], qh[st], st == 0 ? negm : sc[kb]);
-                    sc[kb] = mma32<false>(fl[kb], qh[st], sc[kb]);
-                    sc[kb] = mma32<false>(fh[kb], ql[st], sc[kb]);
+                    if (Q2A_ATTN_QK_TERMS != 21) sc[kb] = mma32<false>(fl[kb], qh[st], sc[kb]);
+                    if (Q2A_ATTN_QK_TERMS != 22) sc[kb] = mma32<false>(fh[kb], ql[st], sc[kb]);
                 }
                 if (st < 3) { fh[0] = nh[0]; fh[1] = nh[1]; fl[0] = nl[0]; fl[1] = nl[1]; }
             }
@@ -340,13 +351,13 @@ __global__ __launch_bounds__(256, 3) void k_attn_g(const q2a_attn_args p) {
             }
     };
 
-    dma_tile(ldsA, ldsA + 2 * KIMG, 0, true, !VHL);
+    dma_tile(ldsA, ldsA + 2 * KIMG, 0, true, !VHL || VDB);
     // the Q fragments must be complete before the loop (an asm "use" makes the waitcnt pass wait for them here):
     // otherwise their loads stay pending at the loop header, merge with the next-tile prefetch and every
     // iteration's QK^T MFMAs wait on that prefetch
     asm volatile("" :: "v"(qh[0]), "v"(qh[1]), "v"(qh[2]), "v"(qh[3]), "v"(ql[0]), "v"(ql[1]), "v"(ql[2]), "v"(ql[3]));
     __syncthreads();   // (waits for the DMA: a pending LDS-DMA is a vmcnt event)
-    if constexpr (VHL) {
+    if constexpr (VHL && !VDB) {
         // iteration t: V(t) -> V stage and K(t+1) -> the other K stage; QK^T(t) + softmax; barrier (V(t) landed);
         // P.V(t); barrier (every wave done with the V stage and K(t)'s stage)
         for (int t = 0; t < ntiles; t += 2) {
