@@ -6,17 +6,16 @@
 //
 // Numerics (reference contract): the reference computes QK^T, the softmax and P.V all in F32. Here Q and K arrive as
 // fp16 hi/lo pairs (x = hi + lo, 22 significant bits) and S = Kh.Qh + Kl.Qh + Kh.Ql on fp16 MFMA with fp32
-// accumulation (the lo.lo term is below 2^-22 relative), i.e. F32-class scores. The P.V product's precision is set
-// by Q2A_ATTN_PHL / Q2A_ATTN_VHL below (hi/lo fp16 splits of P and of V: F32-class when both are on). Online softmax
-// keeps a running max/sum per query; the 1/sum normalisation is applied once at the end.
+// accumulation (the lo.lo term is below 2^-22 relative), i.e. F32-class scores; P and V^T enter the P.V MFMA as hi/lo
+// pairs too (Vh.Ph + Vh.Pl + Vl.Ph). Online softmax keeps a running reference point and sum per query; the 1/sum
+// normalisation is applied once at the end.
 //
 // Kernels (the schedules measured and not adopted live in diag/attn_variants.hip, built only into diag libraries):
-//   k_attn_g       reference contract: one 256-thread workgroup = 4 waves x 32 queries of one (clip, head), K/V tiles
-//                  of 64 keys by LDS-DMA into two LDS stages
+//   k_attn_t       reference contract: one 256-thread workgroup = 4 waves x 32 queries of one (clip, head), K/V tiles
+//                  of 32 keys by LDS-DMA into three LDS stages, software-pipelined, 16x16x32 MFMAs
 //   k_attn_pp<BF>  bf16-activation contract (BF = true): 8-wave ping-pong, one 512-thread workgroup = 256 queries
-// S^T = K.Q^T is computed with v_mfma_f32_32x32x16_f16 so each lane owns one query column (softmax is lane-local plus
-// one lane^32 exchange) and the S accumulator feeds the P.V MFMA as its B operand with no data movement
-// (cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand").
+// The S accumulator feeds the P.V MFMA as its B operand with no data movement (K rows permuted so a lane's scores are
+// the keys of its P.V fragment; cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand").
 #include "q2a_internal.h"
 
 #include <cstdlib>
@@ -26,6 +25,7 @@ namespace {
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef _Float16 half4 __attribute__((ext_vector_type(4)));
 typedef float f16v __attribute__((ext_vector_type(16)));
+typedef float f4v_t __attribute__((ext_vector_type(4)));
 typedef __bf16 bf8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void * lds_ptr_t;
 
@@ -79,7 +79,7 @@ __device__ __forceinline__ float max_lane32(float x) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
-// P.V precision of k_attn_g (reference: F32 P and V, qwen2-whisper.cpp:2088-2102):
+// P.V precision of the diagnostic k_attn_g (diag/attn_variants.hip; reference: F32 P and V, qwen2-whisper.cpp:2088-2102):
 //   Q2A_ATTN_PHL = 1: P = Ph + Pl, two fp16 halves (Ph = P truncated to fp16, Pl = the exact f32 remainder truncated
 //                     to fp16: 22 significant bits), two P.V MFMAs per fragment
 //   Q2A_ATTN_VHL = 1: V^T = Vh + Vl likewise (the QKV epilogue writes the lo image), one more MFMA per fragment
@@ -99,7 +99,7 @@ __device__ __forceinline__ float max_lane32(float x) {
 #ifndef Q2A_ATTN_QK_TERMS
 #define Q2A_ATTN_QK_TERMS 3
 #endif
-// lazy re-basing threshold of the softmax reference point (k_attn_g): a lane re-bases when the 32 P of its tile sum to
+// lazy re-basing threshold of the softmax reference point: a lane re-bases when the P of its tile (8 or 16 per lane) sum to
 // more than this (so each P <= 2^15 < 65504, inside fp16, between moves)
 constexpr float PLIM = 32768.0f;
 typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
@@ -115,302 +115,341 @@ __device__ __forceinline__ float sub_half(float p, half2_t h) {
     else asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(p));
     return r;
 }
-// LDS: VHL = 0: two stages of K hi | K lo | V^T (24 KiB each), one barrier per tile. VHL = 1: two stages of K hi | K lo
-// (16 KiB each) and ONE V^T hi | lo stage (16 KiB): 48 KiB, three workgroups per CU (a second V stage would make it
-// 64 KiB and two per CU). Tile t's V^T is DMA'd at the start of its iteration beside K(t+1), lands under QK^T(t) and
-// the softmax, and a second barrier per tile separates the P.V reads from the next overwrite.
-#ifndef Q2A_ATTN_VDB
-#define Q2A_ATTN_VDB 0     // 1: V^T hi | lo double-buffered beside K (64 KiB, one barrier per tile; diagnostic builds)
+// ---- reference contract (k_attn_t): the QK^T MFMAs of tile t+1 in one scheduling region with the softmax VALU of
+// tile t (exp2, row sum, P hi/lo split: independent of those MFMAs), then the P.V MFMAs of tile t; 32-key tiles, three
+// LDS stages of 16 KiB (K hi | K lo | V^T hi | V^T lo): iteration t reads K(t+1) from one, V(t) (and, on the rare
+// re-base path, K(t)) from another, and DMAs tile t+2 into the third; one barrier per tile. The re-base path (a lane's
+// P of the tile sum past PLIM) recomputes tile t's scores from K(t), re-bases, and moves the already computed
+// S(t+1) - m' by the same shift.
+#ifndef Q2A_ATTN_S_SCHED
+#define Q2A_ATTN_S_SCHED 1   // sched_group_barrier interleaving (0: the compiler's own order; diagnostic builds)
 #endif
-#ifndef Q2A_ATTN_G_OCC
-#define Q2A_ATTN_G_OCC (Q2A_ATTN_VDB ? 2 : 3)   // workgroups per CU the register budget is sized for
-#endif
-__global__ __launch_bounds__(256, Q2A_ATTN_G_OCC) void k_attn_g(const q2a_attn_args p) {
-    typedef attn_lds_g LY;
-    constexpr bool VHL = Q2A_ATTN_VHL, PHL = Q2A_ATTN_PHL, VDB = VHL && Q2A_ATTN_VDB;
-    constexpr int KROW = LY::KROW, VROW = LY::VROW;
-    constexpr int KIMG = KT * KROW, VIMG = 64 * VROW, STAGE = 2 * KIMG + (VHL ? (VDB ? 2 * VIMG : 0) : VIMG);
+constexpr int KS = 32;   // keys per tile
+// fp16 remainder pair p - h (h = the truncated fp16 pair of p0, p1) in two v_fma_mix{lo,hi}_f16: the exact f32
+// difference rounded once to fp16 (RNE), written straight into the packed register
+__device__ __forceinline__ half2_t rem_pair(float p0, float p1, half2_t h) {
+    half2_t r;
+    asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(p0));
+    asm("v_fma_mixhi_f16 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(r) : "v"(h), "v"(p1));
+    return r;
+}
+// The matrix work is v_mfma_f32_16x16x32_f16, not 32x32x16 (same cycles per flop; the attention runs power-limited,
+// ~1.6 GHz against the GEMMs' ~2.0, and the 16x16 form draws less per flop: MI355X_MICROARCH.md, "bare bf16 MFMA
+// loops"; the same software pipeline on 32x32x16 tiles, diag k_attn_s, measured 58.9 vs 56.0 ms/step). A wave = 32 queries as two 16-query blocks qb. S^T tile of 16 keys x 16 queries: lane l holds query
+// 16qb + (l&15) and accumulator rows 4(l>>4) + r; the K row loaded into MFMA row i of key block kb is key
+// 8(i>>2) + 4kb + (i&3), so lane group g = l>>4 holds keys 8g..8g+3 (kb 0) and 8g+4..8g+7 (kb 1): exactly the 8
+// contiguous keys of its P.V B fragment, whose V^T operand is granule g of the V^T row (one 16-B read).
+__device__ __forceinline__ f4v_t mma16(half8 a, half8 b, f4v_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+// x combined with the value of lane ^ 16 / lane ^ 32 (v_permlane16/32_swap: one of the two results is the lane's own)
+__device__ __forceinline__ float max_lane16(float x) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+__device__ __forceinline__ float sum_lane16(float x) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float sum_lane32(float x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
+    constexpr int KROW = 128, VROW = 64;
+    constexpr int KIMG = KS * KROW, VIMG = 64 * VROW;
+    constexpr int STAGE = 2 * KIMG + 2 * VIMG;                   // Kh | Kl | Vh^T | Vl^T of 32 keys
     __shared__ __attribute__((aligned(16))) char ldsA[STAGE];
     __shared__ __attribute__((aligned(16))) char ldsB[STAGE];
-    __shared__ __attribute__((aligned(16))) char ldsV[VHL && !VDB ? 2 * VIMG : 16];
+    __shared__ __attribute__((aligned(16))) char ldsC[STAGE];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int T = p.T, D = p.D;
     const int nq = (T + 127) / 128, total = (int) gridDim.x;
     const int L = (int) blockIdx.x;
-    // XCD-contiguous work order: workgroup L is dispatched to XCD L % 8, so work item w = (L % 8)·(total/8) + L/8
-    // puts the q-tiles of one (clip, head) on ONE XCD at about the same time and its K/V are fetched into that
-    // L2 once instead of into up to eight of them (bijective when total % 8 == 0, identity otherwise)
-    const int w = (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);
+    const int w = (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);   // XCD-contiguous work order: the q-tiles of one (clip, head) on one XCD
     const int qt = w % nq, h = (w / nq) % p.H, clip = w / (nq * p.H);
     const int q0 = qt * 128 + wave * 32;
     const int64_t rowbase = (int64_t) clip * T;
-    const int hi = lane >> 5, col = lane & 31;
+    const int c16 = lane & 15, g = lane >> 4;
 
-    // Q fragments (B operand of S^T = K.Q^T): lane holds Q[q0+col][16s + 8hi .. +7]
-    half8 qh[4], ql[4];
-    {
-        const int q = min(q0 + col, T - 1);
-        const q2a_half * sh = p.qh + (rowbase + q) * D + h * 64 + 8 * hi;
-        const q2a_half * sl = p.ql + (rowbase + q) * D + h * 64 + 8 * hi;
+    // Q fragments (B operand): query 16qb + c16, d = 32ds + 8g .. +7
+    half8 qh[2][2], ql[2][2];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            qh[s] = *(const half8 *) (sh + 16 * s);
-            ql[s] = *(const half8 *) (sl + 16 * s);
+    for (int qb = 0; qb < 2; ++qb) {
+        const int q = min(q0 + 16 * qb + c16, T - 1);
+        const q2a_half * sh = p.qh + (rowbase + q) * D + h * 64 + 8 * g;
+        const q2a_half * sl = p.ql + (rowbase + q) * D + h * 64 + 8 * g;
+#pragma unroll
+        for (int ds = 0; ds < 2; ++ds) {
+            qh[qb][ds] = *(const half8 *) (sh + 32 * ds);
+            ql[qb][ds] = *(const half8 *) (sl + 32 * ds);
         }
     }
-    // tile t -> stage: wave w's instruction i covers rows (2w + i) * 8 .. +7 of each image (1 KiB), lane l row
-    // + l / 8, LDS granule l % 8 <- source granule (l % 8) ^ ((row >> 1) & 7)
-    // sources as a uniform (clip, head) base + a 32-bit per-lane byte offset (the saddr form of the DMA: no 64-bit
-    // address arithmetic per tile; a clip's K rows span T·D·2 B, its head's V^T 64·TP·2 B)
     const int64_t vt_off = ((int64_t) clip * p.H + h) * 64 * p.TP;
     const char * khb = (const char *) (p.kh + rowbase * D + h * 64);
     const char * klb = (const char *) (p.kl + rowbase * D + h * 64);
     const char * vtb = (const char *) (p.vt + vt_off);
-    const char * vlb = VHL ? (const char *) (p.vtl + vt_off) : nullptr;
-    // st: the K hi | K lo stage of tile t; vst: where its V^T (hi [| lo]) goes (st + 2 KIMG, or the V stage)
-    auto dma_tile = [&](char * st, char * vst, int t, bool with_k, bool with_v) {
+    const char * vlb = (const char *) (p.vtl + vt_off);
+    const int krow_d = 8 * wave + (lane >> 3), kg = (lane & 7) ^ ((krow_d >> 1) & 7);
+    const int vrow_d = 16 * wave + (lane >> 2), vg = (lane & 3) ^ ((vrow_d >> 2) & 3);
+    auto dma_tile = [&](char * st, int t) {   // (k_attn_s's DMA)
+        const int key = min(t * KS + krow_d, T - 1);
+        const uint32_t ko = (uint32_t) (key * D + kg * 8) * 2u;
+        const uint32_t vo = (uint32_t) (vrow_d * p.TP + t * KS + vg * 8) * 2u;
+        __builtin_amdgcn_global_load_lds((const void *) (khb + ko), (lds_ptr_t) (st + wave * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void *) (klb + ko), (lds_ptr_t) (st + KIMG + wave * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void *) (vtb + vo), (lds_ptr_t) (st + 2 * KIMG + wave * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void *) (vlb + vo), (lds_ptr_t) (st + 2 * KIMG + VIMG + wave * 1024), 16, 0, 0);
+    };
+
+    f4v_t o[2][4];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int row = (2 * wave + i) * 8 + (lane >> 3), g = (lane & 7) ^ ((row >> 1) & 7);
-            const int key = min(t * KT + row, T - 1);
-            const uint32_t ko = (uint32_t) (key * D + g * 8) * 2u;
-            const uint32_t vo = (uint32_t) (row * p.TP + t * KT + g * 8) * 2u;
-            const int pc = (2 * wave + i) * 1024;
-            if (with_k) {
-                __builtin_amdgcn_global_load_lds((const void *) (khb + ko), (lds_ptr_t) (st + pc), 16, 0, 0);
-                __builtin_amdgcn_global_load_lds((const void *) (klb + ko), (lds_ptr_t) (st + pc + KIMG), 16, 0, 0);
-            }
-            if (with_v) {
-                __builtin_amdgcn_global_load_lds((const void *) (vtb + vo), (lds_ptr_t) (vst + pc), 16, 0, 0);
-                if (VHL) __builtin_amdgcn_global_load_lds((const void *) (vlb + vo), (lds_ptr_t) (vst + pc + VIMG), 16, 0, 0);
-            }
+    for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int db = 0; db < 4; ++db) o[qb][db] = f4v_t{0.f, 0.f, 0.f, 0.f};
+    float m_run[2] = {0.f, 0.f}, l_run[2] = {0.f, 0.f};
+    const int ntiles = (T + KS - 1) / KS;
+    // LDS byte offsets: K row of (kb, i = c16), chunk 4ds + g (swizzled); V^T row c16 (+16db), granule g (swizzled)
+    uint32_t kofs[2][2], vofs;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+        const int kr = 8 * (c16 >> 2) + 4 * kb + (c16 & 3);
+#pragma unroll
+        for (int ds = 0; ds < 2; ++ds) kofs[kb][ds] = (uint32_t) (kr * KROW + (((4 * ds + g) ^ ((kr >> 1) & 7)) << 4));
+    }
+    vofs = (uint32_t) (2 * KIMG + c16 * VROW + ((g ^ ((c16 >> 2) & 3)) << 4));   // (row + 16db: same swizzle)
+    auto launder_ofs = [&]() {
+        asm volatile("" : "+v"(kofs[0][0]), "+v"(kofs[0][1]), "+v"(kofs[1][0]), "+v"(kofs[1][1]), "+v"(vofs));
+    };
+    typedef f4v_t sc_t[2][2];   // [qb][kb]
+    auto splat = [&](sc_t & s) {
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) {
+            float nm = -m_run[qb];
+            asm volatile("" : "+v"(nm));
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) s[qb][kb] = f4v_t{nm, nm, nm, nm};
         }
     };
-
-    f16v o[2];
+    // P of the tile: [qb] = B fragment of keys 8g .. 8g+7 (hi and lo halves)
+    half8 ph[2], pl[2];
+    // S'^T - m' of the tile at stage st into s (initialised by the caller with the splat); with sm: the softmax of the
+    // previous tile's scores interleaved (2 scores per MFMA pair) -> ph, pl, ls
+    auto qk = [&](const char * st, sc_t & s, const sc_t * sm, float (&ls)[2]) {
+        launder_ofs();
 #pragma unroll
-    for (int dt = 0; dt < 2; ++dt)
+        for (int ds = 0; ds < 2; ++ds) {
+            half8 kh[2], kl[2];
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
-    // Online softmax in log2 units: Q arrives pre-multiplied by log2(e) (the QKV epilogue folds it into the 1/8
-    // scale), so S' = log2(e)·S and P = exp2(S' - m'). The reference point m' of the lane's query enters the QK^T
-    // MFMAs as their initial accumulator (negm = -m' in all 16 C registers of each chain's first MFMA), so the
-    // accumulators hold S' - m' and feed v_exp_f32 directly: no subtraction per score. m' is set on the first tile (its
-    // max) and moves (lazily) only when a tile's P would leave the range the fp16 P halves hold: a lane whose 32 P of
-    // the tile sum to more than PLIM (then every one of them is <= PLIM < 65504) re-bases to the tile's max, so the
-    // common path needs no per-score max either.
-    float m_run = 0.f, l_run = 0.f;
-    f16v negm;
+            for (int kb = 0; kb < 2; ++kb) {
+                kh[kb] = *(const half8 *) (st + kofs[kb][ds]);
+                kl[kb] = *(const half8 *) (st + KIMG + kofs[kb][ds]);
+            }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) negm[r] = 0.f;
-    const int ntiles = (T + KT - 1) / KT;
-
-    // P of the current tile, packed two per register (truncated to fp16); PHL: plus the truncated remainders
-    half2_t ph[2][8], pl[2][8];
-    // per-lane LDS byte offsets of the fragment reads, computed once: K (key row kperm(col), chunk 2st+hi, swizzled) per
-    // step st for the first 32-key half (the second is +32 rows = +4096, the lo image +KIMG, the stage a constant);
-    // V^T (row col, granule 4kb+2sp+hi, swizzled) per (kb, sp) for d-block 0 (d-block 1 is +32 rows = +4096). Kept
-    // opaque (asm) so the compiler folds the constants into the ds_read immediate instead of re-deriving the swizzle
-    uint32_t kofs[4], vofs[2][2];
-    {
-        const int kr = kperm(col);
-#pragma unroll
-        for (int st = 0; st < 4; ++st) kofs[st] = (uint32_t) (kr * KROW + LY::k(kr, 2 * st + hi));
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int sp = 0; sp < 2; ++sp) vofs[kb][sp] = (uint32_t) (col * VROW + LY::vg(col, 4 * kb + 2 * sp + hi));
-    }
-    auto launder_ofs = [&]() {
-        asm volatile("" : "+v"(kofs[0]), "+v"(kofs[1]), "+v"(kofs[2]), "+v"(kofs[3]), "+v"(vofs[0][0]), "+v"(vofs[0][1]),
-                          "+v"(vofs[1][0]), "+v"(vofs[1][1]));
-    };
-    // QK^T + online softmax of tile t (K hi | K lo image at kh_img) -> ph / pl, l_run, m_run, rescaled O
-    auto qk_softmax = [&](const char * kh_img, int t) {
-        const char * kl_img = kh_img + KIMG;
-        f16v sc[2];
-        // S'^T - m' for both 32-key halves of the tile (24 MFMAs, the two chains interleaved per 16-deep step, each
-        // starting from negm); the K fragments of step st+1 are read before the MFMAs of step st, so each MFMA group
-        // waits only for its own reads
-        auto qk = [&]() {
-            half8 fh[2], fl[2];
-            launder_ofs();
-            auto rdk = [&](int st, int kb, half8 & hh, half8 & ll) {
-                const uint32_t off = kofs[st] + kb * 32 * KROW;   // (krow >> 1) & 7 does not depend on kb
-                hh = *(const half8 *) (kh_img + off);
-                ll = *(const half8 *) (kl_img + off);
-            };
-            rdk(0, 0, fh[0], fl[0]);
-            rdk(0, 1, fh[1], fl[1]);
-#pragma unroll
-            for (int st = 0; st < 4; ++st) {
-                half8 nh[2], nl[2];
-                if (st < 3) { rdk(st + 1, 0, nh[0], nl[0]); rdk(st + 1, 1, nh[1], nl[1]); }
+            for (int qb = 0; qb < 2; ++qb) {
 #pragma unroll
                 for (int kb = 0; kb < 2; ++kb) {
-                    sc[kb] = mma32<false>(fh[kb], qh[st], st == 0 ? negm : sc[kb]);
-                    if (Q2A_ATTN_QK_TERMS != 21) sc[kb] = mma32<false>(fl[kb], qh[st], sc[kb]);
-                    if (Q2A_ATTN_QK_TERMS != 22) sc[kb] = mma32<false>(fh[kb], ql[st], sc[kb]);
+                    s[qb][kb] = mma16(kh[kb], qh[qb][ds], s[qb][kb]);
+                    s[qb][kb] = mma16(kl[kb], qh[qb][ds], s[qb][kb]);
+                    s[qb][kb] = mma16(kh[kb], ql[qb][ds], s[qb][kb]);
                 }
-                if (st < 3) { fh[0] = nh[0]; fh[1] = nh[1]; fl[0] = nl[0]; fl[1] = nl[1]; }
             }
-            if (t == ntiles - 1) {   // keys >= T exist only in the last tile (key of reg r: 16(r>>3) + 8hi + (r&7))
+        }
+        if (sm) {
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb) {
+                float e[8];
 #pragma unroll
                 for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-                    for (int r = 0; r < 16; ++r)
-                        if (t * KT + kb * 32 + 16 * (r >> 3) + 8 * hi + (r & 7) >= T) sc[kb][r] = -1e30f;
-            }
-        };
-        // re-base to the tile's max (per query: both lane halves): on the first tile m' := that max (O and l are 0);
-        // later only for queries whose max exceeds m' (alpha = 1 for the others)
-        auto rebase = [&](bool first) {
-            float mx = fmaxf(sc[0][0], sc[1][0]);
+                    for (int r = 0; r < 4; ++r) e[4 * kb + r] = __builtin_amdgcn_exp2f((*sm)[qb][kb][r]);
+                float a = e[0];
 #pragma unroll
-            for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(sc[0][r], sc[1][r]));   // (v_max3_f32; -fno-honor-nans)
-            mx = max_lane32(mx);
-            const float sh = first ? mx : fmaxf(mx, 0.f);
-            if (!first) {
-                const float alpha = __builtin_amdgcn_exp2f(-sh);
-                l_run *= alpha;
+                for (int j = 1; j < 8; ++j) a += e[j];
+                ls[qb] = a;
+                half2_t hp[4], lp[4];
 #pragma unroll
-                for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) o[dt][r] *= alpha;
-            }
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) sc[kb][r] -= sh;
-            m_run += sh;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) negm[r] = -m_run;
-        };
-        // P = exp2(S' - m') in place of the scores, and the lane's f32 sum of them
-        float ls = 0.f;
-        auto exps = [&]() {
-            ls = 0.f;
-#pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    sc[kb][r] = __builtin_amdgcn_exp2f(sc[kb][r]);
-                    ls += sc[kb][r];
+                for (int j = 0; j < 4; ++j) {
+                    hp[j] = pk_rtz(e[2 * j], e[2 * j + 1]);
+                    lp[j] = rem_pair(e[2 * j], e[2 * j + 1], hp[j]);
                 }
-        };
-        qk();
-        if (t == 0) rebase(true);
-        exps();
-        if (t != 0 && __any(ls > PLIM)) {   // rare: some P of the tile may not fit fp16; the scores again (the K stage
-            qk();                           // is still in place), re-based, and their P
-            rebase(false);
-            exps();
-        }
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-            for (int r = 0; r < 16; r += 2) {
-                const float p0 = sc[kb][r], p1 = sc[kb][r + 1];
-                const half2_t hp = pk_rtz(p0, p1);
-                ph[kb][r >> 1] = hp;
-                if (PHL) {   // exact remainders p - fp16(p) (one v_fma_mix each: the fp16 operand read in place)
-                    pl[kb][r >> 1] = pk_rtz(sub_half<0>(p0, hp), sub_half<1>(p1, hp));
-                }
+                ph[qb] = half8{hp[0][0], hp[0][1], hp[1][0], hp[1][1], hp[2][0], hp[2][1], hp[3][0], hp[3][1]};
+                pl[qb] = half8{lp[0][0], lp[0][1], lp[1][0], lp[1][1], lp[2][0], lp[2][1], lp[3][0], lp[3][1]};
             }
-        if (!PHL) {   // the denominator of fp16 P: the sum of exactly those fp16 values
-            ls = 0.f;
+#if Q2A_ATTN_S_SCHED
+            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
-            for (int kb = 0; kb < 2; ++kb)
+            for (int i = 0; i < 12; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
-                for (int r = 0; r < 8; ++r) ls = __builtin_amdgcn_fdot2(ph[kb][r], half2_t{(_Float16) 1.0f, (_Float16) 1.0f}, ls, false);
+            for (int i = 0; i < 12; ++i) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+            }
+#endif
         }
-        l_run += ls;
     };
-    // O^T[d][q] += V^T[d][keys] . P^T[keys][q] for the tile whose V^T (hi [| lo]) image is at vt_img
-    auto pv = [&](const char * vt_img) {
-        launder_ofs();
-        auto frag8 = [](const half2_t (&v)[8], int sp) {
-            return half8{v[4 * sp][0], v[4 * sp][1], v[4 * sp + 1][0], v[4 * sp + 1][1],
-                         v[4 * sp + 2][0], v[4 * sp + 2][1], v[4 * sp + 3][0], v[4 * sp + 3][1]};
-        };
-        // O^T[d][q] += V^T[d][keys] . P^T[keys][q] (small terms first)
+    auto mask = [&](sc_t & s, int t) {   // keys >= T (last tile only): key of (kb, r) in lane group g is 8g + 4kb + r
+        if (t == ntiles - 1) {
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        if (t * KS + 8 * g + 4 * kb + r >= T) s[qb][kb][r] = -1e30f;
+        }
+    };
+    // re-base query block qb to the tile's max over its 32 keys (4 lane groups): first tile m' := that max
+    auto rebase = [&](sc_t & s, int qb, bool first) {
+        float mx = s[qb][0][0];
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
-            for (int dt = 0; dt < 2; ++dt) {
-                const int vr = dt * 32 + col;
+            for (int r = 0; r < 4; ++r) mx = fmaxf(mx, s[qb][kb][r]);
+        mx = max_lane32(max_lane16(mx));
+        const float sh = first ? mx : fmaxf(mx, 0.f);
+        if (!first) {
+            const float alpha = __builtin_amdgcn_exp2f(-sh);
+            l_run[qb] *= alpha;
 #pragma unroll
-                for (int sp = 0; sp < 2; ++sp) {   // keys 32kb + 16sp + 8hi .. +7: one 16-B granule of the V^T row
-                    const uint32_t vo = vofs[kb][sp] + dt * 32 * VROW;   // (vr >> 1) & 7 does not depend on dt
-                    const half8 va = *(const half8 *) (vt_img + vo);
-                    const half8 pb = frag8(ph[kb], sp);
-                    if (VHL) o[dt] = mma32<false>(*(const half8 *) (vt_img + VIMG + vo), pb, o[dt]);
-                    if (PHL) o[dt] = mma32<false>(va, frag8(pl[kb], sp), o[dt]);
-                    o[dt] = mma32<false>(va, pb, o[dt]);
-                }
+            for (int db = 0; db < 4; ++db) o[qb][db] *= alpha;
+        }
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) s[qb][kb] -= sh;
+        m_run[qb] += sh;
+        return sh;
+    };
+    // O^T[d][q] += V^T[d][keys] . P^T[keys][q] (small terms first); then the next QK^T's initial accumulators
+    auto pv = [&](const char * st, sc_t & init) {
+        launder_ofs();
+        half8 va[4], vl[4];
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+            va[db] = *(const half8 *) (st + vofs + db * 16 * VROW);
+            vl[db] = *(const half8 *) (st + VIMG + vofs + db * 16 * VROW);
+        }
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int db = 0; db < 4; ++db) {
+                o[qb][db] = mma16(vl[db], ph[qb], o[qb][db]);
+                o[qb][db] = mma16(va[db], pl[qb], o[qb][db]);
+                o[qb][db] = mma16(va[db], ph[qb], o[qb][db]);
             }
+        splat(init);
+        asm volatile("" : "+v"(init[0][0]), "+v"(init[0][1]), "+v"(init[1][0]), "+v"(init[1][1]));
+#if Q2A_ATTN_S_SCHED
+        __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+            __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+#endif
     };
 
-    dma_tile(ldsA, ldsA + 2 * KIMG, 0, true, !VHL || VDB);
-    // the Q fragments must be complete before the loop (an asm "use" makes the waitcnt pass wait for them here):
-    // otherwise their loads stay pending at the loop header, merge with the next-tile prefetch and every
-    // iteration's QK^T MFMAs wait on that prefetch
-    asm volatile("" :: "v"(qh[0]), "v"(qh[1]), "v"(qh[2]), "v"(qh[3]), "v"(ql[0]), "v"(ql[1]), "v"(ql[2]), "v"(ql[3]));
-    __syncthreads();   // (waits for the DMA: a pending LDS-DMA is a vmcnt event)
-    if constexpr (VHL && !VDB) {
-        // iteration t: V(t) -> V stage and K(t+1) -> the other K stage; QK^T(t) + softmax; barrier (V(t) landed);
-        // P.V(t); barrier (every wave done with the V stage and K(t)'s stage)
-        for (int t = 0; t < ntiles; t += 2) {
-            dma_tile(ldsB, ldsV, t + 1, t + 1 < ntiles, false);
-            dma_tile(ldsA, ldsV, t, false, true);
-            qk_softmax(ldsA, t);
-            __syncthreads();
-            pv(ldsV);
-            __syncthreads();
-            if (t + 1 >= ntiles) break;
-            dma_tile(ldsA, ldsV, t + 2, t + 2 < ntiles, false);
-            dma_tile(ldsB, ldsV, t + 1, false, true);
-            qk_softmax(ldsB, t + 1);
-            __syncthreads();
-            pv(ldsV);
-            __syncthreads();
+    sc_t sc, sn, init;
+    auto iter = [&](const char * sK, const char * sV, char * sD, int t) {
+        if (t + 2 < ntiles) dma_tile(sD, t + 2);
+        mask(sc, t);
+        float ls[2];
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) sn[qb][kb] = init[qb][kb];
+        qk(sK, sn, &sc, ls);
+        if (t != 0 && __any(ls[0] > PLIM || ls[1] > PLIM)) {   // rare: re-base from tile t's scores (K(t) in place)
+            sc_t s2;
+            splat(s2);
+            float dummy[2];
+            qk(sV, s2, nullptr, dummy);
+            mask(s2, t);
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb) {
+                const float sh = rebase(s2, qb, false);
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb) sn[qb][kb] -= sh;
+            }
+            // P of tile t again (against the new reference point)
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb) {
+                float e[8];
+#pragma unroll
+                for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) e[4 * kb + r] = __builtin_amdgcn_exp2f(s2[qb][kb][r]);
+                float a = e[0];
+#pragma unroll
+                for (int j = 1; j < 8; ++j) a += e[j];
+                ls[qb] = a;
+                half2_t hp[4], lp[4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    hp[j] = pk_rtz(e[2 * j], e[2 * j + 1]);
+                    lp[j] = rem_pair(e[2 * j], e[2 * j + 1], hp[j]);
+                }
+                ph[qb] = half8{hp[0][0], hp[0][1], hp[1][0], hp[1][1], hp[2][0], hp[2][1], hp[3][0], hp[3][1]};
+                pl[qb] = half8{lp[0][0], lp[0][1], lp[1][0], lp[1][1], lp[2][0], lp[2][1], lp[3][0], lp[3][1]};
+            }
         }
-    } else {
-        for (int t = 0; t < ntiles; t += 2) {
-            if (t + 1 < ntiles) dma_tile(ldsB, ldsB + 2 * KIMG, t + 1, true, true);
-            qk_softmax(ldsA, t);
-            pv(ldsA + 2 * KIMG);
-            __syncthreads();   // tile t + 1 landed (vmcnt(0) in the barrier), every wave done with A
-            if (t + 1 >= ntiles) break;
-            if (t + 2 < ntiles) dma_tile(ldsA, ldsA + 2 * KIMG, t + 2, true, true);
-            qk_softmax(ldsB, t + 1);
-            pv(ldsB + 2 * KIMG);
-            __syncthreads();
-        }
+        l_run[0] += ls[0];
+        l_run[1] += ls[1];
+        pv(sV, init);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+            for (int kb = 0; kb < 2; ++kb) sc[qb][kb] = sn[qb][kb];
+        __syncthreads();   // tile t+2 landed; every wave done with tile t's stage
+    };
+
+    dma_tile(ldsA, 0);
+    if (ntiles > 1) dma_tile(ldsB, 1);
+    asm volatile("" :: "v"(qh[0][0]), "v"(qh[0][1]), "v"(qh[1][0]), "v"(qh[1][1]), "v"(ql[0][0]), "v"(ql[0][1]),
+                 "v"(ql[1][0]), "v"(ql[1][1]));
+    __syncthreads();
+    {
+        float dummy[2];
+        splat(sc);
+        qk(ldsA, sc, nullptr, dummy);   // tile 0 against m' = 0, then m' := its max
+        mask(sc, 0);
+        rebase(sc, 0, true);
+        rebase(sc, 1, true);
+        splat(init);
+    }
+    for (int t = 0; t < ntiles; t += 3) {
+        iter(ldsB, ldsA, ldsC, t);
+        if (t + 1 >= ntiles) break;
+        iter(ldsC, ldsB, ldsA, t + 1);
+        if (t + 2 >= ntiles) break;
+        iter(ldsA, ldsC, ldsB, t + 2);
     }
 
-    const float l_tot = l_run + __shfl_xor(l_run, 32);
-    const float inv = 1.0f / l_tot;
-    const int q = q0 + col;
-    if (q < T) {
-        const int64_t orow = (rowbase + q) * D + h * 64;
 #pragma unroll
-        for (int dt = 0; dt < 2; ++dt)
+    for (int qb = 0; qb < 2; ++qb) {
+        const float l_tot = sum_lane32(sum_lane16(l_run[qb]));
+        const float inv = 1.0f / l_tot;
+        const int q = q0 + 16 * qb + c16;
+        if (q < T) {
+            const int64_t orow = (rowbase + q) * D + h * 64;
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int d = dt * 32 + 8 * g + 4 * hi;
-                const float v0 = o[dt][4 * g + 0] * inv, v1 = o[dt][4 * g + 1] * inv;
-                const float v2 = o[dt][4 * g + 2] * inv, v3 = o[dt][4 * g + 3] * inv;
+            for (int db = 0; db < 4; ++db) {
+                const int d = 16 * db + 4 * g;
+                const f4v_t v = o[qb][db] * inv;
                 if (p.outH) {
-                    const half4 hv = {(_Float16) v0, (_Float16) v1, (_Float16) v2, (_Float16) v3};
+                    const half4 hv = {(_Float16) v[0], (_Float16) v[1], (_Float16) v[2], (_Float16) v[3]};
                     *(half4 *) (p.outH + orow + d) = hv;
                 } else {
-                    *(float4 *) (p.outF + orow + d) = make_float4(v0, v1, v2, v3);
+                    *(float4 *) (p.outF + orow + d) = make_float4(v[0], v[1], v[2], v[3]);
                 }
             }
+        }
     }
 }
-
 
 // ---- ping-pong variant (default): one 512-thread workgroup = 8 waves x 32 queries (256 queries of one (clip, head)),
 // the two waves that share a SIMD (w and w + 4) run the same loop one segment apart: while group A (waves 0-3) is in
@@ -661,8 +700,8 @@ hipError_t Q2A_ATTN_LAUNCH(const q2a_attn_args & a, hipStream_t s) {
         if (!a.outH) return hipErrorInvalidValue;
         hipLaunchKernelGGL(k_attn_pp<true>, dim3(((a.T + 255) / 256) * a.H * a.n_clips), dim3(512), 0, s, a);
     } else {
-        if (Q2A_ATTN_VHL && !a.vtl) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_attn_g, dim3(((a.T + 127) / 128) * a.H * a.n_clips), dim3(256), 0, s, a);
+        if (!a.vtl) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_attn_t, dim3(((a.T + 127) / 128) * a.H * a.n_clips), dim3(256), 0, s, a);
     }
     return hipGetLastError();
 }

@@ -56,15 +56,77 @@ def golden_f32():
 @pytest.fixture(scope="session")
 def crossbuild():
     """The reference's OWN disagreement with itself (tests/golden/crossbuild.json, tests/golden/make_crossbuild.py):
-    the same model bytes and clips through six builds of /root/reference's sources — scalar x86-64, SSE4.2, AVX2 (the
-    golden build), AVX2 with GCC's default -ffp-contract=fast, AVX-512, and the shipped -O0 configuration (bit-identical
-    to AVX-512) — every pair of builds compared with the statistics the tests compute."""
+    the same model bytes and clips through eight builds of /root/reference's sources — GCC at scalar x86-64, SSE4.2,
+    AVX2 (the golden build) and AVX-512, AVX2 with GCC's default -ffp-contract=fast, the shipped -O0 configuration
+    (bit-identical to AVX-512), LLVM clang at AVX2 and AVX-512 — every pair of builds compared with the statistics the
+    tests compute."""
     with open(os.path.join(GOLDEN_DIR, "crossbuild.json")) as f:
         return json.load(f)
 
 
 def _widest(pairs, key):
     return max(p[key] for p in pairs)
+
+
+@pytest.fixture(scope="session")
+def xclips():
+    """The golden (AVX2) build's outputs for the further clips of the cross-build fixture (tests/golden/xclips.npz):
+    full size "full_<wt>_c<c>_val" on the golden's sampled indices, tiny "tiny_<wt>_c<c>_rows" on rows_stride5."""
+    return dict(np.load(os.path.join(GOLDEN_DIR, "xclips.npz"), allow_pickle=False))
+
+
+def _avg_bar(entries, keys):
+    """Widest pair of reference builds by the statistic AVERAGED over the fixture's clips: entries = one cross-build
+    entry per clip; only pairs present for every clip count. One clip's widest pair is an extreme-value draw that any
+    member of the population of builds exceeds on some clip; the clip average separates a larger error from it."""
+    common = set(entries[0]["pairs"])
+    for e in entries[1:]:
+        common &= set(e["pairs"])
+    return {out: max(float(np.mean([e["pairs"][pn][k] for e in entries])) for pn in common) for out, k in keys.items()}
+
+
+def _clip_ids(crossbuild, prefix):
+    return [0] + sorted(int(k[len(prefix):]) for k in crossbuild if k.startswith(prefix))
+
+
+@pytest.fixture(scope="session")
+def xbuild_avg_bar(crossbuild):
+    """Full-size bars averaged over clips (x1.0): bar(wt) -> {"clips", "max_rel", "rel_l2"}, the widest
+    pair of builds by its clip-averaged statistic on the golden's 8 192 sampled indices. The engine's statistic is
+    averaged over the same clips."""
+    def bar(wt):
+        clips = _clip_ids(crossbuild, f"{wt}_clip")
+        entries = [crossbuild[wt]] + [crossbuild[f"{wt}_clip{c}"] for c in clips[1:]]
+        b = _avg_bar(entries, {"max_rel": "sampled_max_rel", "rel_l2": "sampled_rel_l2"})
+        b["clips"] = clips
+        return b
+
+    return bar
+
+
+@pytest.fixture(scope="session")
+def tiny_avg_bar(crossbuild):
+    """Tiny-model bars averaged over clips (x1.0): the statistics on the golden's sampled rows (rows_stride5)."""
+    def bar(wt):
+        clips = _clip_ids(crossbuild, f"tiny_{wt}_clip")
+        entries = [crossbuild[f"tiny_{wt}"]] + [crossbuild[f"tiny_{wt}_clip{c}"] for c in clips[1:]]
+        b = _avg_bar(entries, {"max_rel": "rows_max_rel", "rel_l2": "rows_rel_l2"})
+        b["clips"] = clips
+        return b
+
+    return bar
+
+
+def tiny_ref_rows(g, xc, wt, c):
+    """The golden build's rows_stride5 output of the tiny <wt> model on clip c."""
+    if c == 0:
+        return g["tiny_f16_c0"][g["rows_stride5"]] if wt == "f16" else g[f"tiny_{wt}_c0_rows"]
+    return xc[f"tiny_{wt}_c{c}_rows"]
+
+
+def full_ref_samples(g, xc, wt, c):
+    """The golden build's full-size <wt> output of clip c on the golden's sampled indices."""
+    return g[f"full_{wt}_c0_val"] if c == 0 else xc[f"full_{wt}_c{c}_val"]
 
 
 @pytest.fixture(scope="session")

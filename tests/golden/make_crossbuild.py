@@ -19,6 +19,7 @@ pair statistics on the full output and on the rows the tiny golden samples (rows
 evidence for the tiny-model parity bars (tests/test_gpu_parity.py, tests/test_gpu_ggml_backend.py).
 
 usage: python tests/golden/make_crossbuild.py [--workdir DIR] [--types q4_k,q8_0,f16] [--builds x86-64,avx512] [--tiny]
+                                             [--clip-ids 101,102]
 """
 from __future__ import annotations
 
@@ -37,7 +38,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
 TOOL = os.path.join(ROOT, "qwen2-audio-whisper-ggml_amd", "bin", "q2a_tool")
 BUILDS = {"avx2": "_ref", "x86-64": "_ref_x86-64", "avx512": "_ref_avx512", "sse42": "_ref_v2", "avx2-fma": "_ref_fma",
-          "shipped-o0": "_ref_o0"}
+          "shipped-o0": "_ref_o0", "clang-avx2": "_ref_clang", "clang-avx512": "_ref_clang512"}
 T, D, F, L = 1500, 1280, 5120, 32
 POINTS = {"ln1": 3, "attn": 21, "ln2": 27, "gelu": 30}   # node offsets within a layer (oracle/ref_harness.cpp)
 
@@ -118,33 +119,49 @@ def node(dump, idx):
 
 
 def tiny(args, gmeta, gold, result, clip):
-    """Cross-build spread of the tiny model (no per-layer dumps): every pair of builds, full output + sampled rows."""
+    """Cross-build spread of the tiny model (no per-layer dumps): every pair of builds, full output + sampled rows.
+    Clip 0 under "tiny_<wt>"; with --clip-ids also further 30 s clips under "tiny_<wt>_clip<c>", whose golden-build
+    (AVX2) sampled rows go to xclips.npz ("tiny_<wt>_c<c>_rows"), so the GPU tests average over several clips."""
     base = os.path.join(args.workdir, "tiny-f16.bin")
     if not os.path.exists(base):
         subprocess.check_call([TOOL, "gen-model", base, "tiny", "f16", "0x51A2", str(args.threads)])
     rows = gold["rows_stride5"]
+    npz = os.path.join(HERE, "xclips.npz")
+    store = dict(np.load(npz, allow_pickle=False)) if os.path.exists(npz) else {}
+    clips = [(0, clip)]
+    for c in [int(v) for v in args.clip_ids.split(",") if v]:
+        cp = os.path.join(args.workdir, f"clip{c}.f32")
+        if not os.path.exists(cp):
+            subprocess.check_call([TOOL, "synth-clip", cp, "480000", str(c)])
+        clips.append((c, cp))
     for wt in args.types.split(","):
         model = base if wt == "f16" else os.path.join(args.workdir, f"tiny-{wt}.bin")
         if not os.path.exists(model):
             subprocess.check_call([TOOL, "quantize", base, model, wt, str(args.threads)])
         assert sha(model) == gmeta["models"][f"tiny-{wt}"]["sha256"], wt
-        finals = {}
-        for b in ["avx2"] + args.builds.split(","):
-            exe = os.path.join(ROOT, "oracle", BUILDS[b], "ref_harness")
-            out = os.path.join(args.workdir, f"tiny-{wt}-{b}.out")
-            subprocess.run([exe, "encode", model, clip, out, str(args.threads), "1"], check=True, capture_output=True)
-            finals[b] = np.fromfile(out, dtype=np.float32).reshape(750, -1)
-        names = list(finals)
-        ent = {"pairs": {}}
-        for i, a in enumerate(names):
-            for c in names[i + 1:]:
-                mx, l2 = relerr(finals[c], finals[a])
-                rmx, rl2 = relerr(finals[c][rows], finals[a][rows])
-                ent["pairs"][f"{a}_vs_{c}"] = {"max_rel": mx, "rel_l2": l2, "rows_max_rel": rmx, "rows_rel_l2": rl2}
-        ref_rows = gold["tiny_f16_c0"][rows] if wt == "f16" else gold[f"tiny_{wt}_c0_rows"]
-        ent["avx2_matches_golden_rows"] = bool(np.array_equal(finals["avx2"][rows], ref_rows))
-        result[f"tiny_{wt}"] = ent
-        print("tiny", wt, json.dumps(ent), flush=True)
+        for c, cpath in clips:
+            finals = {}
+            for b in ["avx2"] + args.builds.split(","):
+                exe = os.path.join(ROOT, "oracle", BUILDS[b], "ref_harness")
+                out = os.path.join(args.workdir, f"tiny-{wt}-{b}-c{c}.out")
+                subprocess.run([exe, "encode", model, cpath, out, str(args.threads), "1"], check=True, capture_output=True)
+                finals[b] = np.fromfile(out, dtype=np.float32).reshape(750, -1)
+            names = list(finals)
+            ent = {"pairs": {}}
+            for i, a in enumerate(names):
+                for d in names[i + 1:]:
+                    mx, l2 = relerr(finals[d], finals[a])
+                    rmx, rl2 = relerr(finals[d][rows], finals[a][rows])
+                    ent["pairs"][f"{a}_vs_{d}"] = {"max_rel": mx, "rel_l2": l2, "rows_max_rel": rmx, "rows_rel_l2": rl2}
+            if c == 0:
+                ref_rows = gold["tiny_f16_c0"][rows] if wt == "f16" else gold[f"tiny_{wt}_c0_rows"]
+                ent["avx2_matches_golden_rows"] = bool(np.array_equal(finals["avx2"][rows], ref_rows))
+                result[f"tiny_{wt}"] = ent
+            else:
+                result[f"tiny_{wt}_clip{c}"] = ent
+                store[f"tiny_{wt}_c{c}_rows"] = finals["avx2"][rows]
+                np.savez_compressed(npz, **store)
+            print("tiny", wt, c, json.dumps(ent), flush=True)
 
 
 def frontend(args, gmeta, result, clip):
@@ -232,7 +249,7 @@ def main():
         subprocess.check_call([TOOL, "synth-clip", clip, "480000", "0"])
     assert sha(clip) == gmeta["clips"]["0"]["sha256"]
     gold = dict(np.load(os.path.join(HERE, "golden.npz"), allow_pickle=False))
-    if args.clip_ids:
+    if args.clip_ids and not args.tiny:
         more_clips(args, gmeta, gold, result)
         print("wrote", outp)
         return
@@ -261,11 +278,13 @@ def main():
         if not os.path.exists(model):
             subprocess.check_call([TOOL, "quantize", base, model, wt, str(args.threads)])
         assert sha(model) == gmeta["models"][f"full-{wt}"]["sha256"], wt
-        dref = os.path.join(args.workdir, f"dump-{wt}-avx2")
+        traced_any = any(b in args.layers_for.split(",") for b in args.builds.split(","))
+        dref = os.path.join(args.workdir, f"dump-{wt}-avx2") if traced_any else None
         yref, iref = run_ref("avx2", model, clip, os.path.join(args.workdir, f"{wt}-avx2.out"), dref, args.threads)
         g = gmeta["outputs"][f"full_{wt}_c0"]
         ent = {"avx2_matches_golden_l2": abs(float(np.linalg.norm(yref.astype(np.float64))) - g["l2"]) < 1e-3 * g["l2"],
-               "seconds": {"avx2": iref["wall_s"]}, "pairs": {}, "layers": {}}
+               "seconds": {"avx2": iref["wall_s"]}, "pairs": {},
+               "layers": dict(result.get(wt, {}).get("layers", {}))}   # earlier traces kept
         finals = {"avx2": yref}
         for b in args.builds.split(","):
             traced = b in args.layers_for.split(",")
@@ -292,7 +311,8 @@ def main():
                 print(wt, b, r, flush=True)
             ent["layers"][b] = rows
             shutil.rmtree(dother)
-        shutil.rmtree(dref)
+        if dref:
+            shutil.rmtree(dref)
         names = list(finals)
         for i, a in enumerate(names):
             for c in names[i + 1:]:
