@@ -1,0 +1,9 @@
+#!/bin/bash
+# round 3: full GPU suite without -x (every failure listed), smoke, default bench line
+cd /root/repo
+mkdir -p gpurun_out
+export Q2A_BENCH_DIR=/tmp/q2ab Q2A_PARITY_LOG=$PWD/gpurun_out/u_parity_log.jsonl
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > gpurun_out/u_tests.log 2>&1; echo "tests rc=$?"; tail -12 gpurun_out/u_tests.log
+timeout -k 10 120 python3 -c "import __graft_entry__ as g; g.smoke()" || exit 1
+timeout -k 10 600 python3 bench.py > gpurun_out/u_bench.json 2> gpurun_out/u_bench.err || { tail -20 gpurun_out/u_bench.err; exit 1; }
+tail -c 1500 gpurun_out/u_bench.json

@@ -47,6 +47,9 @@ void set_err(const char * fmt, ...) {
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t BLOB_MAGIC = 0x42413251u;   // "Q2AB"
 // version 3: the Q4_K gamma array holds -(dmin/dx) (stored negated); a version-2 blob (positive gamma) is refused
+#ifndef Q2A_FC1_PATH
+#define Q2A_FC1_PATH 0   // the engine's default fc1 -> fc2 operand path (below; diagnostic builds select another)
+#endif
 constexpr uint32_t BLOB_VERSION = 4;   // 4: conv1 taps against the three-part mel operand
 constexpr int MAX_LAYERS = 64;
 constexpr size_t HEADER_BYTES = 32768;
@@ -555,8 +558,8 @@ struct q2a_engine {
     // Q4_K fc1 -> fc2 operand path (q2a_test_fc1_path; the three produce identical Q8_K codes):
     //   0 (default) fc1 writes its fp16 pre-activation, the Q8_K quantizer applies the GELU table on the way
     //   1 GELU in the fc1 epilogue, then the fp16-input quantizer
-    //   2 GELU + Q8_K quantization fused into the fc1 epilogue (8-phase tiles only; no faster at present)
-    int fc1_path = 0;
+    //   2 GELU + Q8_K quantization fused into the fc1 epilogue (8-phase tiles only)
+    int fc1_path = Q2A_FC1_PATH;
     // q2a_test_block_taps: device buffers receiving the GEMM A operands of one block (LN1 -> QKV, attention -> O,
     // LN2 -> fc1, GELU -> fc2) as they were fed to the MFMA, for the per-layer divergence trace (NULL: off)
     void * taps[4] = {nullptr, nullptr, nullptr, nullptr};

@@ -829,6 +829,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
         static_assert(BN == 256 && WN == 4 && WM == 2 && BM == 256, "Q8_K epilogue layout");
         static_assert(Q2A_GELU_C_BYTES + 128 * RSH * 2 <= LDS_BYTES, "Q8_K staging exceeds LDS");
         _Float16 * tl = (_Float16 *) (lds_raw + Q2A_GELU_C_BYTES);
+        float * sd = (float *) (lds_raw + Q2A_GELU_C_BYTES + 128 * RSH * 2);   // d of the pass's 128 rows
+        _Float16 * sa = (_Float16 *) (sd + 128);                                // their bsum operands [128][16]
+        static_assert(Q2A_GELU_C_BYTES + 128 * RSH * 2 + 128 * 4 + 128 * 32 <= LDS_BYTES, "Q8_K side staging exceeds LDS");
         const uint16_t * lut = (const uint16_t *) lds_raw;
         const int kb = n0 / 256;
         f4 bias4[NJ];   // C^T tiles: columns 16j + 4(lane>>4) + r of row 16i + (lane&15)
@@ -871,9 +874,31 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                 float v[16];
 #pragma unroll
                 for (int e = 0; e < 8; ++e) { v[e] = (float) h0[e]; v[8 + e] = (float) h1[e]; }
-                if (m < p.M)
-                    quant_q8k_row16(v, sub, p.outH + (int64_t) m * p.ldo + n0 + sub * 16, p.qdy + (int64_t) kb * p.dy_ld + m,
-                                    p.qaext + ((int64_t) kb * p.dy_ld + m) * 16);
+                float d;
+                int sm;
+                quant_q8k_row16c(v, sub, p.outH + (int64_t) min(m, p.M - 1) * p.ldo + n0 + sub * 16, m < p.M, d, sm);
+                if (sub == 0) sd[rl] = d;
+                if ((sub & 1) == 0) {   // the bsum operand pair (64·hi + lo = bsum32, both exact in fp16)
+                    const int hi = (sm >= 0) ? (sm >> 6) : -((-sm + 63) >> 6);
+                    typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
+                    *(h2_t *) (sa + rl * 16 + sub) = h2_t{(_Float16) (float) hi, (_Float16) (float) (sm - 64 * hi)};
+                }
+            }
+            __syncthreads();
+            // the pass's side outputs are contiguous in their block-major arrays (rows m0 + 128ps ..): d 512 B, bsum
+            // operands 4 KiB — whole 16-B pieces per lane instead of one 4-B write per row (partial sectors)
+            const int mb = m0 + ps * 128;
+            if (tid < 32) {
+                const int r0 = 4 * tid;
+                float * dst = p.qdy + (int64_t) kb * p.dy_ld + mb + r0;
+                if (mb + r0 + 3 < p.M) *(float4 *) dst = *(const float4 *) (sd + r0);
+                else for (int r = 0; r < 4; ++r) if (mb + r0 + r < p.M) dst[r] = sd[r0 + r];
+            }
+            if (tid < 256) {
+                const int r = tid >> 1;
+                if (mb + r < p.M)
+                    *(uint4 *) (p.qaext + ((int64_t) kb * p.dy_ld + mb + r) * 16 + (tid & 1) * 8) =
+                        *(const uint4 *) (sa + r * 16 + (tid & 1) * 8);
             }
             __syncthreads();
         }
