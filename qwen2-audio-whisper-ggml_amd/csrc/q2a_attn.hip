@@ -243,7 +243,11 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb) {
                 kh[kb] = *(const half8 *) (st + kofs[kb][ds]);
+#ifdef Q2A_ATTN_DIAG_NOKL   // timing diagnostic only (wrong results): the K lo fragment reads skipped
+                kl[kb] = kh[kb];
+#else
                 kl[kb] = *(const half8 *) (st + KIMG + kofs[kb][ds]);
+#endif
             }
 #pragma unroll
             for (int qb = 0; qb < 2; ++qb) {
@@ -262,7 +266,11 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
 #pragma unroll
                 for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
+#ifdef Q2A_ATTN_DIAG_NOEXP   // timing diagnostic only (wrong results): the exponentials skipped
+                    for (int r = 0; r < 4; ++r) e[4 * kb + r] = fmaxf(fmaf((*sm)[qb][kb][r], 0.001f, 1.0f), 0.f);
+#else
                     for (int r = 0; r < 4; ++r) e[4 * kb + r] = __builtin_amdgcn_exp2f((*sm)[qb][kb][r]);
+#endif
                 float a = e[0];
 #pragma unroll
                 for (int j = 1; j < 8; ++j) a += e[j];
@@ -330,7 +338,11 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
 #pragma unroll
         for (int db = 0; db < 4; ++db) {
             va[db] = *(const half8 *) (st + vofs + db * 16 * VROW);
+#ifdef Q2A_ATTN_DIAG_NOVL   // timing diagnostic only (wrong results): the V^T lo fragment reads skipped
+            vl[db] = va[db];
+#else
             vl[db] = *(const half8 *) (st + VIMG + vofs + db * 16 * VROW);
+#endif
         }
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb)
