@@ -555,7 +555,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     const int ngrp = (GROUPABLE && p.ngroup == 2) ? 2 : 1;
     const int ksplit = (!PIPE && (BLK == 0 || BLK == 32) && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) &&
                         p.ksplit > 1 && ngrp == 1) ? p.ksplit : 1;
-    const int nbn = p.N / BN, nbm = (p.M + BM - 1) / BM, ntl = nbn * nbm, nwg = ntl * ksplit * ngrp;
+    const int nbn = p.N / BN, nbm = (p.M - p.m_base + BM - 1) / BM, ntl = nbn * nbm, nwg = ntl * ksplit * ngrp;
     const int bid = blockIdx.x, xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
     int wgid_all = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (bid >> 3);
     if constexpr (GROUPABLE) {
@@ -570,7 +570,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     const int gsize = GM * nbn, g = wgid / gsize, gr = wgid % gsize;
     const int gm = min(GM, nbm - g * GM);
     const int tm = g * GM + gr % gm, tn = gr / gm;
-    const int m0 = tm * BM, n0 = tn * BN;
+    const int m0 = p.m_base + tm * BM, n0 = tn * BN;
 
     f4 acc[MI][NJ];
 #pragma unroll
@@ -1372,7 +1372,7 @@ hipError_t launch_cfg(const q2a_gemm_args & a, hipStream_t s) {
     const bool grouped = !PIPE && (BLK == 0 || BLK == 256) && EPI == Q2A_EPI_STORE_F && a.ngroup == 2;
     const bool split = !PIPE && (BLK == 0 || BLK == Q2A_BLK_BF16 || BLK == 32) &&
                        (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) && a.ksplit > 1 && !grouped;
-    const int nwg = (a.N / BN) * ((a.M + BM - 1) / BM) * (split ? a.ksplit : 1) * (grouped ? 2 : 1);
+    const int nwg = (a.N / BN) * ((a.M - a.m_base + BM - 1) / BM) * (split ? a.ksplit : 1) * (grouped ? 2 : 1);
     hipLaunchKernelGGL((k_gemm<BM, BN, WM, WN, EPI, BLK, PIPE>), dim3(nwg), dim3(WM * WN * 64), 0, s, a);
     if (split) {
         const int64_t n4 = (int64_t) a.M * a.N / 4;
@@ -1428,6 +1428,57 @@ bool wide_tiles(int M, int N) {
 
 bool pipe8_enabled() { return Q2A_GEMM_PIPE != 0; }
 
+// Q2A_GEMM_TAIL (compile time): 1 = partial last round of an 8-phase grid on 128x128 tiles (product), 0 = off,
+// 2 = on the two-stage 128x256 (Q4_K) / 256x256 tiles (diagnostic)
+#ifndef Q2A_GEMM_TAIL
+#define Q2A_GEMM_TAIL 1
+#endif
+
+// compute units of the current device, cached per device ordinal
+int cu_count() {
+    static int cus[64] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    if (!cus[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+        cus[dev] = n;
+    }
+    return cus[dev];
+}
+
+// The 8-phase kernel holds a whole CU per 256x256 tile, so a grid whose last round is partly filled leaves the rest of
+// the chip idle for one whole tile time: the O / fc2 GEMMs at 64 clips are 375 x 5 = 1 875 tiles = 7.32 rounds on 256
+// CUs, fc1 7 500 = 29.3. When the last round would fill at most 5/8 of the CUs, the whole rounds run on the 8-phase
+// kernel (rows [0, m_main)) and the remaining rows on 128x128 tiles (two workgroups per CU, a quarter of the work per
+// tile), which sum K in the same order with the same block recurrence: outputs are bit-identical to the one-launch grid
+// (batch invariance). Only for epilogues whose row addressing is absolute (no per-tile row remap), and
+// only for deep K: measured at 64 clips Q4_K (diag/gpurun_r03ta.sh, same box, alternating) fc2 (K = 5120) 45.2 -> 44.4
+// ms/step, but O (K = 1280) 17.05 -> 17.3 and fc1 (K = 1280) 48.6 -> 48.75 — a shallow tile's partial round costs less
+// than the second launch and the 128x128 tiles' lower rate.
+template <int EPI, int BLK>
+hipError_t launch_pipe8(const q2a_gemm_args & a, hipStream_t s) {
+    constexpr bool TAILABLE = Q2A_GEMM_TAIL && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_PRE_H || EPI == Q2A_EPI_GELU_H);
+    if constexpr (TAILABLE) {
+        const int cus = cu_count();
+        const int nbn = a.N / 256, nbm = (a.M - a.m_base + 255) / 256;
+        const int64_t ntl = (int64_t) nbn * nbm, rem = cus > 0 ? ntl % cus : 0;
+        const int m_main = (int) ((ntl - rem) / nbn);   // whole M-tiles inside the full rounds
+        if (a.K >= 4096 && a.m_base == 0 && rem > 0 && rem * 8 <= (int64_t) cus * 5 && m_main > 0 && m_main < nbm) {
+            q2a_gemm_args h = a;
+            h.M = m_main * 256;
+            const hipError_t err = launch_cfg<256, 256, 2, 4, EPI, BLK, 1>(h, s);
+            if (err != hipSuccess) return err;
+            q2a_gemm_args t = a;
+            t.m_base = m_main * 256;
+            if constexpr (Q2A_GEMM_TAIL == 2)   // diagnostic: the two-stage wide tiles (one workgroup per CU)
+                return BLK == 256 ? launch_cfg<128, 256, 2, 4, EPI, BLK>(t, s) : launch_cfg<256, 256, 2, 4, EPI, BLK>(t, s);
+            return launch_cfg<128, 128, 2, 2, EPI, BLK>(t, s);
+        }
+    }
+    return launch_cfg<256, 256, 2, 4, EPI, BLK, 1>(a, s);
+}
+
 // the 8-phase kernels: 256x256 tiles, 32-bit operand offsets, K-steps in pairs (fp16) or whole Q4_K blocks
 bool pipe8_ok(const q2a_gemm_args & a, int blk) {
     if (!pipe8_enabled() || !wide_tiles(a.M, a.N)) return false;
@@ -1451,13 +1502,13 @@ hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
         // same block recurrence): a clip's outputs are bit-identical whichever tile regime its batch size selects
         const bool narrow = !big && narrow_tiles(a.M, a.N) && a.ksplit <= 1 && a.ngroup != 2;
         if (blk == 0) {
-            if (p8) return launch_cfg<256, 256, 2, 4, EPI, 0, 1>(a, s);
+            if (p8) return launch_pipe8<EPI, 0>(a, s);
             if (narrow) return launch_cfg<64, 128, 2, 2, EPI, 0>(a, s);
             return big ? launch_cfg<256, 256, 2, 4, EPI, 0>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 0>(a, s);
         }
         if (blk == 256) {
             if (!a.beta || !a.gamma) return hipErrorInvalidValue;   // the block recurrence needs beta / gamma
-            if (p8) return launch_cfg<256, 256, 2, 4, EPI, 256, 1>(a, s);
+            if (p8) return launch_pipe8<EPI, 256>(a, s);
             if (narrow) return launch_cfg<64, 128, 2, 2, EPI, 256>(a, s);
             return big ? launch_cfg<128, 256, 2, 4, EPI, 256>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 256>(a, s);
         }
@@ -1468,7 +1519,7 @@ hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
         if constexpr (EPI == Q2A_EPI_QKV || EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_STORE_F) {
             if (blk == Q2A_BLK_BF16) {
                 constexpr int B16 = Q2A_BLK_BF16;
-                if (p8) return launch_cfg<256, 256, 2, 4, EPI, B16, 1>(a, s);
+                if (p8) return launch_pipe8<EPI, B16>(a, s);
                 if (narrow) return launch_cfg<64, 128, 2, 2, EPI, B16>(a, s);
                 return big ? launch_cfg<256, 256, 2, 4, EPI, B16>(a, s) : launch_cfg<128, 128, 2, 2, EPI, B16>(a, s);
             }
@@ -1507,6 +1558,7 @@ int q2a_gemm_kq_ksplit(int M, int N, int K, int blk) {
 
 hipError_t q2a_launch_gemm(const q2a_gemm_args & a_in, int epi, int blk, hipStream_t s) {
     q2a_gemm_args a = a_in;
+    a.m_base = 0;
     a.stagger_ns = Q2A_GEMM_STAGGER_NS; a.stagger_g = std::max(1, Q2A_GEMM_STAGGER_G);
     a.group_m = Q2A_GEMM_GROUP_M;
     if (a.ngroup == 2 && (epi != Q2A_EPI_STORE_F || (blk != 0 && blk != 256) || wide_tiles(a.M, a.N))) return hipErrorInvalidValue;

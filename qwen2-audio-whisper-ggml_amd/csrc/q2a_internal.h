@@ -91,6 +91,7 @@ struct q2a_gemm_args {
     const q2a_half * wext2;
     int split_kq;                     // allow the small-tile split-K for k-quant / Q8_0 / Q4_0 weights (q2a_gemm_kq_ksplit)
     q2a_half * vtl;                   // Q2A_EPI_QKV: V^T lo image fp16(v - fp16(v)), same layout as vt (null = not written)
+    int m_base;                       // first output row of the launch (tiles cover rows [m_base, M)); set by the launcher
 };
 
 // the launcher's split factor for a small-tile Q2A_EPI_RESID GEMM (0 = none): a function of K only, so every batch
