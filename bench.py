@@ -241,7 +241,9 @@ def main():
     torch.cuda.set_device(local)
     coll_dev = "cpu" if rehearse else "cuda"
     dist = None
-    if ws > 1:
+    # Q2A_BENCH_PG=1: bring up the process group (RCCL) at world size 1 too, so a 1-GPU box executes the N>1 path's
+    # collectives (communicator init on the device, the blob broadcast, the max-over-ranks all-reduce, barriers)
+    if ws > 1 or os.environ.get("Q2A_BENCH_PG") == "1":
         import torch.distributed as dist
         if rehearse:
             dist.init_process_group("gloo")
@@ -444,7 +446,8 @@ def main():
         "host_api_frames_per_s": round(host_rate, 1) if host_rate else None,
         "per_kernel": per_kernel,
         "per_kernel_source": f"separate pass of {brk_steps} step(s), every kernel class bracketed by HIP events",
-        "setup_s": {"total": round(t_setup, 1), "weight_h2d_plus_rccl_broadcast": round(t_bcast, 4), "weight_blob_bytes": nbytes},
+        "setup_s": {"total": round(t_setup, 1), "weight_h2d_plus_rccl_broadcast": round(t_bcast, 4), "weight_blob_bytes": nbytes,
+                    "collective_backend": dist.get_backend() if dist is not None else None},
     }
     print(json.dumps(res), flush=True)
     eng.close()

@@ -55,3 +55,28 @@ def test_bench_two_ranks_rehearsal(tmp_path):
     assert res["config"]["global_batch"] == 4 and res["scaling"] == "weak"
     assert res["value"] > 0 and res["steps"] == 2
     assert res["setup_s"]["weight_h2d_plus_rccl_broadcast"] > 0
+
+
+@pytest.mark.gpu
+def test_bench_rccl_world_size_one(tmp_path):
+    """The driver's own launch form (`torch.distributed.run --nproc-per-node N ... bench.py --gpus N`) at N = 1 with the
+    process group forced up (Q2A_BENCH_PG=1): the RCCL communicator is created on the device and the N>1 path's
+    collectives run through it (size + blob broadcast on device memory, barriers, the max-over-ranks all-reduce).
+    A 1-GPU box cannot run 2 RCCL ranks (one device per rank), so this is the most of the RCCL path it can execute;
+    the engine must come up from the broadcast blob and report one JSON line labelled nccl / dp1."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), BENCH, "--gpus", "1", "--steps", "2",
+           "--warmup", "1", "--clips", "2", "--config", "f16x1", "--no-cpu-baseline", "--no-host-legs",
+           "--workdir", str(tmp_path)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=_env(Q2A_BENCH_PG="1"))
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    res = json.loads(lines[0])
+    assert res["setup_s"]["collective_backend"] == "nccl"
+    assert res["n_gpus"] == 1 and res["config"]["parallelism"] == "dp1" and res["value"] > 0
+    assert res["setup_s"]["weight_h2d_plus_rccl_broadcast"] > 0
