@@ -50,7 +50,9 @@ def main():
     fetch_csv, write_csv, out, source = sys.argv[1:5]
     fetch, write = load(fetch_csv, "FETCH_SIZE"), load(write_csv, "WRITE_SIZE")
     res = {}
-    for k in sorted(set(fetch) | set(write)):
+    # the kernel with the most dispatches of a class keeps the class name (e.g. the 8-phase O / fc2 kernel), smaller
+    # parts of the same launches (fc2's 128x128 partial-round tail) get primed keys
+    for k in sorted(set(fetch) | set(write), key=lambda n: (-max(len(fetch.get(n, [])), len(write.get(n, []))), n)):
         cls = classify(k)
         f = fetch.get(k, [])
         w = write.get(k, [])
