@@ -1429,7 +1429,8 @@ bool wide_tiles(int M, int N) {
 bool pipe8_enabled() { return Q2A_GEMM_PIPE != 0; }
 
 // Q2A_GEMM_TAIL (compile time): 1 = partial last round of an 8-phase grid on 128x128 tiles (product), 0 = off,
-// 2 = on the two-stage 128x256 (Q4_K) / 256x256 tiles (diagnostic)
+// 2 = on the two-stage 128x256 (Q4_K) / 256x256 tiles (diagnostic), 3 = on the 64x128 deep-pipeline tiles at every K
+// (diagnostic)
 #ifndef Q2A_GEMM_TAIL
 #define Q2A_GEMM_TAIL 1
 #endif
@@ -1464,13 +1465,15 @@ hipError_t launch_pipe8(const q2a_gemm_args & a, hipStream_t s) {
         const int nbn = a.N / 256, nbm = (a.M - a.m_base + 255) / 256;
         const int64_t ntl = (int64_t) nbn * nbm, rem = cus > 0 ? ntl % cus : 0;
         const int m_main = (int) ((ntl - rem) / nbn);   // whole M-tiles inside the full rounds
-        if (a.K >= 4096 && a.m_base == 0 && rem > 0 && rem * 8 <= (int64_t) cus * 5 && m_main > 0 && m_main < nbm) {
+        if ((Q2A_GEMM_TAIL == 3 || a.K >= 4096) && a.m_base == 0 && rem > 0 && rem * 8 <= (int64_t) cus * 5 && m_main > 0 && m_main < nbm) {
             q2a_gemm_args h = a;
             h.M = m_main * 256;
             const hipError_t err = launch_cfg<256, 256, 2, 4, EPI, BLK, 1>(h, s);
             if (err != hipSuccess) return err;
             q2a_gemm_args t = a;
             t.m_base = m_main * 256;
+            if constexpr (Q2A_GEMM_TAIL == 3)   // diagnostic: the deep-pipeline 64x128 tiles, every K
+                return launch_cfg<64, 128, 2, 2, EPI, BLK>(t, s);
             if constexpr (Q2A_GEMM_TAIL == 2)   // diagnostic: the two-stage wide tiles (one workgroup per CU)
                 return BLK == 256 ? launch_cfg<128, 256, 2, 4, EPI, BLK>(t, s) : launch_cfg<256, 256, 2, 4, EPI, BLK>(t, s);
             return launch_cfg<128, 128, 2, 2, EPI, BLK>(t, s);
