@@ -264,7 +264,9 @@ def main():
     blob_host = None
     if rank == 0:
         model_path = make_model(wt, args.workdir, threads)
-        blob_host = q2a.pack_model(model_path, q2a.ACT_BF16 if "bf16" in args.config else q2a.ACT_REFERENCE)
+        # the compact transport form (ggml weight rows: Q4_K at 144 B per 256 weights); each rank expands it into the
+        # device layout on its own GPU when it opens the engine
+        blob_host = q2a.pack_model(model_path, q2a.ACT_BF16 if "bf16" in args.config else q2a.ACT_REFERENCE, compact=True)
     t_bcast = 0.0
     if dist is not None:
         dist.barrier()
@@ -275,7 +277,10 @@ def main():
         t_bcast = time.time() - tb
     del blob_host
     nbytes = blob.numel()
-    eng = q2a.Engine(device=local, device_blob=blob.data_ptr(), blob_size=nbytes)
+    tx = time.time()
+    eng = q2a.Engine(device=local, device_blob=blob.data_ptr(), blob_size=nbytes)   # expands on the GPU (owns it)
+    t_expand = time.time() - tx
+    del blob
     eng.reserve(clips_per_gpu)
     t_setup = time.time() - t0
 
@@ -446,7 +451,8 @@ def main():
         "host_api_frames_per_s": round(host_rate, 1) if host_rate else None,
         "per_kernel": per_kernel,
         "per_kernel_source": f"separate pass of {brk_steps} step(s), every kernel class bracketed by HIP events",
-        "setup_s": {"total": round(t_setup, 1), "weight_h2d_plus_rccl_broadcast": round(t_bcast, 4), "weight_blob_bytes": nbytes,
+        "setup_s": {"total": round(t_setup, 1), "weight_h2d_plus_rccl_broadcast": round(t_bcast, 4), "weight_blob_bytes": nbytes, "weight_device_bytes": int(eng.info.weight_bytes),
+                    "weight_expand_on_gpu": round(t_expand, 4),
                     "collective_backend": dist.get_backend() if dist is not None else None},
     }
     print(json.dumps(res), flush=True)

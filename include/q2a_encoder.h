@@ -40,6 +40,7 @@ typedef enum {
 #define Q2A_CLIP_ENCODED 0
 #define Q2A_CLIP_SKIPPED 1   /* < 1 s of audio after the offset: the reference returns 0 without encoding
                                 (qwen2-whisper.cpp:2359-2365); the clip's output rows are left untouched */
+#define Q2A_CLIP_FAILED 2    /* the call returned an error before this clip's output reached the caller (host API) */
 
 typedef struct {
     int32_t n_audio_ctx, n_audio_state, n_audio_head, n_audio_layer, n_mels;
@@ -75,6 +76,17 @@ int64_t q2a_pack_model_ex(const char * model_path, int act, void ** host_blob);
 int64_t q2a_pack_model(const char * model_path, void ** host_blob);   /* returns size in bytes, < 0 on error */
 void q2a_free_host_blob(void * host_blob);
 q2a_engine * q2a_open_device_blob(const void * device_blob, int64_t size, int device);  /* blob not owned */
+/* The compact TRANSPORT form of the same blob (what rank 0 broadcasts): the small sections plus every
+ * linear weight as the model file's own ggml rows (Q4_K: raw block_q4_K, 144 B per 256 weights, ggml-common.h:282-297)
+ * instead of the device layout's expanded operands — 0.37 GB instead of 1.40 GB for the full-size Q4_K model.
+ * q2a_open_device_blob accepts it too and expands it on the GPU into an engine-owned device layout that is byte for
+ * byte what q2a_pack_model_ex writes on the host. */
+int64_t q2a_pack_model_compact(const char * model_path, int act, void ** host_blob);
+/* From a blob's first header_bytes (>= 32 KiB) on the host: the device-layout size (return) and the size of the
+ * blob as given (*transport_bytes: the compact size for a compact blob). */
+int64_t q2a_blob_device_size(const void * host_header, int64_t header_bytes, int64_t * transport_bytes);
+/* Expand a compact blob already on device `device` into out_dev (out_bytes >= the device-layout size). */
+int q2a_expand_blob(const void * device_blob, int64_t size, void * out_dev, int64_t out_bytes, int device, void * stream);
 
 /* A second engine on the same device sharing `base`'s weights (its own workspace and stream): the analogue of a
  * second whisper_state on one whisper_context. `base` must outlive it. */

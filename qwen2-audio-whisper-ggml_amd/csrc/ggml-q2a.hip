@@ -502,9 +502,9 @@ __global__ void k_attn_out(const float * o, tview d, int T, int H, int64_t n) {
 // MUL_MAT(F32 im2col, F16 conv kernel) on the fp16 MFMA GEMM (the conv graph nodes, qwen2-whisper.cpp:1926-1931 via
 // ggml_conv_1d): every f32 activation x is written as P fp16 parts against the weight row repeated P times, operand rows
 // [M][K] -> [M][PK] against [N][PK]. P = 3 (conv_parts): hi = fp16(x), mid = fp16(x - hi), lo = fp16(x - hi - mid)
-// hold x exactly (24 bits in three 11-bit pieces), so every product is the f32 product exactly; P = 2 (hi | mid, 22
-// significant bits) where the third part would triple a large node's MFMA work for nothing (conv2: its input is the
-// GELU table's fp16 values, for which mid = lo = 0)
+// hold x exactly (24 bits in three 11-bit pieces), so every product is the f32 product exactly. Both conv nodes use
+// it: conv2's input is mostly the GELU table's fp16 values (mid = lo = 0), but ggml_vec_gelu_f32 passes x >= 10
+// through as f32 (ggml.c:2562), which two parts (22 bits) would round
 __global__ void k_hilo_rows(const float * x, _Float16 * a, int K, int P, int n) {
     const int i = (int) blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -770,8 +770,11 @@ dim3 grid1(int64_t n) { return dim3((unsigned) ((n + 255) / 256)); }
 // buffers), so no replay can touch freed memory.
 // A buffer must grow while graph_compute is capturing (the second sighting of a cgraph whose node sequence needs more
 // than its first run did): a capturing stream cannot be synchronised and the capture would bake in the buffer about
-// to be freed. End the capture and discard it (nothing captured has run); run_nodes stops at the next node and
-// graph_compute runs the cgraph again directly, against the new buffers.
+// to be freed. End the capture and discard it (nothing captured has run). The node that asked for the buffer would
+// otherwise go on launching its kernels directly, on inputs that earlier nodes only captured and never computed, so
+// once the buffer has grown a DISCARD capture is begun (resume_discard): whatever the rest of that node launches is
+// captured into it and thrown away. run_nodes stops at the next node, and graph_compute ends the discard capture and
+// runs the cgraph again directly, against the new buffers.
 void abort_capture(q2a_backend_ctx * b) {
     hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(b->stream, &st) == hipSuccess && st == hipStreamCaptureStatusActive) {
@@ -781,6 +784,23 @@ void abort_capture(q2a_backend_ctx * b) {
         (void) hipGetLastError();
         b->capture_aborted = true;
     }
+}
+
+// after the growth that abort_capture allowed: route the aborted node's remaining launches into a discarded capture
+void resume_discard(q2a_backend_ctx * b) {
+    if (b->capture_aborted && hipStreamBeginCapture(b->stream, hipStreamCaptureModeThreadLocal) != hipSuccess)
+        (void) hipGetLastError();
+}
+
+// end (and drop) the discard capture, if one is open
+void end_discard(q2a_backend_ctx * b) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(b->stream, &st) == hipSuccess && st == hipStreamCaptureStatusActive) {
+        hipGraph_t gr = nullptr;
+        (void) hipStreamEndCapture(b->stream, &gr);
+        if (gr) (void) hipGraphDestroy(gr);
+    }
+    (void) hipGetLastError();
 }
 
 void drop_graphs(q2a_backend_ctx * b) {
@@ -802,6 +822,7 @@ void * scratch(q2a_backend_ctx * b, size_t bytes) {
         Q2A_HIP(hipMalloc(&b->scratch, bytes));
         b->scratch_bytes = bytes;
         drop_graphs(b);
+        resume_discard(b);
     }
     return b->scratch;
 }
@@ -999,12 +1020,12 @@ bool conv_hilo_ok(const ggml_tensor * op) {
     if (!ggml_is_contiguous(x) || !ggml_is_contiguous(w) || !ggml_is_contiguous(op)) return false;
     if (x->ne[2] != 1 || x->ne[3] != 1 || w->ne[2] != 1 || w->ne[3] != 1) return false;
     const int64_t K = x->ne[0], M = x->ne[1], N = w->ne[1];
-    return K % 64 == 0 && N % 128 == 0 && 2 * K <= 16384 && M * K < (1ll << 30) && N * K < (1ll << 30);
+    return K % 64 == 0 && N % 128 == 0 && 3 * K <= 16384 && M * K < (1ll << 30) && N * K < (1ll << 30);
 }
 
-// operand parts of a conv MUL_MAT: the exact three-part split where it is cheap (conv1: K = 3 x 128 mel bins), the
-// two-part one for the large conv2 node (K = 3 x 1280, fp16-exact GELU inputs)
-int conv_parts(int K) { return 3 * K <= 4096 ? 3 : 2; }
+// operand parts of a conv MUL_MAT: the exact three-part split for both nodes (conv1: K = 3 x 128 mel bins; conv2:
+// K = 3 x 1280, where the GELU passthrough values x >= 10 need all 24 bits)
+int conv_parts(int K) { (void) K; return 3; }
 
 // out[n][m] = sum_k x[m][k] * w[n][k] (ggml MUL_MAT with src0 = x F32, src1 = w F16): GEMM [M][N] into the scratch,
 // then one transpose into the node's [N][M] layout
@@ -1110,6 +1131,7 @@ _Float16 * vt_buffer(q2a_backend_ctx * b, size_t bytes) {
         Q2A_HIP(hipMalloc((void **) &b->vt_buf, bytes));
         b->vt_bytes = bytes;
         drop_graphs(b);
+        resume_discard(b);
     }
     return b->vt_buf;
 }
@@ -1126,6 +1148,7 @@ _Float16 * claim_a16(q2a_backend_ctx * b, const ggml_tensor * t) {
         Q2A_HIP(hipMalloc((void **) &b->a16[k], bytes));
         b->a16_bytes[k] = bytes;
         drop_graphs(b);
+        resume_discard(b);
     }
     b->a16_last = k;
     b->a16_src[k] = t;
@@ -1580,6 +1603,7 @@ ggml_status graph_compute(ggml_backend_t backend, ggml_cgraph * g) {
         if (hipStreamBeginCapture(b->stream, hipStreamCaptureModeThreadLocal) == hipSuccess) {
             const ggml_status st = run_nodes(b, g);
             if (b->capture_aborted) {   // a buffer grew mid-capture: the capture is gone, nothing of it ran
+                end_discard(b);         // (the aborted node's remaining launches, discarded)
                 b->capture_aborted = false;
                 c->seen = 1;            // captured again on its next sighting, against the grown buffers
                 return run_nodes(b, g);

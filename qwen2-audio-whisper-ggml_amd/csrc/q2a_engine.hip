@@ -50,7 +50,7 @@ constexpr uint32_t BLOB_MAGIC = 0x42413251u;   // "Q2AB"
 #ifndef Q2A_FC1_PATH
 #define Q2A_FC1_PATH 0   // the engine's default fc1 -> fc2 operand path (below; diagnostic builds select another)
 #endif
-constexpr uint32_t BLOB_VERSION = 4;   // 4: conv1 taps against the three-part mel operand
+constexpr uint32_t BLOB_VERSION = 5;   // 4: conv1 taps against the three-part mel operand; 5: compact transport form
 constexpr int MAX_LAYERS = 64;
 constexpr size_t HEADER_BYTES = 32768;
 
@@ -64,7 +64,8 @@ struct blob_header {
     uint32_t magic, version;
     q2a_hparams hp;
     int32_t wtype, blk, n_bins, act;   // act: Q2A_ACT_REFERENCE (0) or Q2A_ACT_BF16 (1)
-    uint64_t total;
+    int32_t compact;                   // 1: the transport form (compact_of below); 0: the device layout
+    uint64_t total;                    // bytes of the device layout (goff / loff address it)
     uint64_t goff[G_COUNT];
     uint64_t loff[MAX_LAYERS][L_COUNT];
 };
@@ -139,6 +140,41 @@ bool plan(blob_header & h, const q2a_hparams & hp, int wtype, int act) {
     }
     h.total = off;
     return true;
+}
+
+// The compact TRANSPORT form of a blob (what rank 0 broadcasts): the header (compact = 1, goff / loff
+// still describing the device layout), the small sections verbatim as two kinds of runs — the global one
+// [HEADER_BYTES, loff[0][L_BQKV]) and, per layer, the biases + LayerNorm run [loff[l][L_BQKV], loff[l][L_MAT0]) — then
+// every linear weight as the model file's own ggml rows (QKV: the q | k | v rows), e.g. raw block_q4_K at 144 B per
+// 256 weights instead of the 2-byte sc*q expansion plus its block-scale arrays. expand_blob rebuilds the device
+// layout from it on the GPU, byte for byte what pack() writes on the host.
+struct compact_layout {
+    uint64_t g_off, g_len;
+    uint64_t l_off[MAX_LAYERS], l_len[MAX_LAYERS];
+    uint64_t raw_off[MAX_LAYERS][4], raw_len[MAX_LAYERS][4];
+    uint64_t total;
+};
+compact_layout compact_of(const blob_header & h) {
+    compact_layout c;
+    memset(&c, 0, sizeof(c));
+    const dims d = dims_of(h.hp);
+    uint64_t off = HEADER_BYTES;
+    auto take = [&](uint64_t bytes) { const uint64_t o = off; off += (bytes + 255) & ~uint64_t(255); return o; };
+    c.g_len = h.loff[0][L_BQKV] - HEADER_BYTES;
+    c.g_off = take(c.g_len);
+    for (int l = 0; l < d.L; ++l) {
+        c.l_len[l] = h.loff[l][L_MAT0 + A_W] - h.loff[l][L_BQKV];
+        c.l_off[l] = take(c.l_len[l]);
+    }
+    for (int l = 0; l < d.L; ++l)
+        for (int w = 0; w < 4; ++w) {
+            int N, K;
+            mat_dims(d, w, N, K);
+            c.raw_len[l][w] = (uint64_t) N * q2a_row_size(h.wtype, K);
+            c.raw_off[l][w] = take(c.raw_len[l][w]);
+        }
+    c.total = off;
+    return c;
 }
 
 inline void scale_min_k4(int j, const uint8_t * q, uint8_t * dd, uint8_t * mm) {   // ggml-quants.c:1898
@@ -272,7 +308,7 @@ void expand_rows(const uint8_t * src, int wtype, int K, int Ntot, int r0, int r1
     }
 }
 
-int pack(const char * path, std::vector<uint8_t> & out, int act = 0) {
+int pack(const char * path, std::vector<uint8_t> & out, int act = 0, bool compact = false) {
     char err[256];
     q2a_model_file * mf = q2a_model_file_read(path, err, sizeof(err));
     if (!mf) { set_err("%s", err); return errno == ENOENT ? Q2A_ERR_IO : Q2A_ERR_FORMAT; }
@@ -405,6 +441,28 @@ int pack(const char * path, std::vector<uint8_t> & out, int act = 0) {
         jobs.push_back({w1, d.D, d.F, 0, d.F, lo + L_MAT0 + 2 * A_COUNT, 0});
         jobs.push_back({w2, d.F, d.D, 0, d.D, lo + L_MAT0 + 3 * A_COUNT, 0});
     }
+    if (compact) {   // the transport form: small sections verbatim, linear weights as the file's ggml rows
+        h.compact = 1;
+        const compact_layout c = compact_of(h);
+        std::vector<uint8_t> cb(c.total, 0);
+        memcpy(cb.data(), &h, sizeof(h));
+        memcpy(cb.data() + c.g_off, blob + HEADER_BYTES, c.g_len);
+        for (int l = 0; l < d.L; ++l) {
+            memcpy(cb.data() + c.l_off[l], blob + h.loff[l][L_BQKV], c.l_len[l]);
+            for (int w = 0; w < 4; ++w) {   // jobs[6l..6l+5] = q, k, v, o, fc1, fc2
+                const int j0 = w == 0 ? 0 : w + 2, nj = w == 0 ? 3 : 1;
+                uint64_t o = c.raw_off[l][w];
+                for (int q = 0; q < nj; ++q) {
+                    const job & jb = jobs[6 * l + j0 + q];
+                    const size_t n = (size_t) (jb.r1 - jb.r0) * q2a_row_size(wtype, jb.K);
+                    memcpy(cb.data() + o, jb.src, n);
+                    o += n;
+                }
+            }
+        }
+        out.swap(cb);
+        return Q2A_OK;
+    }
     const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::thread> th;
     for (unsigned t = 0; t < nt; ++t)
@@ -492,6 +550,133 @@ __global__ void k_split3(const float * x, q2a_half * y, int K, int64_t n) {
     o[0] = h;
     o[K] = (_Float16) (v - (float) h);
     o[2 * K] = h;
+}
+
+// ---- compact blob -> device layout (expand_rows on the GPU: every value bit-identical to the host pack) ----
+__device__ __forceinline__ float h2f(uint16_t u) { return (float) __builtin_bit_cast(_Float16, u); }
+__device__ __forceinline__ uint16_t f2h(float f) { return __builtin_bit_cast(uint16_t, (_Float16) f); }   // RNE
+__device__ __forceinline__ uint16_t f2bf(float f) {   // RNE on the bits, as f32_to_bf16 (finite inputs)
+    const uint32_t u = __builtin_bit_cast(uint32_t, f);
+    return (uint16_t) ((u + 0x7FFFu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ void scale_min_k4_d(int j, const uint8_t * q, int & dd, int & mm) {   // ggml-quants.c:1898
+    if (j < 4) { dd = q[j] & 63; mm = q[j + 4] & 63; }
+    else { dd = (q[j + 4] & 0xF) | ((q[j - 4] >> 6) << 4); mm = (q[j + 4] >> 4) | ((q[j - 0] >> 6) << 4); }
+}
+
+struct expand_args {
+    const uint8_t * raw;    // ggml rows [nrows][row_size]
+    uint8_t * blob;         // device layout
+    uint64_t a[A_COUNT];    // the matrix's array offsets in the device layout
+    int wtype, act, K, Ntot, kx;
+};
+
+// one workgroup = 256 consecutive weights of one row (blockIdx.x = row, blockIdx.y = 256-chunk of K); the float
+// operations are expand_rows' / dequant_row's, uncontracted, so every byte equals the host pack
+__global__ __launch_bounds__(256) void k_expand_rows(const expand_args p) {
+#pragma clang fp contract(off)
+    const int n = blockIdx.x, t = threadIdx.x, k = blockIdx.y * 256 + t;
+    const size_t rs = p.wtype == Q2A_TYPE_Q4_K ? (size_t) p.K / 256 * 144 : p.wtype == Q2A_TYPE_Q8_0 ? (size_t) p.K / 32 * 34
+                    : p.wtype == Q2A_TYPE_Q4_0 ? (size_t) p.K / 32 * 18 : p.wtype == Q2A_TYPE_F16 ? (size_t) p.K * 2 : (size_t) p.K * 4;
+    const uint8_t * row = p.raw + (size_t) n * rs;
+    uint16_t * W = (uint16_t *) (p.blob + p.a[A_W]);
+    if (k >= p.K) return;
+    float val = 0.0f;   // dequantized value (bf16 mode)
+    if (p.wtype == Q2A_TYPE_Q4_K) {
+        const int b = k / 256, j = (k % 256) / 32, l = k % 32;
+        const q2a_block_q4_K * x = (const q2a_block_q4_K *) row + b;
+        int sc, m;
+        scale_min_k4_d(j, x->scales, sc, m);
+        const int v = (j & 1) ? (x->qs[32 * (j / 2) + l] >> 4) : (x->qs[32 * (j / 2) + l] & 0xF);
+        const float d = h2f(x->d), dmin = h2f(x->dmin);
+        if (p.act) {
+            const float d1 = d * (float) sc, m1 = dmin * (float) m;
+            val = d1 * (float) v - m1;
+        } else {
+            W[(size_t) n * p.K + k] = d != 0.0f ? f2h((float) (sc * v)) : (uint16_t) 0;
+            const size_t bi = (size_t) b * p.Ntot + n;
+            const float deff = d != 0.0f ? d : 1.0f;
+            if (t == 0) {
+                float dprev = 1.0f;
+                if (b > 0) { const float dp = h2f(((const q2a_block_q4_K *) row + b - 1)->d); dprev = dp != 0.0f ? dp : 1.0f; }
+                ((float *) (p.blob + p.a[A_DX]))[bi] = deff;
+                ((float *) (p.blob + p.a[A_DMIN]))[bi] = dmin;
+                ((float *) (p.blob + p.a[A_BETA]))[bi] = dprev / deff;
+                ((float *) (p.blob + p.a[A_GAMMA]))[bi] = -(dmin / deff);
+            }
+            if (t < 16) {
+                int sj, mj;
+                scale_min_k4_d(t / 2, x->scales, sj, mj);
+                ((uint16_t *) (p.blob + p.a[A_WEXT]))[bi * 16 + t] = f2h((t & 1) ? (float) mj : 64.0f * (float) mj);
+            }
+            return;
+        }
+    } else if (p.wtype == Q2A_TYPE_Q8_0) {
+        const q2a_block_q8_0 * x = (const q2a_block_q8_0 *) row + k / 32;
+        const float d = h2f(x->d);
+        if (p.act) val = x->qs[k % 32] * d;
+        else {
+            W[(size_t) n * p.K + k] = f2h((float) x->qs[k % 32]);
+            if (k % 32 == 0) ((float *) (p.blob + p.a[A_DX]))[(size_t) (k / 32) * p.Ntot + n] = d;
+            return;
+        }
+    } else if (p.wtype == Q2A_TYPE_Q4_0) {
+        const q2a_block_q4_0 * x = (const q2a_block_q4_0 *) row + k / 32;
+        const int l = k % 32, q = (l < 16 ? (x->qs[l] & 0xF) : (x->qs[l - 16] >> 4)) - 8;
+        const float d = h2f(x->d);
+        if (p.act) val = q * d;
+        else {
+            W[(size_t) n * p.K + k] = f2h((float) q);
+            if (l == 0) ((float *) (p.blob + p.a[A_DX]))[(size_t) (k / 32) * p.Ntot + n] = d;
+            return;
+        }
+    } else if (p.wtype == Q2A_TYPE_F16) {
+        const uint16_t u = ((const uint16_t *) row)[k];
+        if (p.act) val = h2f(u);
+        else { W[(size_t) n * p.K + k] = u; return; }
+    } else {   // F32
+        const float x = ((const float *) row)[k];
+        if (p.act) val = x;
+        else {   // [Wh | Wh | Wl]
+            uint16_t * w3 = W + (size_t) n * 3 * p.K;
+            const uint16_t hi = f2h(x);
+            w3[k] = hi;
+            w3[p.K + k] = hi;
+            w3[2 * p.K + k] = f2h(x - h2f(hi));
+            return;
+        }
+    }
+    W[(size_t) n * p.K + k] = f2bf(val);
+}
+
+// device layout of `h` (compact = 1) from the compact blob `cb` (both on the current device); `out` holds h.total bytes
+int expand_blob(const uint8_t * cb, const blob_header & h, uint8_t * out, hipStream_t s) {
+    const compact_layout c = compact_of(h);
+    const dims d = dims_of(h.hp);
+    std::vector<uint8_t> head(HEADER_BYTES, 0);
+    blob_header hx = h;
+    hx.compact = 0;
+    memcpy(head.data(), &hx, sizeof(hx));
+    HIP_TRY(hipMemsetAsync(out, 0, h.total, s));
+    HIP_TRY(hipMemcpyAsync(out, head.data(), HEADER_BYTES, hipMemcpyHostToDevice, s));
+    HIP_TRY(hipMemcpyAsync(out + HEADER_BYTES, cb + c.g_off, c.g_len, hipMemcpyDeviceToDevice, s));
+    const int kx = h.wtype == Q2A_TYPE_F32 && !h.act ? 3 : 1;
+    for (int l = 0; l < d.L; ++l) {
+        HIP_TRY(hipMemcpyAsync(out + h.loff[l][L_BQKV], cb + c.l_off[l], c.l_len[l], hipMemcpyDeviceToDevice, s));
+        for (int w = 0; w < 4; ++w) {
+            int N, K;
+            mat_dims(d, w, N, K);
+            expand_args a;
+            a.raw = cb + c.raw_off[l][w];
+            a.blob = out;
+            for (int i = 0; i < A_COUNT; ++i) a.a[i] = h.loff[l][L_MAT0 + w * A_COUNT + i];
+            a.wtype = h.wtype; a.act = h.act; a.K = K; a.Ntot = N; a.kx = kx;
+            hipLaunchKernelGGL(k_expand_rows, dim3((unsigned) N, (unsigned) ((K + 255) / 256)), dim3(256), 0, s, a);
+            HIP_TRY(hipGetLastError());
+        }
+    }
+    HIP_TRY(hipStreamSynchronize(s));   // (the header's host staging must outlive its copy)
+    return Q2A_OK;
 }
 
 hipError_t launch_split3(const float * x, q2a_half * y, int K, int64_t n, hipStream_t s) {
@@ -1007,6 +1192,37 @@ int64_t q2a_pack_model_ex(const char * path, int act, void ** host_blob) {
     return (int64_t) v.size();
 }
 
+int64_t q2a_pack_model_compact(const char * path, int act, void ** host_blob) {
+    if (act != Q2A_ACT_REFERENCE && act != Q2A_ACT_BF16) { set_err("unknown activation mode %d", act); return Q2A_ERR_ARG; }
+    std::vector<uint8_t> v;
+    const int rc = pack(path, v, act, true);
+    if (rc) return rc;
+    void * p = malloc(v.size());
+    if (!p) { set_err("host allocation failed"); return Q2A_ERR_OOM; }
+    memcpy(p, v.data(), v.size());
+    *host_blob = p;
+    return (int64_t) v.size();
+}
+
+int64_t q2a_blob_device_size(const void * host_header, int64_t header_bytes, int64_t * transport_bytes) {
+    blob_header h;
+    if (!host_header || header_bytes < (int64_t) sizeof(h)) { set_err("invalid arguments"); return Q2A_ERR_ARG; }
+    memcpy(&h, host_header, sizeof(h));
+    if (h.magic != BLOB_MAGIC || h.version != BLOB_VERSION) { set_err("not a q2a weight blob"); return Q2A_ERR_FORMAT; }
+    if (transport_bytes) *transport_bytes = h.compact ? (int64_t) compact_of(h).total : (int64_t) h.total;
+    return (int64_t) h.total;
+}
+
+int q2a_expand_blob(const void * dev_blob, int64_t size, void * dev_out, int64_t out_bytes, int device, void * stream) {
+    if (!dev_blob || !dev_out || size < (int64_t) HEADER_BYTES) { set_err("invalid arguments"); return Q2A_ERR_ARG; }
+    HIP_TRY(hipSetDevice(device));
+    blob_header h;
+    HIP_TRY(hipMemcpy(&h, dev_blob, sizeof(h), hipMemcpyDeviceToHost));
+    if (h.magic != BLOB_MAGIC || h.version != BLOB_VERSION || !h.compact) { set_err("not a compact q2a weight blob"); return Q2A_ERR_FORMAT; }
+    if ((int64_t) compact_of(h).total != size || out_bytes < (int64_t) h.total) { set_err("blob size mismatch"); return Q2A_ERR_ARG; }
+    return expand_blob((const uint8_t *) dev_blob, h, (uint8_t *) dev_out, stream ? (hipStream_t) stream : nullptr);
+}
+
 void q2a_free_host_blob(void * p) { free(p); }
 
 q2a_engine * q2a_open(const char * model_path, int device) { return q2a_open_ex(model_path, device, Q2A_ACT_REFERENCE); }
@@ -1043,10 +1259,26 @@ q2a_engine * q2a_open_device_blob(const void * dev_blob, int64_t size, int devic
         q2a_close(e);
         return nullptr;
     }
-    if (engine_adopt_header(e) || (int64_t) e->h.total != size) {
+    g_err.clear();
+    const int64_t want = e->h.compact ? (int64_t) compact_of(e->h).total : (int64_t) e->h.total;
+    if (engine_adopt_header(e) || want != size) {
         if (g_err.empty()) set_err("blob size mismatch");
         q2a_close(e);
         return nullptr;
+    }
+    if (e->h.compact) {   // the transport form: expand into an engine-owned device layout
+        const blob_header hc = e->h;
+        e->h.compact = 0;
+        if (hipMalloc((void **) &e->blob, e->h.total) != hipSuccess) {
+            (void) hipGetLastError();
+            set_err("weight allocation of %.2f GB failed", e->h.total / 1e9);
+            q2a_close(e);
+            return nullptr;
+        }
+        e->own_blob = true;
+        e->blob_size = (int64_t) e->h.total;
+        if (expand_blob((const uint8_t *) dev_blob, hc, e->blob, e->stream)) { q2a_close(e); return nullptr; }
+        return e;
     }
     e->blob = (uint8_t *) dev_blob;
     e->own_blob = false;
@@ -1131,16 +1363,21 @@ int q2a_encode_host_ex(q2a_engine * e, const float * const * pcm, const int32_t 
     maxn = (maxn + 63) & ~int64_t(63);
     if (int rc = ensure_host_bufs(e, C, maxn)) return rc;
     const size_t per_out = (size_t) e->d.TO * e->d.D;
-    std::vector<int32_t> st(n_clips);
+    // st: what encode_impl reported per clip; pub: what the caller gets — a clip's status is published only once its
+    // chunk's outputs reached out_host, so a failure part-way leaves every later clip (and a chunk whose copy-out
+    // never ran) at Q2A_CLIP_FAILED rather than a stale "encoded"
+    std::vector<int32_t> st(n_clips, Q2A_CLIP_FAILED), pub(n_clips, Q2A_CLIP_FAILED);
     hipStream_t cs = e->copy_stream, s = e->stream;
     int rc = Q2A_OK;
     auto copy_out = [&](int k) {   // chunk k's encoded outputs: pinned -> caller (after its D2H)
         const int c0 = k * C, n = std::min(C, n_clips - c0);
         q2a_engine::host_buf & b = e->hb[k & 1];
         if (hipEventSynchronize(b.d2h) != hipSuccess) return Q2A_ERR_HIP;
-        for (int c = 0; c < n; ++c)
+        for (int c = 0; c < n; ++c) {
             if (st[c0 + c] == Q2A_CLIP_ENCODED)
                 memcpy(out_host + (c0 + c) * per_out, b.pin_out + c * per_out, per_out * 4);
+            pub[c0 + c] = st[c0 + c];
+        }
         return Q2A_OK;
     };
     for (int k = 0; k < nchunk && rc == Q2A_OK; ++k) {
@@ -1175,7 +1412,7 @@ int q2a_encode_host_ex(q2a_engine * e, const float * const * pcm, const int32_t 
         if (rc == Q2A_OK) { set_err("stream error"); rc = Q2A_ERR_HIP; }
     }
     if (rc == Q2A_ERR_HIP && g_err.empty()) set_err("host-path copy failed");
-    if (status) for (int c = 0; c < n_clips; ++c) status[c] = st[c];
+    if (status) for (int c = 0; c < n_clips; ++c) status[c] = pub[c];
     return rc;
 }
 

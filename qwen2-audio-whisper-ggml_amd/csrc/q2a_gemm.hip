@@ -63,6 +63,10 @@ __device__ __forceinline__ void q2a_st(const V & v, V * ptr) {
 #ifndef Q2A_GEMM_STAGED_EPI
 #define Q2A_GEMM_STAGED_EPI 1
 #endif
+// 8-phase kernel: waves 4-7 one barrier behind waves 0-3 (0 = lockstep halves)
+#ifndef Q2A_GEMM_WSTAGGER
+#define Q2A_GEMM_WSTAGGER 0
+#endif
 
 constexpr int BK = 64;
 constexpr int ROWB = BK * 2;   // bytes per LDS row (64 halves)
@@ -404,11 +408,23 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
                 for (int j = 0; j < 2; ++j)
                     acc[qm * 4 + i][qn * 2 + j] = mma16<BF>(bf[qn][j][s2], af[i][s2], acc[qm * 4 + i][qn * 2 + j]);
     };
+#if Q2A_GEMM_WSTAGGER
+    // staggered halves: the fragment reads retire BEFORE the barrier, so an image restaged the phase after its last
+    // read (A_q0) cannot overtake the other half's reads, which now run one barrier later (cdna_hip_programming.md
+    // §5 WAR rule)
+#define Q2A_PB(N)                                               \
+    asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory");       \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          \
+    __builtin_amdgcn_s_barrier();                               \
+    asm volatile("" ::: "memory");                              \
+    __builtin_amdgcn_s_setprio(1)
+#else
 #define Q2A_PB(N)                                               \
     asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory");       \
     __builtin_amdgcn_s_barrier();                               \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          \
     __builtin_amdgcn_s_setprio(1)
+#endif
 #define Q2A_PE()                                                \
     __builtin_amdgcn_s_setprio(0);                              \
     asm volatile("" ::: "memory");                              \
@@ -428,8 +444,14 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    // wave stagger: the M-half wm = 1 (waves 4-7, the SIMD partners of waves 0-3) runs one barrier behind, so each
+    // SIMD alternates one wave's MFMA segment with its partner's fragment reads / glds issue (MI355X_MICROARCH.md,
+    // "Two waves per SIMD" item 9); the other half pays the extra barrier after the loop
+    auto stagger_in = [&]() { if (Q2A_GEMM_WSTAGGER && wm == 1) { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); } };
+    auto stagger_out = [&]() { if (Q2A_GEMM_WSTAGGER && wm == 0) { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); } };
 
     if constexpr (BLK == 0) {
+        stagger_in();
         int kt = 0;
         for (; kt < nk - 2; kt += 2) {
             Q2A_KSTEP(0, stage(1, 1, kt + 1), stage(0, 0, kt + 2), stage(0, 2, kt + 2), stage(0, 3, kt + 2), 10, 10, 10, 10);
@@ -443,6 +465,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // raw barrier: __syncthreads would drain the prologue glds
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
+        stagger_in();
         int kt = 0;
         for (; kt < nk - 4; kt += 4) {
             if (kt == 0) block_start(std::true_type{});
@@ -469,6 +492,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #undef Q2A_KSTEP
 #undef Q2A_PB
 #undef Q2A_PE
+    stagger_out();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tail re-loads still land in LDS: drain before the epilogue
     __syncthreads();
     if constexpr (BLK == 256) {

@@ -21,6 +21,7 @@ EXPORTS = (
     "q2a_test_linear", "q2a_test_block", "q2a_test_block_taps", "q2a_test_attention", "q2a_test_fc1_path",
     "q2a_test_frontend", "q2a_test_pool_ln",
     "q2a_projector_open", "q2a_projector_close", "q2a_projector_get_dims", "q2a_projector_apply",
+    "q2a_pack_model_compact", "q2a_blob_device_size", "q2a_expand_blob",
 )
 
 CLIP_ENCODED, CLIP_SKIPPED = 0, 1
@@ -63,6 +64,12 @@ def lib() -> C.CDLL:
         L.q2a_pack_model_ex.restype = C.c_int64
         L.q2a_pack_model_ex.argtypes = [C.c_char_p, C.c_int, C.POINTER(vp)]
         L.q2a_free_host_blob.argtypes = [vp]
+        if hasattr(L, "q2a_pack_model_compact"):   # round 4 (optional: earlier diagnostic builds load too)
+            L.q2a_pack_model_compact.restype = C.c_int64
+            L.q2a_pack_model_compact.argtypes = [C.c_char_p, C.c_int, C.POINTER(vp)]
+            L.q2a_blob_device_size.restype = C.c_int64
+            L.q2a_blob_device_size.argtypes = [vp, C.c_int64, C.POINTER(C.c_int64)]
+            L.q2a_expand_blob.argtypes = [vp, C.c_int64, vp, C.c_int64, C.c_int, vp]
         L.q2a_open_device_blob.restype = vp
         L.q2a_open_device_blob.argtypes = [vp, C.c_int64, C.c_int]
         L.q2a_close.argtypes = [vp]
@@ -221,13 +228,34 @@ class Projector:
             pass
 
 
-def pack_model(path: str, act: int = ACT_REFERENCE) -> bytes:
-    """Pack a model file into the device-layout blob (host bytes), e.g. for an RCCL broadcast."""
+def pack_model(path: str, act: int = ACT_REFERENCE, compact: bool = False) -> bytearray:
+    """Pack a model file into a blob (host bytes, one copy out of the library's buffer): the device layout, or with
+    compact=True its transport form (ggml weight rows, expanded on the GPU by Engine(device_blob=...)), e.g. for the
+    RCCL broadcast."""
     p = C.c_void_p()
-    n = lib().q2a_pack_model_ex(path.encode(), act, C.byref(p))
+    f = lib().q2a_pack_model_compact if compact else lib().q2a_pack_model_ex
+    n = f(path.encode(), act, C.byref(p))
     if n < 0:
         raise Q2AError(lib().q2a_last_error().decode())
     try:
-        return C.string_at(p, n)
+        out = bytearray(n)
+        C.memmove((C.c_char * n).from_buffer(out), p, n)
+        return out
     finally:
         lib().q2a_free_host_blob(p)
+
+
+def blob_device_size(blob) -> tuple[int, int]:
+    """(device-layout bytes, transport bytes) of a host blob (its header)."""
+    head = (C.c_char * 32768).from_buffer_copy(bytes(blob[:32768]))
+    tb = C.c_int64(0)
+    n = lib().q2a_blob_device_size(C.cast(head, C.c_void_p), 32768, C.byref(tb))
+    if n < 0:
+        raise Q2AError(lib().q2a_last_error().decode())
+    return int(n), int(tb.value)
+
+
+def expand_blob(dev_ptr: int, size: int, out_ptr: int, out_bytes: int, device: int = 0, stream=None):
+    """Expand a compact blob on the device into the device layout (what q2a_open_device_blob does internally)."""
+    _check(lib().q2a_expand_blob(C.c_void_p(dev_ptr), C.c_int64(size), C.c_void_p(out_ptr), C.c_int64(out_bytes),
+                                 device, C.c_void_p(stream) if stream else None))

@@ -40,8 +40,9 @@ def broadcast_blob(dist, blob_host: bytes | bytearray | None, rank: int, device)
         dist.broadcast(size_t, 0)
     nbytes = int(size_t.item())
     blob = torch.empty(nbytes, dtype=torch.uint8, device=device)
-    if rank == 0:
-        blob.copy_(torch.frombuffer(bytearray(blob_host), dtype=torch.uint8))
+    if rank == 0:   # a bytearray (q2a.pack_model) is viewed, not copied; other buffers are copied once
+        src = blob_host if isinstance(blob_host, bytearray) else bytearray(blob_host)
+        blob.copy_(torch.frombuffer(src, dtype=torch.uint8))
     if dist is not None:
         dist.broadcast(blob, 0)
     return blob

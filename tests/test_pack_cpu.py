@@ -12,9 +12,9 @@ import pytest
 
 from q2a import ggmlfile
 
-# blob_header layout: u32 magic, version | 11 x i32 hparams | i32 wtype, blk, n_bins, act | u64 total |
+# blob_header layout: u32 magic, version | 11 x i32 hparams | i32 wtype, blk, n_bins, act, compact | u64 total |
 # u64 goff[11] | u64 loff[64][32]
-OFF_WTYPE, OFF_BLK, OFF_ACT, OFF_TOTAL, OFF_GOFF = 52, 56, 64, 72, 80
+OFF_WTYPE, OFF_BLK, OFF_ACT, OFF_COMPACT, OFF_TOTAL, OFF_GOFF = 52, 56, 64, 68, 72, 80
 G_COUNT, L_COUNT, L_MAT0, A_COUNT, A_W, A_DX = 11, 32, 8, 6, 0, 1
 
 
@@ -73,16 +73,52 @@ def test_unknown_activation_contract_is_rejected(make_model):
 
 def test_blob_version_tracks_the_q4k_layout(make_model):
     """Blob version 3 = Q4_K gamma stored negated (-(dmin/dx)); version 4 = conv1 taps against the three-part mel
-    operand. The Q4_K gamma section of a packed blob must be <= 0 everywhere, and the header must say 4 so an older
-    build's blob (positive gamma, two-part conv1 taps) is refused on open."""
+    operand; version 5 = the compact transport flag in the header. The Q4_K gamma section of a packed blob must be
+    <= 0 everywhere, and the header must say 5 so an older build's blob is refused on open."""
     import q2a
     path = make_model("tiny", "q4_k")
     blob = q2a.pack_model(path)
     magic, version = struct.unpack_from("<II", blob, 0)
-    assert magic == 0x42413251 and version == 4
+    assert magic == 0x42413251 and version == 5
     _, blk, _, _, loff0 = header(blob)
     assert blk == 256
     A_GAMMA = 5
     off = loff0[L_MAT0 + A_GAMMA]
     gamma = np.frombuffer(blob, dtype=np.float32, count=(256 // 256) * 3 * 256, offset=off)
     assert np.all(gamma <= 0) and np.any(gamma < 0)
+
+
+@pytest.mark.parametrize("cfg,wt", [("tiny", "q4_k"), ("tiny", "q8_0"), ("tiny", "q4_0"), ("tiny", "f16"), ("full", "q4_k")])
+def test_compact_blob_is_the_file_rows_plus_small_sections(make_model, cfg, wt):
+    """The compact transport blob (q2a_pack_model_compact): same header (compact = 1, goff / loff of the device layout),
+    the small sections verbatim, and every linear weight as the model file's own ggml rows (QKV = q | k | v rows).
+    For the full-size Q4_K model it is <= 0.4 GB against the 1.40 GB device layout (SURVEY.md §8e's 354 MB of Q4_K
+    weights plus the F16 conv kernels, positions and tables). The GPU test expands it and compares bytes."""
+    import q2a
+    path = make_model(cfg, wt)
+    full = q2a.pack_model(path)
+    comp = q2a.pack_model(path, compact=True)
+    assert struct.unpack_from("<i", comp, OFF_COMPACT)[0] == 1 and struct.unpack_from("<i", full, OFF_COMPACT)[0] == 0
+    # the header is the device layout's but for the flag
+    hf, hc = bytearray(full[:32768]), bytearray(comp[:32768])
+    hc[OFF_COMPACT:OFF_COMPACT + 4] = b"\0\0\0\0"
+    assert hf == hc
+    dev, tr = q2a.blob_device_size(comp)
+    assert dev == len(full) and tr == len(comp)
+    assert q2a.blob_device_size(full) == (len(full), len(full))
+    if (cfg, wt) == ("full", "q4_k"):
+        assert len(comp) <= 0.4e9 < 1.3e9 < len(full)
+    # layout (compact_of): global run, per-layer small runs, then the raw rows of layer 0's q | k | v first
+    _, _, _, total, loff0 = header(full)
+    L = struct.unpack_from("<i", full, 8 + 4 * 4)[0]
+    g_len = loff0[0] - 32768
+    assert comp[32768:32768 + g_len] == full[32768:32768 + g_len]
+    off = 32768 + ((g_len + 255) & ~255)
+    for l in range(L):
+        lo = struct.unpack_from(f"<{L_COUNT}Q", full, OFF_GOFF + 8 * G_COUNT + 8 * L_COUNT * l)
+        n = lo[L_MAT0 + A_W] - lo[0]
+        assert comp[off:off + n] == full[lo[0]:lo[0] + n]
+        off += (n + 255) & ~255
+    mf = ggmlfile.read(path)
+    qkv = b"".join(np.ascontiguousarray(mf.t(f"layers.0.self_attn.{n}_proj.weight").data).tobytes() for n in "qkv")
+    assert comp[off:off + len(qkv)] == qkv
