@@ -339,10 +339,11 @@ __global__ __launch_bounds__(256) void k_quant_q8k_h16(const q2a_half * __restri
     quant_q8k_row16(v, sub, outH + blk * 256 + sub * 16, dy + (int64_t) bf * ld + m, aext + ((int64_t) bf * ld + m) * 16);
 }
 
-// GELU + Q8_K of the fc1 pre-activation (Q2A_EPI_PRE_H output; fp16, x <= -10 marked -inf). Persistent workgroups
-// of 8 waves stage ggml's whole 64 Ki-entry fp16 GELU table (128 KiB) into LDS once, so an element is one lookup at
-// its own bits: entries for h >= 10 are h itself (ggml_vec_gelu_f32's x >= 10 branch: tanhf saturates to 1), and the
-// -inf marker's entry is patched to ggml's +0 for x <= -10. The kernel is VALU-bound once its stores are whole
+// GELU + Q8_K of the fc1 pre-activation (Q2A_EPI_PRE_H output, fp16). Persistent workgroups of 8 waves stage ggml's
+// whole 64 Ki-entry fp16 GELU table (128 KiB) into LDS once, so an element is one lookup at its own bits: entries for
+// h >= 10 are h itself (ggml_vec_gelu_f32's x >= 10 branch: tanhf saturates to 1), entries for h <= -10 are -0 (the
+// x <= -10 branch's +0 up to the sign, which the Q8_K codes do not see), and the -inf entry (NaN in the table) is
+// patched to +0. The kernel is VALU-bound once its stores are whole
 // sectors (~19 -> ~13 VALU per element with the direct index).
 //
 // Work unit = one block column bf of 16 consecutive rows, four wave-iterations of 4 rows (16 lanes per 256-block,
@@ -362,7 +363,7 @@ __global__ __launch_bounds__(GQ_THREADS) void k_gelu_quant_q8k_h16(const q2a_hal
     __shared__ __attribute__((aligned(16))) char stage[GQ_WAVES][2048];
     for (int i = threadIdx.x; i < 65536 / 8; i += GQ_THREADS) ((uint4 *) lut)[i] = ((const uint4 *) gelu_tab)[i];
     __syncthreads();
-    if (threadIdx.x == 0) lut[0xFC00] = 0;   // -inf marker (x <= -10) -> +0
+    if (threadIdx.x == 0) lut[0xFC00] = 0;   // -inf (x below the fp16 range) -> +0
     __syncthreads();
     const int lane = threadIdx.x & 63, sub = lane & 15, grp = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);

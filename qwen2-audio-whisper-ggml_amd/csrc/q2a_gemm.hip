@@ -68,6 +68,23 @@ __device__ __forceinline__ void q2a_st(const V & v, V * ptr) {
 #define Q2A_GEMM_WSTAGGER 0
 #endif
 
+// Timing diagnostic Q2A_DIAG_STAMPS=<epi>: the 8-phase kernels of epilogue <epi> record s_memtime at fixed points of
+// every workgroup's tile (waves 0 and 4, lane 0) into g_q2a_stamps, read back by q2a_diag_stamps (diag/tile_stamps.py):
+// 0 entry | 1 prologue landed | 2 main loop end | 3 final multiply done | 4 epilogue staged | 5 stores issued |
+// 6 stores drained | 7 sum of the Q4_K block starts | 8 / 9 s_memrealtime at entry / end (100 MHz). Never in libq2a.so.
+#ifdef Q2A_DIAG_STAMPS
+constexpr int Q2A_STAMP_SLOTS = 16;
+__device__ uint64_t g_q2a_stamps[16384 * 2 * Q2A_STAMP_SLOTS];
+__device__ __forceinline__ void q2a_stamp_put(int k, uint64_t v) {
+    if ((threadIdx.x & 255) == 0) g_q2a_stamps[((int64_t) blockIdx.x * 2 + (threadIdx.x >> 8)) * Q2A_STAMP_SLOTS + k] = v;
+}
+#define Q2A_STAMP(ON, k) do { if (ON) q2a_stamp_put((k), __builtin_amdgcn_s_memtime()); } while (0)
+#define Q2A_STAMP_RT(ON, k) do { if (ON) q2a_stamp_put((k), __builtin_amdgcn_s_memrealtime()); } while (0)
+#else
+#define Q2A_STAMP(ON, k) do { } while (0)
+#define Q2A_STAMP_RT(ON, k) do { } while (0)
+#endif
+
 constexpr int BK = 64;
 constexpr int ROWB = BK * 2;   // bytes per LDS row (64 halves)
 constexpr int GROUP_M = 4;   // swept 2..32 at the batched shapes (Q2A_GEMM_GROUP_M): 4 best by ~1 %
@@ -211,7 +228,7 @@ constexpr int SBUF_OFF = 8 * 128 * ROWB;     // 128 KiB: scale staging after the
 constexpr int SBUF_BYTES = 25 * 1024;       // 21 pieces of 1 KiB (+3 pad slots for the uniform 3 glds per thread)
 constexpr int ALPHA_OFF = 24 * 1024;        //   + alpha = dy_{b-1}/dy_b per tile row (1 KiB), computed a block ahead
 
-template <int BLK, bool LUT, bool BF>
+template <int BLK, bool LUT, bool BF, bool ST = false>
 __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&acc)[8][4], char * lds_raw, int m0, int n0,
                                                 int lane, int wave, int wm, int wn) {
     constexpr int HT = 128 * ROWB;                        // one half-tile image (16 KiB)
@@ -307,6 +324,14 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
         const float al = kq_alpha(yp, yc);
         asm volatile("ds_write_b32 %0, %1" :: "v"(sb0 + ALPHA_OFF + row * 4), "v"(al) : "memory");
     };
+#ifdef Q2A_DIAG_STAMPS
+    uint64_t bs_cycles = 0, bs_t0 = 0;
+#define BS_T0() do { if (ST) bs_t0 = __builtin_amdgcn_s_memtime(); } while (0)
+#define BS_T1() do { if (ST) bs_cycles += __builtin_amdgcn_s_memtime() - bs_t0; } while (0)
+#else
+#define BS_T0() do { } while (0)
+#define BS_T1() do { } while (0)
+#endif
     auto block_start = [&](auto first) {   // first: std::true_type for block 0 (acc = 0: only the min term)
 #ifdef Q2A_DIAG_NO_RESCALE
         return;   // timing diagnostic only (wrong results)
@@ -447,6 +472,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     // wave stagger: the M-half wm = 1 (waves 4-7, the SIMD partners of waves 0-3) runs one barrier behind, so each
     // SIMD alternates one wave's MFMA segment with its partner's fragment reads / glds issue (MI355X_MICROARCH.md,
     // "Two waves per SIMD" item 9); the other half pays the extra barrier after the loop
+    Q2A_STAMP(ST, 1);
     auto stagger_in = [&]() { if (Q2A_GEMM_WSTAGGER && wm == 1) { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); } };
     auto stagger_out = [&]() { if (Q2A_GEMM_WSTAGGER && wm == 0) { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); } };
 
@@ -468,8 +494,10 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
         stagger_in();
         int kt = 0;
         for (; kt < nk - 4; kt += 4) {
+            BS_T0();
             if (kt == 0) block_start(std::true_type{});
             else block_start(std::false_type{});
+            BS_T1();
             asm volatile("" ::: "memory");
             Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
                       stage(0, 3, kt + 2), 10, 13, 13, 13);
@@ -480,8 +508,10 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             Q2A_KSTEP(1, stage(0, 1, kt + 4), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5), 10, 10, 10, 10);
         }
         // last block: its scales stay in place for the final multiply (the scale re-stage keeps the vmcnt counts)
+        BS_T0();
         if (kt == 0) block_start(std::true_type{});
         else block_start(std::false_type{});
+        BS_T1();
         asm volatile("" ::: "memory");
         Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4)), stage(0, 2, kt + 2),
                   stage(0, 3, kt + 2), 10, 13, 13, 13);
@@ -492,7 +522,13 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #undef Q2A_KSTEP
 #undef Q2A_PB
 #undef Q2A_PE
+#undef BS_T0
+#undef BS_T1
     stagger_out();
+    Q2A_STAMP(ST, 2);
+#ifdef Q2A_DIAG_STAMPS
+    if (ST) q2a_stamp_put(7, bs_cycles);
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tail re-loads still land in LDS: drain before the epilogue
     __syncthreads();
     if constexpr (BLK == 256) {
@@ -514,6 +550,11 @@ template <int BM, int BN, int WM, int WN, int EPI, int BLK_, int PIPE>
 __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_arg) {
     q2a_gemm_args p = p_arg;   // (the grouped STORE_F launch swaps in its second GEMM's operands below)
     constexpr bool BF = BLK_ == Q2A_BLK_BF16;              // bf16 operands, no block scales
+#ifdef Q2A_DIAG_STAMPS
+    constexpr bool ST = PIPE == 1 && EPI == Q2A_DIAG_STAMPS;   // timing stamps (diagnostic builds only)
+#else
+    constexpr bool ST = false;
+#endif
     constexpr int BLK = BF ? 0 : BLK_;
     constexpr int NW = WM * WN;
     constexpr int MI = BM / WM / 16, NJ = BN / WN / 16;   // 16x16 tiles per wave
@@ -602,7 +643,10 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
     if constexpr (PIPE == 1) {
-        mainloop_8phase<BLK, LUT_EPI, BF>(p, acc, lds_raw, m0, n0, lane, wave, wm, wn);
+        Q2A_STAMP(ST, 0);
+        Q2A_STAMP_RT(ST, 8);
+        mainloop_8phase<BLK, LUT_EPI, BF, ST>(p, acc, lds_raw, m0, n0, lane, wave, wm, wn);
+        Q2A_STAMP(ST, 3);
     } else {
         // per-lane source rows of this wave's glds instructions (rows past M clamp to M-1: loaded, never stored)
         int64_t arow[LA], wrow[LB];
@@ -1053,9 +1097,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                     h4v hv;
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        if constexpr (EPI == Q2A_EPI_PRE_H) {       // pre-activation; x <= -10 marked -inf (GELU = 0)
-                            const float v = val(i, j, r);
-                            hv[r] = v <= -10.0f ? (_Float16) -INFINITY : (_Float16) v;
+                        if constexpr (EPI == Q2A_EPI_PRE_H) {       // pre-activation (no x <= -10 marker: see
+                            hv[r] = (_Float16) val(i, j, r);       // q2a_internal.h, Q2A_EPI_PRE_H)
                         } else if (pass == 0) {                     // hi, and the exact remainder's fp16 (lo)
                             const float v = val(i, j, r);
                             const _Float16 h = to16<BF>(v);
@@ -1069,6 +1112,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                 }
             }
             __syncthreads();
+            Q2A_STAMP(ST && pass == NPASS - 1, 4);
             const int g = lane & 31;
 #pragma unroll 4
             for (int k = 0; k < 16; ++k) {
@@ -1085,6 +1129,12 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                 }
             }
         }
+        Q2A_STAMP(ST, 5);
+#ifdef Q2A_DIAG_STAMPS
+        if (ST) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+        Q2A_STAMP(ST, 6);
+        Q2A_STAMP_RT(ST, 9);
       }
     } else if (EPI == Q2A_EPI_QKV && part == 2) {
       if constexpr (EPI == Q2A_EPI_QKV) {
@@ -1185,10 +1235,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     if (EPI == Q2A_EPI_GELU_H && LUT_EPI) {
-                    } else if (EPI == Q2A_EPI_PRE_H) {   // pre-activation; x <= -10 marked -inf (GELU = 0)
-                        const float va = val(i, 2 * jp, r), vb = val(i, 2 * jp + 1, r);
-                        ha[r] = va <= -10.0f ? (_Float16) -INFINITY : (_Float16) va;
-                        hb[r] = vb <= -10.0f ? (_Float16) -INFINITY : (_Float16) vb;
+                    } else if (EPI == Q2A_EPI_PRE_H) {   // pre-activation (q2a_internal.h, Q2A_EPI_PRE_H)
+                        ha[r] = (_Float16) val(i, 2 * jp, r);
+                        hb[r] = (_Float16) val(i, 2 * jp + 1, r);
                     } else {
                         const float va = val(i, 2 * jp, r), vb = val(i, 2 * jp + 1, r);
                         ha[r] = to16<BF>(va);
@@ -1352,6 +1401,12 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                 }
             }
         }
+        Q2A_STAMP(ST, 5);
+#ifdef Q2A_DIAG_STAMPS
+        if (ST) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+        Q2A_STAMP(ST, 6);
+        Q2A_STAMP_RT(ST, 9);
     }
 #undef LDS_STAGE
 }
@@ -1612,3 +1667,15 @@ hipError_t q2a_launch_gemm(const q2a_gemm_args & a_in, int epi, int blk, hipStre
 bool q2a_gemm_wide_tiles(int M, int N, int blk) { (void) blk; return wide_tiles(M, N); }
 
 bool q2a_gemm_pipe8(const q2a_gemm_args & a, int blk) { return pipe8_ok(a, blk) && (blk != 256 || a.beta); }
+
+#ifdef Q2A_DIAG_STAMPS
+// diagnostic builds only: copy the stamp array (Q2A_DIAG_STAMPS comment above) to the host
+extern "C" int q2a_diag_stamps(uint64_t * host, int64_t n) {
+    n = n < (int64_t) (sizeof(g_q2a_stamps) / 8) ? n : (int64_t) (sizeof(g_q2a_stamps) / 8);
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_q2a_stamps), (size_t) n * 8, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -3;
+}
+extern "C" int q2a_diag_stamps_clear(void) {
+    static uint64_t z[16384 * 2 * Q2A_STAMP_SLOTS];
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_q2a_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -3;
+}
+#endif

@@ -17,8 +17,11 @@ enum q2a_epi {
     Q2A_EPI_STORE_F = 5,    // outF[m][n] = acc                                   (unit tests)
     Q2A_EPI_GELU_Q8K = 6,   // gelu_lut(acc + bias) quantized to Q8_K in-tile: codes -> outH, d -> dy, bsums -> aext
                             // (fc1 on the Q4_K path; needs the 256-column tile = one Q8_K block per row)
-    Q2A_EPI_PRE_H = 7,      // outH[m][n] = x <= -10 ? -inf : fp16(x), x = acc + bias[n]: the fc1 pre-activation,
-                            // whose GELU (the fp16 LUT) the Q8_K quantizer applies (q2a_launch_gelu_quant_q8k)
+    Q2A_EPI_PRE_H = 7,      // outH[m][n] = fp16(acc + bias[n]): the fc1 pre-activation, whose GELU (the fp16 LUT)
+                            // the Q8_K quantizer applies (q2a_launch_gelu_quant_q8k). ggml's x <= -10 branch (+0) needs
+                            // no marker: for every fp16 h <= -10 the table holds -0 (tanhf saturates: 0.5 h (1 - 1)),
+                            // or +0 (the patched -inf entry), and Q8_K turns +0 and -0 into the same code 0 (|x| for
+                            // the block max, nearest_int(-0) = 0), so the fc2 operand is bit-identical
 };
 
 // compact GELU table: entries for fp16 bits 0x0000..0x4900 (+0..+10) then 0x8000..0xC900 (-0..-10), padded to
