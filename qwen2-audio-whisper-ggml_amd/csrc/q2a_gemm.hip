@@ -63,9 +63,16 @@ __device__ __forceinline__ void q2a_st(const V & v, V * ptr) {
 #ifndef Q2A_GEMM_STAGED_EPI
 #define Q2A_GEMM_STAGED_EPI 1
 #endif
-// 8-phase kernel: waves 4-7 one barrier behind waves 0-3 (0 = lockstep halves)
+// fc1 (Q4_K pre-activation) on persistent 8-phase tiles whose epilogue stores retire under the next tile (0 = one tile
+// per workgroup)
+#ifndef Q2A_GEMM_PERSIST
+#define Q2A_GEMM_PERSIST 0
+#endif
+// 8-phase kernel: waves 4-7 one barrier behind waves 0-3 (0 = lockstep halves, a diagnostic build). Round 4, same box
+// (diag/gpurun_r04b.sh): fc1 tile 98.0k -> 82.4k shader cycles (main loop 84.2k -> 68.8k), whole step 238.6 / 242.9 ->
+// 229.2 / 227.9 ms, every weight GEMM 4-7 % faster
 #ifndef Q2A_GEMM_WSTAGGER
-#define Q2A_GEMM_WSTAGGER 0
+#define Q2A_GEMM_WSTAGGER 1
 #endif
 
 // Timing diagnostic Q2A_DIAG_STAMPS=<epi>: the 8-phase kernels of epilogue <epi> record s_memtime at fixed points of
@@ -228,23 +235,41 @@ constexpr int SBUF_OFF = 8 * 128 * ROWB;     // 128 KiB: scale staging after the
 constexpr int SBUF_BYTES = 25 * 1024;       // 21 pieces of 1 KiB (+3 pad slots for the uniform 3 glds per thread)
 constexpr int ALPHA_OFF = 24 * 1024;        //   + alpha = dy_{b-1}/dy_b per tile row (1 KiB), computed a block ahead
 
-template <int BLK, bool LUT, bool BF, bool ST = false>
+// PERS = 1: the persistent form (k_gemm<..., PIPE = 2>): the workgroup walks a sequence of tiles (next(m0, n0) gives the
+// next one, false at the end) and runs the K-step pipeline ACROSS tile boundaries — the last block's tail stages load
+// the next tile's first two K-steps and its phase-2 scale pieces the next tile's block-0 scales, while the finishing
+// tile's final-multiply and bias operands go to a separate 3 KiB area (FIN_OFF) — then calls epi(m0, n0) for the
+// finished tile, whose global stores (S_EPI per wave) retire under the next tile's first five phases: their counted
+// vmcnt waits are raised by S_EPI, so nothing drains between tiles.
+constexpr int FIN_OFF = SBUF_OFF + 21 * 1024;   // dy_last | dx_last | bias of the finishing tile (persistent form): the
+                                                //   three pad pieces' slots, which every other block fills with dummies
+constexpr int S_EPI = 16;                        // global stores per wave of the persistent epilogue
+struct no_tiles {
+    __device__ bool operator()(int &, int &) const { return false; }
+};
+struct no_epi {
+    __device__ void operator()(f4 (&)[8][4], int, int) const {}
+};
+template <int BLK, bool LUT, bool BF, bool ST = false, int PERS = 0, class NEXT = no_tiles, class EPIF = no_epi>
 __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&acc)[8][4], char * lds_raw, int m0, int n0,
-                                                int lane, int wave, int wm, int wn) {
+                                                int lane, int wave, int wm, int wn, NEXT next = NEXT{}, EPIF epi = EPIF{}) {
     constexpr int HT = 128 * ROWB;                        // one half-tile image (16 KiB)
     // per-lane element offsets of this thread's two glds rows in each image (image row ir = i*64 + wave*8 + lane/8)
     uint32_t aoff[2][2], woff[2][2];
+    auto set_offsets = [&](int tm0, int tn0) {
 #pragma unroll
-    for (int x = 0; x < 2; ++x)
+        for (int x = 0; x < 2; ++x)
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int ir = i * 64 + wave * 8 + (lane >> 3);
-            const int sw = ((lane & 7) ^ (ir & 7)) << 3;
-            const int am = m0 + (ir >> 6) * 128 + x * 64 + (ir & 63);
-            aoff[x][i] = (uint32_t) (a_row_off(p, min(am, p.M - 1)) + sw);
-            const int wr = n0 + (ir >> 5) * 64 + x * 32 + (ir & 31);
-            woff[x][i] = (uint32_t) ((int64_t) wr * p.ldw + sw);
-        }
+            for (int i = 0; i < 2; ++i) {
+                const int ir = i * 64 + wave * 8 + (lane >> 3);
+                const int sw = ((lane & 7) ^ (ir & 7)) << 3;
+                const int am = tm0 + (ir >> 6) * 128 + x * 64 + (ir & 63);
+                aoff[x][i] = (uint32_t) (a_row_off(p, min(am, p.M - 1)) + sw);
+                const int wr = tn0 + (ir >> 5) * 64 + x * 32 + (ir & 31);
+                woff[x][i] = (uint32_t) ((int64_t) wr * p.ldw + sw);
+            }
+    };
+    set_offsets(m0, n0);
     const int nk = p.K / BK;
     // image h of buffer b: h = 0 A_q0, 1 A_q1, 2 B_q0, 3 B_q1
     auto stage = [&](int b, int h, int kt) {
@@ -280,18 +305,68 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     char * sbuf = lds_raw + SBUF_OFF;
     // this wave's three pieces: wave-uniform base/stride per piece (SGPRs), picked once
     const char * sb_base[3];
-    int64_t sb_stride[3];
+    int sb_stride[3];
     bool sb_prev[3];
+    auto set_scale_bases = [&](int tm0, int tn0) {
 #pragma unroll
-    for (int u = 0; u < 3; ++u) {
-        const int pc = wave * 3 + u;
-        sb_prev[u] = pc == 0;
-        if (pc <= 1 || pc >= 21) { sb_base[u] = (const char *) (p.dy + m0); sb_stride[u] = (int64_t) p.dy_ld * 4; }
-        else if (pc == 2) { sb_base[u] = (const char *) (p.beta + n0); sb_stride[u] = (int64_t) p.N * 4; }
-        else if (pc == 3) { sb_base[u] = (const char *) (p.gamma + n0); sb_stride[u] = (int64_t) p.N * 4; }
-        else if (pc == 4) { sb_base[u] = (const char *) (p.dx + n0); sb_stride[u] = (int64_t) p.N * 4; }
-        else if (pc < 13) { sb_base[u] = (const char *) (p.aext + (int64_t) m0 * 16) + (pc - 5) * 1024; sb_stride[u] = (int64_t) p.dy_ld * 32; }
-        else { sb_base[u] = (const char *) (p.wext + (int64_t) n0 * 16) + (pc - 13) * 1024; sb_stride[u] = (int64_t) p.N * 32; }
+        for (int u = 0; u < 3; ++u) {
+            const int pc = wave * 3 + u;
+            sb_prev[u] = pc == 0;
+            if (pc <= 1 || pc >= 21) { sb_base[u] = (const char *) (p.dy + tm0); sb_stride[u] = p.dy_ld * 4; }
+            else if (pc == 2) { sb_base[u] = (const char *) (p.beta + tn0); sb_stride[u] = p.N * 4; }
+            else if (pc == 3) { sb_base[u] = (const char *) (p.gamma + tn0); sb_stride[u] = p.N * 4; }
+            else if (pc == 4) { sb_base[u] = (const char *) (p.dx + tn0); sb_stride[u] = p.N * 4; }
+            else if (pc < 13) { sb_base[u] = (const char *) (p.aext + (int64_t) tm0 * 16) + (pc - 5) * 1024; sb_stride[u] = p.dy_ld * 32; }
+            else { sb_base[u] = (const char *) (p.wext + (int64_t) tn0 * 16) + (pc - 13) * 1024; sb_stride[u] = p.N * 32; }
+        }
+    };
+    // persistent form: every piece's source as a descriptor in LDS (base at tile (0, 0) | bytes per m0 | per n0 | per
+    // block), written once; the tile switch then reads 3 of them instead of keeping the six scale-array pointers live
+    // in SGPRs across the loop (past 106 SGPRs the compiler spills into VGPRs). Descriptor u + 3 of a wave is its
+    // pad piece's final-multiply source (dy_last | dx_last | bias of the finishing tile; pads: waves 7's three pieces)
+    constexpr int DESC_OFF = SBUF_OFF + SBUF_BYTES + 512;
+    const uint32_t desc0 = (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) char *) lds_raw + DESC_OFF + wave * 192;
+    if constexpr (PERS) {
+        if (lane == 0) {
+            const int nkb = p.K / 256;
+#pragma unroll
+            for (int u = 0; u < 6; ++u) {
+                const int pc = wave * 3 + (u % 3);
+                const char * b0;
+                int mc = 0, nc = 0, ks;
+                if (u >= 3 && pc >= 21) {
+                    if (pc == 21) { b0 = (const char *) (p.dy + (int64_t) (nkb - 1) * p.dy_ld); mc = 4; }
+                    else if (pc == 22) { b0 = (const char *) (p.dx + (int64_t) (nkb - 1) * p.N); nc = 4; }
+                    else { b0 = (const char *) p.bias; nc = 4; }
+                    ks = 0;
+                } else if (pc <= 1 || pc >= 21) { b0 = (const char *) p.dy; mc = 4; ks = p.dy_ld * 4; }
+                else if (pc == 2) { b0 = (const char *) p.beta; nc = 4; ks = p.N * 4; }
+                else if (pc == 3) { b0 = (const char *) p.gamma; nc = 4; ks = p.N * 4; }
+                else if (pc == 4) { b0 = (const char *) p.dx; nc = 4; ks = p.N * 4; }
+                else if (pc < 13) { b0 = (const char *) p.aext + (pc - 5) * 1024; mc = 32; ks = p.dy_ld * 32; }
+                else { b0 = (const char *) p.wext + (pc - 13) * 1024; nc = 32; ks = p.N * 32; }
+                int * d = (int *) (lds_raw + DESC_OFF + wave * 192 + u * 32);
+                *(const char **) d = b0;
+                d[2] = mc; d[3] = nc; d[4] = ks;
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+    // a descriptor's source for tile (tm0, tn0): base (SGPRs) and per-block stride
+    auto desc_src = [&](int u, int tm0, int tn0, const char *& base, int & ks) {
+        uint32_t v[8];
+        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
+                     : "=v"(*(uint4 *) &v[0]), "=v"(*(uint4 *) &v[4]) : "v"(desc0 + u * 32) : "memory");
+        const uint64_t b = ((uint64_t) __builtin_amdgcn_readfirstlane(v[1]) << 32) | __builtin_amdgcn_readfirstlane(v[0]);
+        const int mc = __builtin_amdgcn_readfirstlane(v[2]), nc = __builtin_amdgcn_readfirstlane(v[3]);
+        ks = __builtin_amdgcn_readfirstlane(v[4]);
+        base = (const char *) (b + (uint64_t) ((int64_t) tm0 * mc + (int64_t) tn0 * nc));
+    };
+    if constexpr (PERS) {
+#pragma unroll
+        for (int u = 0; u < 3; ++u) desc_src(u, m0, n0, sb_base[u], sb_stride[u]);
+    } else {
+        set_scale_bases(m0, n0);
     }
     auto stage_scales = [&](int kb) {
         kb = min(kb, p.K / 256 - 1);
@@ -300,8 +375,32 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #pragma unroll
         for (int u = 0; u < 3; ++u) {
             const int k = sb_prev[u] ? max(kb - 1, 0) : kb;
-            const char * src = sb_base[u] + k * sb_stride[u] + l16;
+            const char * src = sb_base[u] + (int64_t) (k * sb_stride[u]) + l16;
             __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (sbuf + (wave * 3 + u) * 1024), 16, 0, 0);
+        }
+    };
+    // persistent form, phase 2 of a tile's last block: the three pad pieces (wave 7) carry the finishing tile's
+    // dy_last, dx_last and bias into FIN_OFF; the 21 real pieces carry the next tile's block-0 scales (or, for the
+    // workgroup's last tile, the current block again) — same 3 glds per wave as every block
+    auto stage_scales_last = [&](bool has_next, int tm0, int tn0) {
+        const int nkb = p.K / 256;
+        uint32_t l16 = lane * 16;
+        asm volatile("" : "+v"(l16));
+        const int kb = has_next ? 0 : nkb - 1;
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int pc = wave * 3 + u;
+            const char * src;
+            if (pc >= 21) {   // the finishing tile's final-multiply / bias operands
+                const char * fb;
+                int fks;
+                desc_src(u + 3, m0, n0, fb, fks);
+                src = fb + l16;
+            } else {
+                if (has_next) desc_src(u, tm0, tn0, sb_base[u], sb_stride[u]);
+                src = sb_base[u] + (int64_t) ((sb_prev[u] ? max(kb - 1, 0) : kb) * sb_stride[u]) + l16;
+            }
+            __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (sbuf + pc * 1024), 16, 0, 0);
         }
     };
     // start of block kb: acc <- acc * alpha[m] * beta[n] + ngamma[n] * S2[m][n]
@@ -372,6 +471,33 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #endif
             }
         };
+        if constexpr (PERS) {
+            // register-lean form (the persistent kernel carries more state): min-term MFMAs one 16x16 block ahead
+            // instead of one row block ahead (8 instead of 32 VGPRs of results); the same operations on every value
+            f4 s2r[2];
+            s2r[0] = __builtin_amdgcn_mfma_f32_16x16x16f16(we[0], ae[0], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                if (i + 2 < 8) {
+                    asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(al[(i + 2) % 3]) : "v"(s_al), "i"((i + 2) * 64));
+                    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(ae[(i + 2) % 3]) : "v"(s_ae), "i"((i + 2) * 512));
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int c = (i * 4 + j) & 1;
+                    if (j + 1 < 4) s2r[c ^ 1] = __builtin_amdgcn_mfma_f32_16x16x16f16(we[j + 1], ae[i % 3], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+                    else if (i + 1 < 8) s2r[c ^ 1] = __builtin_amdgcn_mfma_f32_16x16x16f16(we[0], ae[(i + 1) % 3], f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        if constexpr (decltype(first)::value) kq_first2(acc[i][j], h, gam[j], s2r[c]);
+                        else kq_rescale2(acc[i][j], h, al[i % 3], bet[j], gam[j], s2r[c]);
+                    }
+                }
+                if (i + 2 < 8) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(al[(i + 2) % 3]), "+v"(ae[(i + 2) % 3]));
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            return;
+        }
         f4 s2v[2][4];
         minterm(s2v[0], ae[0]);
 #pragma unroll
@@ -485,6 +611,61 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
         }
         Q2A_KSTEP(0, stage(1, 1, kt + 1), stage_tail(0, 0), stage_tail(0, 2), stage_tail(0, 3), 10, 10, 10, 10);
         Q2A_KSTEP(1, stage_tail(0, 1), stage_tail(1, 0), stage_tail(1, 2), stage_tail(1, 3), 10, 10, 10, 10);
+    } else if constexpr (PERS) {
+        static_assert(BLK == 256, "persistent 8-phase loop: Q4_K only");
+        // every tile's block 0 runs with its first five waits raised by S_EPI (the previous tile's epilogue stores sit
+        // between its phase 0 and phase 1); for the first tile nothing is there, so the prologue drains its loads
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        alpha_compute();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        stagger_in();
+        for (;;) {
+            int m0n = 0, n0n = 0;
+            const bool has_next = next(m0n, n0n);
+            // the next tile's first K-steps (tail stages), or a harmless re-load of this tile's last one
+            auto stage_next = [&](int b, int h) { stage(b, h, has_next ? b : nk - 1); };
+            int kt = 0;
+            BS_T0();
+            block_start(std::true_type{});
+            BS_T1();
+            asm volatile("" ::: "memory");
+            Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
+                      stage(0, 3, kt + 2), 26, 29, 29, 29);
+            Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 29, 13, 10, 10);
+            Q2A_KSTEP(0, (alpha_compute(), stage(1, 1, kt + 3)), stage(0, 0, kt + 4), stage(0, 2, kt + 4), stage(0, 3, kt + 4),
+                      10, 10, 10, 10);
+            Q2A_KSTEP(1, stage(0, 1, kt + 4), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5), 10, 10, 10, 10);
+            for (kt = 4; kt < nk - 4; kt += 4) {
+                BS_T0();
+                block_start(std::false_type{});
+                BS_T1();
+                asm volatile("" ::: "memory");
+                Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
+                          stage(0, 3, kt + 2), 10, 13, 13, 13);
+                Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 13, 13, 10, 10);
+                Q2A_KSTEP(0, (alpha_compute(), stage(1, 1, kt + 3)), stage(0, 0, kt + 4), stage(0, 2, kt + 4), stage(0, 3, kt + 4),
+                          10, 10, 10, 10);
+                Q2A_KSTEP(1, stage(0, 1, kt + 4), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5), 10, 10, 10, 10);
+            }
+            BS_T0();
+            block_start(std::false_type{});   // (nk >= 8: the last block is never block 0)
+            BS_T1();
+            asm volatile("" ::: "memory");
+            Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales_last(has_next, m0n, n0n)), stage(0, 2, kt + 2),
+                      stage(0, 3, kt + 2), 10, 13, 13, 13);
+            Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 13, 13, 10, 10);
+            Q2A_KSTEP(0, stage(1, 1, kt + 3), ((has_next ? set_offsets(m0n, n0n) : (void) 0), stage_next(0, 0)), stage_next(0, 2),
+                      stage_next(0, 3), 10, 10, 10, 10);
+            Q2A_KSTEP(1, stage_next(0, 1), stage_next(1, 0), stage_next(1, 2), stage_next(1, 3), 10, 10, 10, 10);
+            __builtin_amdgcn_sched_barrier(0);
+            epi(acc, m0, n0);
+            __builtin_amdgcn_sched_barrier(0);   // the finished tile's values die before the next tile's block 0 starts
+            if (!has_next) break;
+            m0 = m0n;
+            n0 = n0n;
+        }
     } else {
         static_assert(BLK == 256, "8-phase k-quant loop is Q4_K only");
         alpha_compute();                                     // block 0 (alpha = 1: acc is 0 anyway)
@@ -531,6 +712,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // tail re-loads still land in LDS: drain before the epilogue
     __syncthreads();
+    if constexpr (PERS) return;                          // (every tile's epilogue already ran inside the loop)
     if constexpr (BLK == 256) {
         // acc is in units of the last block's scale: multiply by dy_last[m] * dx_last[n]
 #pragma unroll
@@ -600,7 +782,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     constexpr int NS = PIPE || BLK == 32 || BM > 64 ? 2 : (NS_FIT >= NS_MAX ? NS_MAX : NS_FIT >= 2 ? NS_FIT : 2);
     static_assert(PIPE || BLK != 256 || SP + NS <= 6, "Q4_K scale prefetch distance");
     static_assert(NBUF == 2 || (NS == 2 && SP <= 3), "single Q4_K scale buffer: pieces on steps 4b+1 .. 4b+3");
-    constexpr int LDS_MAIN = PIPE ? (BLK ? SBUF_OFF + SBUF_BYTES : 2 * OPB) : NS * OPB + SCALE_LDS;
+    constexpr int LDS_MAIN = PIPE == 2 ? SBUF_OFF + SBUF_BYTES + 512 + 8 * 192 : PIPE ? (BLK ? SBUF_OFF + SBUF_BYTES : 2 * OPB) : NS * OPB + SCALE_LDS;
     constexpr int LDS_BYTES = LDS_MAIN > EPI_OFF + NW * EPI_WREG ? LDS_MAIN : EPI_OFF + NW * EPI_WREG;
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
     __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES];
@@ -642,7 +824,97 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (PIPE == 1) {
+    if constexpr (PIPE == 2) {
+        // persistent 8-phase tiles (launch_pipe8: fc1's pre-activation, M a multiple of 256, K >= 512): virtual
+        // workgroup ids v = blockIdx.x + r * gridDim.x mapped exactly like the one-tile-per-workgroup grid (gridDim is
+        // a multiple of 8, so v and blockIdx.x share an XCD), the pipeline runs across the tiles (mainloop_8phase PERS)
+        static_assert(EPI == Q2A_EPI_PRE_H && BLK == 256 && BM == 256 && BN == 256 && NW == 8, "persistent form: fc1 Q4_K");
+        auto tile_at = [&](int v, int & tm0, int & tn0) {
+            const int x8 = v & 7;
+            const int w = (x8 < rr ? x8 * (qq + 1) : rr * (qq + 1) + (x8 - rr) * qq) + (v >> 3);
+            const int g2 = w / gsize, gr2 = w % gsize, gm2 = min(GM, nbm - g2 * GM);
+            tm0 = p.m_base + (g2 * GM + gr2 % gm2) * BM;
+            tn0 = (gr2 / gm2) * BN;
+        };
+        // the workgroup's tile list (m0 | n0 per entry) in LDS behind the final-multiply area: the loop then carries
+        // one counter instead of the raster's constants (SGPR pressure: past 106 the compiler spills)
+        int * tlist = (int *) (lds_raw + SBUF_OFF + SBUF_BYTES);
+        const int ntw = (ntl - bid + (int) gridDim.x - 1) / (int) gridDim.x;   // tiles of this workgroup (>= 1)
+        for (int r = tid; r < ntw; r += NT) {
+            int a0, b0;
+            tile_at(bid + r * (int) gridDim.x, a0, b0);
+            tlist[2 * r] = a0;
+            tlist[2 * r + 1] = b0;
+        }
+        __syncthreads();
+        const uint32_t tl0 = (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) char *) lds_raw + SBUF_OFF + SBUF_BYTES;
+        int rcur = 0;
+        auto next = [&](int & tm0, int & tn0) -> bool {
+            if (rcur + 1 >= ntw) return false;
+            ++rcur;
+            int2 v;
+            asm volatile("ds_read_b64 %0, %1\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(tl0 + rcur * 8) : "memory");
+            tm0 = __builtin_amdgcn_readfirstlane(v.x);
+            tn0 = __builtin_amdgcn_readfirstlane(v.y);
+            return true;
+        };
+        const uint32_t fin = (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) char *) lds_raw + FIN_OFF;
+        // the finished tile: acc * (dy_last[m] * dx_last[n]) + bias[n] -> fp16 (the PIPE = 1 epilogue's operations,
+        // bit for bit), 16 B per lane after one lane exchange, straight from registers: S_EPI stores per wave
+        auto epi = [&](f4 (&ac)[8][4], int tm0, int tn0) {
+            const int ln = (int) __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));   // lane, rematerialised
+            const int q = ln >> 4, l16 = ln & 15;
+            const int pcol = 16 * (q & 1) + 8 * (q >> 1);
+            f4 dx4[4], b4[4];
+            float yc[8];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t c = fin + (wn * 64 + j * 16 + q * 4) * 4;
+                asm volatile("ds_read_b128 %0, %1 offset:1024" : "=v"(dx4[j]) : "v"(c));
+                asm volatile("ds_read_b128 %0, %1 offset:2048" : "=v"(b4[j]) : "v"(c));
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                asm volatile("ds_read_b32 %0, %1" : "=v"(yc[i]) : "v"(fin + (wm * 128 + i * 16 + l16) * 4));
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(dx4[0]), "+v"(dx4[1]), "+v"(dx4[2]), "+v"(dx4[3]), "+v"(b4[0]),
+                         "+v"(b4[1]), "+v"(b4[2]), "+v"(b4[3]), "+v"(yc[0]), "+v"(yc[1]), "+v"(yc[2]), "+v"(yc[3]),
+                         "+v"(yc[4]), "+v"(yc[5]), "+v"(yc[6]), "+v"(yc[7]));
+            typedef _Float16 h4p __attribute__((ext_vector_type(4)));
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                q2a_half * orow = p.outH + (int64_t) (tm0 + wm * 128 + i * 16 + l16) * p.ldo + tn0 + wn * 64 + pcol;
+#pragma unroll
+                for (int jp = 0; jp < 2; ++jp) {
+                    h4p ha, hb;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+#pragma clang fp contract(off)
+                        const float va = kq_final(ac[i][2 * jp][r], yc[i], dx4[2 * jp][r]) + b4[2 * jp][r];
+                        const float vb = kq_final(ac[i][2 * jp + 1][r], yc[i], dx4[2 * jp + 1][r]) + b4[2 * jp + 1][r];
+                        ha[r] = (_Float16) va;
+                        hb[r] = (_Float16) vb;
+                    }
+                    uint2 ua, ub;
+                    __builtin_memcpy(&ua, &ha, 8);
+                    __builtin_memcpy(&ub, &hb, 8);
+                    const bool odd = q & 1;
+                    const uint2 send = odd ? ua : ub;
+                    uint2 recv;
+                    recv.x = __shfl_xor(send.x, 16, 64);
+                    recv.y = __shfl_xor(send.y, 16, 64);
+                    const uint4 hv = odd ? make_uint4(recv.x, recv.y, ub.x, ub.y) : make_uint4(ua.x, ua.y, recv.x, recv.y);
+                    if (Q2A_ST) q2a_st(hv, (uint4 *) (orow + 32 * jp));
+                }
+            }
+            // (no reset: the next tile's block-0 start writes every accumulator, kq_first2)
+        };
+        Q2A_STAMP(ST, 0);
+        Q2A_STAMP_RT(ST, 8);
+        mainloop_8phase<BLK, false, false, ST, 1>(p, acc, lds_raw, m0, n0, lane, wave, wm, wn, next, epi);
+        Q2A_STAMP(ST, 6);
+        Q2A_STAMP_RT(ST, 9);
+        return;
+    } else if constexpr (PIPE == 1) {
         Q2A_STAMP(ST, 0);
         Q2A_STAMP_RT(ST, 8);
         mainloop_8phase<BLK, LUT_EPI, BF, ST>(p, acc, lds_raw, m0, n0, lane, wave, wm, wn);
@@ -1538,6 +1810,16 @@ int cu_count() {
 // than the second launch and the 128x128 tiles' lower rate.
 template <int EPI, int BLK>
 hipError_t launch_pipe8(const q2a_gemm_args & a, hipStream_t s) {
+    if constexpr (Q2A_GEMM_PERSIST && EPI == Q2A_EPI_PRE_H && BLK == 256) {
+        // persistent tiles (k_gemm PIPE = 2): whole 256-row tiles only, at least two Q4_K blocks
+        const int cus = cu_count();
+        const int ntl = (a.N / 256) * ((a.M - a.m_base) / 256);
+        if ((a.M - a.m_base) % 256 == 0 && a.K >= 512 && ntl > 0 && cus >= 8) {
+            const int grid = std::min(ntl, cus / 8 * 8);
+            hipLaunchKernelGGL((k_gemm<256, 256, 2, 4, EPI, BLK, 2>), dim3(grid), dim3(512), 0, s, a);
+            return hipGetLastError();
+        }
+    }
     constexpr bool TAILABLE = Q2A_GEMM_TAIL && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_PRE_H || EPI == Q2A_EPI_GELU_H);
     if constexpr (TAILABLE) {
         const int cus = cu_count();

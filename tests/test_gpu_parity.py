@@ -116,6 +116,7 @@ def test_attention_propagates_nan(engines):
 
     def run(q, k, v):
         out = torch.empty_like(q)
+        torch.cuda.synchronize()   # q / k / v were written on torch's stream; the engine runs on its own
         e.test_attention(q.data_ptr(), k.data_ptr(), v.data_ptr(), B, out.data_ptr())
         torch.cuda.synchronize()
         return out.cpu()
@@ -243,6 +244,7 @@ def test_compact_blob_expands_to_the_host_pack_bytes(make_model, cfg, wt, act):
         assert len(comp) <= 0.4e9 and len(full) > 1.3e9
     cd = torch.frombuffer(comp, dtype=torch.uint8).cuda()
     out = torch.full((len(full),), 0xA5, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
     q2a.expand_blob(cd.data_ptr(), len(comp), out.data_ptr(), len(full), 0)
     torch.cuda.synchronize()
     want = torch.frombuffer(full, dtype=torch.uint8).cuda()
@@ -331,6 +333,7 @@ def test_linear_full_size_bench_shape_matches_oracle(engines, make_model, wt, wh
     g = torch.Generator(device="cuda").manual_seed(200 + which)
     xd = torch.randn((M, K), device="cuda", generator=g) * (1.0 if which != 3 else 0.3)
     yd = torch.empty((M, N), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()   # x comes from torch's stream; the engine runs on its own (non-blocking) stream
     e.test_linear(7, which, xd.data_ptr(), M, yd.data_ptr())
     torch.cuda.synchronize()
     rows = np.unique(np.concatenate([np.random.default_rng(which).choice(M, 352, replace=False),
