@@ -202,11 +202,13 @@ def host_cpu_info() -> dict:
 
 def fc1_kernel_label(wt: str, bf16: bool, M: int) -> str:
     """The k_gemm instantiation the engine launches for fc1 (N = 5120, K = 1280), mirroring q2a_gemm.hip's tile
-    regimes: 256x256 8-phase tiles once ceil(M/256) x 20 tiles >= 512 (M >= 6401), else 128x128 two-stage tiles."""
+    regimes: 256x256 8-phase tiles once ceil(M/256) x 20 tiles >= 512 (M >= 6401), persistent (PIPE 2) for the Q4_K
+    pre-activation at whole 256-row tiles, else 128x128 two-stage tiles."""
     epi = "GELU_H" if (bf16 or wt != "q4_k") else "PRE_H"
     blk = "BF16" if bf16 else {"q4_k": "256", "f16": "0", "q8_0": "32"}[wt]
     if (M + 255) // 256 * 20 >= 512 and blk != "32":
-        return f"k_gemm<256,256,2,4,{epi},{blk},1>"
+        pipe = 2 if (epi == "PRE_H" and M % 256 == 0) else 1
+        return f"k_gemm<256,256,2,4,{epi},{blk},{pipe}>"
     if (M + 255) // 256 * 20 >= 512:
         return f"k_gemm<128,256,2,4,{epi},{blk},0>"
     return f"k_gemm<128,128,2,2,{epi},{blk},0>"

@@ -9,7 +9,10 @@
 // (lib/libggml-q2a.so). Unlike ref_harness.cpp there is NO conv shim: the graph's MUL_MAT(F32 im2col, F16 kernel)
 // runs on the backend as built.
 //
-//   ggml_harness encode MODEL PCM OUT [reps] [device]   -> embd_enc f32 [750][1280] to OUT, JSON line on stdout
+//   ggml_harness encode MODEL PCM OUT [reps] [device] [dumpdir] [ndump] [skip_lo-skip_hi]
+//                                                       -> embd_enc f32 [750][1280] to OUT, JSON line on stdout; with
+//                                                          dumpdir, the first ndump encoder-graph node outputs of the
+//                                                          first call (per-node comparison with ref_harness's dumps)
 //   ggml_harness graphs [device]                        -> HIP-graph capture vs scratch growth check, JSON line
 
 #define GGML_USE_CUDA
@@ -41,8 +44,41 @@ std::vector<float> read_f32(const char * path) {
     return v;
 }
 
+// first `limit` node outputs of the encoder graph through the sched eval callback (ggml-backend.cpp:2306), the same
+// node numbering and file names as ref_harness's dumps. The sched stops after each observed node, so observed nodes
+// run unfused (the fusion tests show fused == per-node bit for bit); nodes in [skip_lo, skip_hi] are not observed,
+// so a span such as the attention chain still reaches the backend in one piece (its fused kernel)
+struct dump_state {
+    std::string dir;
+    int asked = 0;      // nodes the sched has asked about (its asks come once per node, in graph order)
+    int limit = 0;
+    int skip_lo = -1, skip_hi = -1;
+    FILE * index = nullptr;
+};
+
+bool dump_cb(struct ggml_tensor * t, bool ask, void * ud) {
+    dump_state * ds = (dump_state *) ud;
+    if (ask) {
+        const int n = ds->asked++;
+        return n < ds->limit && !(n >= ds->skip_lo && n <= ds->skip_hi);
+    }
+    const int n = ds->asked - 1;
+    if (t->type == GGML_TYPE_F32 && ggml_is_contiguous(t)) {
+        std::vector<float> buf(ggml_nelements(t));
+        ggml_backend_tensor_get(t, buf.data(), 0, ggml_nbytes(t));
+        char name[64];
+        snprintf(name, sizeof(name), "node%03d_%s.f32", n, ggml_op_desc(t));
+        FILE * f = fopen((ds->dir + "/" + name).c_str(), "wb");
+        fwrite(buf.data(), 1, ggml_nbytes(t), f);
+        fclose(f);
+        fprintf(ds->index, "%d %s %lld %lld %lld %lld %s\n", n, ggml_op_desc(t), (long long) t->ne[0],
+                (long long) t->ne[1], (long long) t->ne[2], (long long) t->ne[3], name);
+    }
+    return true;
+}
+
 int cmd_encode(int argc, char ** argv) {
-    if (argc < 5) { fprintf(stderr, "encode MODEL PCM OUT [reps] [device]\n"); return 1; }
+    if (argc < 5) { fprintf(stderr, "encode MODEL PCM OUT [reps] [device] [dumpdir] [ndump] [skip_lo-skip_hi]\n"); return 1; }
     const int reps = argc > 5 ? atoi(argv[5]) : 1;
     whisper_context_params cp = whisper_context_default_params();
     cp.use_gpu = true;
@@ -52,6 +88,14 @@ int cmd_encode(int argc, char ** argv) {
     ggml_backend_t be = ctx->state->backends[0];
     if (!ggml_backend_is_q2a(be)) { fprintf(stderr, "backend 0 is %s, not Q2A\n", ggml_backend_name(be)); return 4; }
     std::vector<float> pcm = read_f32(argv[3]);
+    dump_state ds;
+    if (argc > 7) {
+        ds.dir = argv[7];
+        ds.limit = argc > 8 ? atoi(argv[8]) : 40;
+        if (argc > 9) sscanf(argv[9], "%d-%d", &ds.skip_lo, &ds.skip_hi);
+        ds.index = fopen((ds.dir + "/index.txt").c_str(), "w");
+        ggml_backend_sched_set_eval_callback(ctx->state->sched_encode.sched, dump_cb, &ds);
+    }
     // whisper_full_default_params() has no return statement in the reference (qwen2-whisper.cpp:4231-4295, UB):
     // zero-initialise and set what the path reads
     whisper_full_params p;
@@ -71,6 +115,17 @@ int cmd_encode(int argc, char ** argv) {
         // the reference's own phase clocks (qwen2-whisper.cpp:2335, 2651): CPU log-mel, then conv + encoder graphs
         best_mel = std::min(best_mel, 1e-6 * (double) (ctx->state->t_mel_us - mel0));
         best_enc = std::min(best_enc, 1e-6 * (double) (ctx->state->t_encode_us - enc0));
+        if (r == 0 && ds.index) {
+            ggml_backend_sched_set_eval_callback(ctx->state->sched_encode.sched, nullptr, nullptr);
+            fclose(ds.index);
+            ds.index = nullptr;
+            ggml_tensor * ec = ctx->state->embd_conv;
+            std::vector<float> buf(ggml_nelements(ec));
+            ggml_backend_tensor_get(ec, buf.data(), 0, ggml_nbytes(ec));
+            FILE * f = fopen((ds.dir + "/embd_conv.f32").c_str(), "wb");
+            fwrite(buf.data(), 1, ggml_nbytes(ec), f);
+            fclose(f);
+        }
     }
     ggml_backend_q2a_stats st;
     memset(&st, 0, sizeof(st));

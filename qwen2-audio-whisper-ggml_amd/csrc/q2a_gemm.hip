@@ -64,9 +64,11 @@ __device__ __forceinline__ void q2a_st(const V & v, V * ptr) {
 #define Q2A_GEMM_STAGED_EPI 1
 #endif
 // fc1 (Q4_K pre-activation) on persistent 8-phase tiles whose epilogue stores retire under the next tile (0 = one tile
-// per workgroup)
+// per workgroup, a diagnostic build). Round 4 (diag/gpurun_r04d.sh): fc1 1.268 ms per launch (rocprof) against 1.341
+// one-tile-per-workgroup; same-box bench A/B fc1 39.5 / 40.4 against 41.1 / 40.7 ms per step; outputs bit-identical
+// (64-clip batch-invariance tests)
 #ifndef Q2A_GEMM_PERSIST
-#define Q2A_GEMM_PERSIST 0
+#define Q2A_GEMM_PERSIST 1
 #endif
 // 8-phase kernel: waves 4-7 one barrier behind waves 0-3 (0 = lockstep halves, a diagnostic build). Round 4, same box
 // (diag/gpurun_r04b.sh): fc1 tile 98.0k -> 82.4k shader cycles (main loop 84.2k -> 68.8k), whole step 238.6 / 242.9 ->
@@ -320,54 +322,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             else { sb_base[u] = (const char *) (p.wext + (int64_t) tn0 * 16) + (pc - 13) * 1024; sb_stride[u] = p.N * 32; }
         }
     };
-    // persistent form: every piece's source as a descriptor in LDS (base at tile (0, 0) | bytes per m0 | per n0 | per
-    // block), written once; the tile switch then reads 3 of them instead of keeping the six scale-array pointers live
-    // in SGPRs across the loop (past 106 SGPRs the compiler spills into VGPRs). Descriptor u + 3 of a wave is its
-    // pad piece's final-multiply source (dy_last | dx_last | bias of the finishing tile; pads: waves 7's three pieces)
-    constexpr int DESC_OFF = SBUF_OFF + SBUF_BYTES + 512;
-    const uint32_t desc0 = (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) char *) lds_raw + DESC_OFF + wave * 192;
-    if constexpr (PERS) {
-        if (lane == 0) {
-            const int nkb = p.K / 256;
-#pragma unroll
-            for (int u = 0; u < 6; ++u) {
-                const int pc = wave * 3 + (u % 3);
-                const char * b0;
-                int mc = 0, nc = 0, ks;
-                if (u >= 3 && pc >= 21) {
-                    if (pc == 21) { b0 = (const char *) (p.dy + (int64_t) (nkb - 1) * p.dy_ld); mc = 4; }
-                    else if (pc == 22) { b0 = (const char *) (p.dx + (int64_t) (nkb - 1) * p.N); nc = 4; }
-                    else { b0 = (const char *) p.bias; nc = 4; }
-                    ks = 0;
-                } else if (pc <= 1 || pc >= 21) { b0 = (const char *) p.dy; mc = 4; ks = p.dy_ld * 4; }
-                else if (pc == 2) { b0 = (const char *) p.beta; nc = 4; ks = p.N * 4; }
-                else if (pc == 3) { b0 = (const char *) p.gamma; nc = 4; ks = p.N * 4; }
-                else if (pc == 4) { b0 = (const char *) p.dx; nc = 4; ks = p.N * 4; }
-                else if (pc < 13) { b0 = (const char *) p.aext + (pc - 5) * 1024; mc = 32; ks = p.dy_ld * 32; }
-                else { b0 = (const char *) p.wext + (pc - 13) * 1024; nc = 32; ks = p.N * 32; }
-                int * d = (int *) (lds_raw + DESC_OFF + wave * 192 + u * 32);
-                *(const char **) d = b0;
-                d[2] = mc; d[3] = nc; d[4] = ks;
-            }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    }
-    // a descriptor's source for tile (tm0, tn0): base (SGPRs) and per-block stride
-    auto desc_src = [&](int u, int tm0, int tn0, const char *& base, int & ks) {
-        uint32_t v[8];
-        asm volatile("ds_read_b128 %0, %2\n\tds_read_b128 %1, %2 offset:16\n\ts_waitcnt lgkmcnt(0)"
-                     : "=v"(*(uint4 *) &v[0]), "=v"(*(uint4 *) &v[4]) : "v"(desc0 + u * 32) : "memory");
-        const uint64_t b = ((uint64_t) __builtin_amdgcn_readfirstlane(v[1]) << 32) | __builtin_amdgcn_readfirstlane(v[0]);
-        const int mc = __builtin_amdgcn_readfirstlane(v[2]), nc = __builtin_amdgcn_readfirstlane(v[3]);
-        ks = __builtin_amdgcn_readfirstlane(v[4]);
-        base = (const char *) (b + (uint64_t) ((int64_t) tm0 * mc + (int64_t) tn0 * nc));
-    };
-    if constexpr (PERS) {
-#pragma unroll
-        for (int u = 0; u < 3; ++u) desc_src(u, m0, n0, sb_base[u], sb_stride[u]);
-    } else {
-        set_scale_bases(m0, n0);
-    }
+    set_scale_bases(m0, n0);
     auto stage_scales = [&](int kb) {
         kb = min(kb, p.K / 256 - 1);
         uint32_t l16 = lane * 16;
@@ -382,26 +337,38 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     // persistent form, phase 2 of a tile's last block: the three pad pieces (wave 7) carry the finishing tile's
     // dy_last, dx_last and bias into FIN_OFF; the 21 real pieces carry the next tile's block-0 scales (or, for the
     // workgroup's last tile, the current block again) — same 3 glds per wave as every block
-    auto stage_scales_last = [&](bool has_next, int tm0, int tn0) {
+    // sources of those three glds, worked out in scalar registers before the last block starts (an address formed
+    // inside the K-step would hold VGPRs at the loop's register peak)
+    const char * sl_src[3];
+    auto prep_scales_last = [&](bool has_next, int tm0, int tn0) {
         const int nkb = p.K / 256;
-        uint32_t l16 = lane * 16;
-        asm volatile("" : "+v"(l16));
         const int kb = has_next ? 0 : nkb - 1;
 #pragma unroll
         for (int u = 0; u < 3; ++u) {
             const int pc = wave * 3 + u;
-            const char * src;
             if (pc >= 21) {   // the finishing tile's final-multiply / bias operands
-                const char * fb;
-                int fks;
-                desc_src(u + 3, m0, n0, fb, fks);
-                src = fb + l16;
+                sl_src[u] = pc == 21 ? (const char *) (p.dy + (int64_t) (nkb - 1) * p.dy_ld + m0)
+                          : pc == 22 ? (const char *) (p.dx + (int64_t) (nkb - 1) * p.N + n0)
+                                     : (const char *) (p.bias + n0);
             } else {
-                if (has_next) desc_src(u, tm0, tn0, sb_base[u], sb_stride[u]);
-                src = sb_base[u] + (int64_t) ((sb_prev[u] ? max(kb - 1, 0) : kb) * sb_stride[u]) + l16;
+                // this piece's bytes per tile row / column: the base moves to the next tile in scalar arithmetic
+                // (the current tile's last-block scales were staged one block ago)
+                if (has_next) {
+                    const int mc = pc <= 1 ? 4 : (pc >= 5 && pc < 13) ? 32 : 0;
+                    const int nc = (pc >= 2 && pc <= 4) ? 4 : pc >= 13 ? 32 : 0;
+                    sb_base[u] += (int64_t) (tm0 - m0) * mc + (int64_t) (tn0 - n0) * nc;
+                }
+                sl_src[u] = sb_base[u] + (int64_t) ((sb_prev[u] ? max(kb - 1, 0) : kb) * sb_stride[u]);
             }
-            __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (sbuf + pc * 1024), 16, 0, 0);
+            asm volatile("" : "+s"(sl_src[u]));
         }
+    };
+    auto stage_scales_last = [&]() {
+        uint32_t l16 = lane * 16;
+        asm volatile("" : "+v"(l16));
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+            __builtin_amdgcn_global_load_lds((const void *) (sl_src[u] + l16), (lds_ptr_t) (sbuf + (wave * 3 + u) * 1024), 16, 0, 0);
     };
     // start of block kb: acc <- acc * alpha[m] * beta[n] + ngamma[n] * S2[m][n]
     // LDS reads below go through integer AS3 addresses (no IR link to the glds destination array): hipcc would
@@ -649,11 +616,12 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
                           10, 10, 10, 10);
                 Q2A_KSTEP(1, stage(0, 1, kt + 4), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5), 10, 10, 10, 10);
             }
+            prep_scales_last(has_next, m0n, n0n);
             BS_T0();
             block_start(std::false_type{});   // (nk >= 8: the last block is never block 0)
             BS_T1();
             asm volatile("" ::: "memory");
-            Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales_last(has_next, m0n, n0n)), stage(0, 2, kt + 2),
+            Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales_last()), stage(0, 2, kt + 2),
                       stage(0, 3, kt + 2), 10, 13, 13, 13);
             Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 13, 13, 10, 10);
             Q2A_KSTEP(0, stage(1, 1, kt + 3), ((has_next ? set_offsets(m0n, n0n) : (void) 0), stage_next(0, 0)), stage_next(0, 2),
@@ -782,7 +750,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     constexpr int NS = PIPE || BLK == 32 || BM > 64 ? 2 : (NS_FIT >= NS_MAX ? NS_MAX : NS_FIT >= 2 ? NS_FIT : 2);
     static_assert(PIPE || BLK != 256 || SP + NS <= 6, "Q4_K scale prefetch distance");
     static_assert(NBUF == 2 || (NS == 2 && SP <= 3), "single Q4_K scale buffer: pieces on steps 4b+1 .. 4b+3");
-    constexpr int LDS_MAIN = PIPE == 2 ? SBUF_OFF + SBUF_BYTES + 512 + 8 * 192 : PIPE ? (BLK ? SBUF_OFF + SBUF_BYTES : 2 * OPB) : NS * OPB + SCALE_LDS;
+    constexpr int LDS_MAIN = PIPE == 2 ? SBUF_OFF + SBUF_BYTES + 512 : PIPE ? (BLK ? SBUF_OFF + SBUF_BYTES : 2 * OPB) : NS * OPB + SCALE_LDS;
     constexpr int LDS_BYTES = LDS_MAIN > EPI_OFF + NW * EPI_WREG ? LDS_MAIN : EPI_OFF + NW * EPI_WREG;
     static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
     __shared__ __attribute__((aligned(16))) char lds_raw[LDS_BYTES];
@@ -1814,8 +1782,9 @@ hipError_t launch_pipe8(const q2a_gemm_args & a, hipStream_t s) {
         // persistent tiles (k_gemm PIPE = 2): whole 256-row tiles only, at least two Q4_K blocks
         const int cus = cu_count();
         const int ntl = (a.N / 256) * ((a.M - a.m_base) / 256);
-        if ((a.M - a.m_base) % 256 == 0 && a.K >= 512 && ntl > 0 && cus >= 8) {
-            const int grid = std::min(ntl, cus / 8 * 8);
+        const int grid = std::min(ntl, cus / 8 * 8);
+        // (the workgroup's tile list holds 64 entries)
+        if ((a.M - a.m_base) % 256 == 0 && a.K >= 512 && ntl > 0 && cus >= 8 && ntl <= 64 * grid) {
             hipLaunchKernelGGL((k_gemm<256, 256, 2, 4, EPI, BLK, 2>), dim3(grid), dim3(512), 0, s, a);
             return hipGetLastError();
         }
