@@ -56,8 +56,8 @@ eng = q2a.Engine(model, device=0)
 eo, _ = eng.encode_host([np.fromfile(pcm[c], dtype=np.float32) for c in clips])
 engine = {c: eo[i] for i, c in enumerate(clips)}
 res = {"engine": engine}
-for name, env in [("fused", {}), ("no_fused_attn", {"GGML_Q2A_NO_FUSED_ATTN": "1"}),
-                  ("no_conv_hilo", {"GGML_Q2A_NO_CONV_HILO": "1"}), ("no_fuse", {"GGML_Q2A_NO_FUSE": "1"})]:
+for name, env in [("fused", {}), ("conv_f64", {"GGML_Q2A_CONV_F64": "1"}), ("no_fused_attn", {"GGML_Q2A_NO_FUSED_ATTN": "1"}),
+                  ("no_conv_hilo", {"GGML_Q2A_NO_CONV_HILO": "1"})]:
     res[name] = backend(env)
 for name, out in res.items():
     st = [stats(out[c][rows], ref(c)) for c in clips]

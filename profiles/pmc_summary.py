@@ -23,6 +23,8 @@ def classify(name: str) -> str:
     if not m:
         return name.split("(")[0].strip()[:60]
     epi, blk = int(m.group(5)), int(m.group(6))
+    if blk == 2:   # Q2A_BLK_EXACT: the conv GEMMs (f64-summed K-steps)
+        return "conv2" if epi == 3 else "conv1" if epi == 2 else "conv (ggml backend)"
     if epi == 0:
         return "gemm_qkv"
     if epi == 1:

@@ -1065,9 +1065,39 @@ void run_mm_conv_hilo(q2a_backend_ctx * b, ggml_tensor * op) {
         a.split_stride = (int64_t) M * N;
         a.split_store = 1;
     }
-    Q2A_HIP(q2a_launch_gemm(a, Q2A_EPI_STORE_F, 0, b->stream));
+    Q2A_HIP(q2a_launch_gemm(a, Q2A_EPI_STORE_F, Q2A_BLK_EXACT, b->stream));
     hipLaunchKernelGGL(k_transpose_f32, dim3((unsigned) ((N + 63) / 64), (unsigned) ((M + 63) / 64)), dim3(256), 0, b->stream,
                        (const float *) tmp, (float *) op->data, M, N);
+}
+
+// diagnostic (GGML_Q2A_CONV_F64=1): the conv MUL_MAT(F32 x, F16 w) summed in double, one thread per output, rounded
+// to f32 once — the conv without accumulation error, to measure how much of the path's distance to the reference
+// builds comes from the conv's own summation (diag/backend_tiny_variants.py)
+__global__ void k_conv_f64(const float * x, const _Float16 * w, float * out, int M, int N, int K) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t) M * N) return;
+    const int m = (int) (i % M), n = (int) (i / M);
+    const float * xr = x + (int64_t) m * K;
+    const _Float16 * wr = w + (int64_t) n * K;
+    double acc = 0.0;
+    for (int k = 0; k < K; ++k) acc += (double) xr[k] * (double) (float) wr[k];
+    out[(int64_t) n * M + m] = (float) acc;
+}
+bool conv_f64_diag(const ggml_tensor * op) {
+    static const bool on = [] { const char * v = getenv("GGML_Q2A_CONV_F64"); return v && atoi(v); }();
+    const ggml_tensor * x = op->src[0];
+    const ggml_tensor * w = op->src[1];
+    return on && x->type == GGML_TYPE_F32 && w->type == GGML_TYPE_F16 && op->type == GGML_TYPE_F32 &&
+           ggml_is_contiguous(x) && ggml_is_contiguous(w) && ggml_is_contiguous(op) && x->ne[2] == 1 && x->ne[3] == 1 &&
+           w->ne[2] == 1 && w->ne[3] == 1;
+}
+void run_mm_conv_f64(q2a_backend_ctx * b, ggml_tensor * op) {
+    const ggml_tensor * x = op->src[0];
+    const ggml_tensor * w = op->src[1];
+    const int K = (int) x->ne[0], M = (int) x->ne[1], N = (int) w->ne[1];
+    b->quant_src = nullptr;
+    hipLaunchKernelGGL(k_conv_f64, grid1((int64_t) M * N), dim3(256), 0, b->stream, (const float *) x->data,
+                       (const _Float16 *) w->data, (float *) op->data, M, N, K);
 }
 
 void run_mm_f32(q2a_backend_ctx * b, ggml_tensor * op) {
@@ -1397,6 +1427,7 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                     i += used - 1;
                     break;
                 }
+                if (!mm_fast_ok(op) && conv_f64_diag(op)) { run_mm_conv_f64(b, op); b->stats.n_mul_mat_conv++; break; }
                 if (!mm_fast_ok(op) && conv_hilo_ok(op)) {
                     run_mm_conv_hilo(b, op);
                     b->stats.n_mul_mat_conv++;

@@ -1096,6 +1096,8 @@ int run_frontend(q2a_engine * e, const float * pcm, int64_t stride, int B, int m
     ma.mel = e->mel; ma.clip_max = cmax; ma.xc1 = e->xc1; ma.xc_f32 = e->f32 ? 1 : 0;
     PLAUNCH(e, s, Q2A_PROF_MEL, q2a_launch_mel(ma, s));
     const int P1 = 3, P2 = e->f32 ? 2 : 1;   // operand parts per mel row / per conv1 output row
+    // both convs sum each 64-deep K-step's MFMA partial in f64 (Q2A_BLK_EXACT): within rounding of the exact dot
+    // product, where a plain f32 MFMA chain carried twice the reference builds' own conv error
     {   // conv1: implicit GEMM, A row t = xc1 rows t..t+2 of its clip (3 x P1 x M halves), K = 3 P1 M
         q2a_gemm_args a;
         memset(&a, 0, sizeof(a));
@@ -1107,7 +1109,7 @@ int run_frontend(q2a_engine * e, const float * pcm, int64_t stride, int B, int m
         a.o_dup = e->f32 ? d.D : 0;
         a.gelu_tab = e->g<const uint16_t *>(G_GELU);
         a.gelu_c = e->g<const uint16_t *>(G_GELU_C);
-        PLAUNCH(e, s, Q2A_PROF_CONV1, q2a_launch_gemm(a, Q2A_EPI_GELU_H, 0, s));
+        PLAUNCH(e, s, Q2A_PROF_CONV1, q2a_launch_gemm(a, Q2A_EPI_GELU_H, Q2A_BLK_EXACT, s));
     }
     {   // conv2 (stride 2): A row t = y1 rows 2t..2t+2 (inputs 2t-1..2t+1), K = 3D; + pe
         q2a_gemm_args a;
@@ -1119,7 +1121,7 @@ int run_frontend(q2a_engine * e, const float * pcm, int64_t stride, int B, int m
         a.outF = e->X; a.ldo = d.D; a.pe = e->g<const float *>(G_PE); a.T = d.T;
         a.gelu_tab = e->g<const uint16_t *>(G_GELU);
         a.gelu_c = e->g<const uint16_t *>(G_GELU_C);
-        PLAUNCH(e, s, Q2A_PROF_CONV2, q2a_launch_gemm(a, Q2A_EPI_CONV2, 0, s));
+        PLAUNCH(e, s, Q2A_PROF_CONV2, q2a_launch_gemm(a, Q2A_EPI_CONV2, Q2A_BLK_EXACT, s));
     }
     return Q2A_OK;
 }

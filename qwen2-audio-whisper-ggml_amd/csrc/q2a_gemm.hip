@@ -705,7 +705,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
 #else
     constexpr bool ST = false;
 #endif
-    constexpr int BLK = BF ? 0 : BLK_;
+    constexpr bool EX = BLK_ == Q2A_BLK_EXACT;             // fp16 operands, f64 sum of per-K-step partials
+    constexpr int BLK = (BF || EX) ? 0 : BLK_;
+    static_assert(!EX || PIPE == 0, "exact accumulation: small-tile kernels only");
     constexpr int NW = WM * WN;
     constexpr int MI = BM / WM / 16, NJ = BN / WN / 16;   // 16x16 tiles per wave
     constexpr int LA = BM / 8 / NW, LB = BN / 8 / NW;     // glds instructions per wave per stage
@@ -747,7 +749,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     constexpr int NS_MAX = BLK == 256 ? 6 - SP : 5;
     // deep pipelines only on the narrow 64-row tiles (grids under one workgroup per CU); the 128-row tiles keep two
     // stages so two workgroups share a CU (their grids have several tiles per CU)
-    constexpr int NS = PIPE || BLK == 32 || BM > 64 ? 2 : (NS_FIT >= NS_MAX ? NS_MAX : NS_FIT >= 2 ? NS_FIT : 2);
+    constexpr int NS = PIPE || BLK == 32 || EX || BM > 64 ? 2 : (NS_FIT >= NS_MAX ? NS_MAX : NS_FIT >= 2 ? NS_FIT : 2);
     static_assert(PIPE || BLK != 256 || SP + NS <= 6, "Q4_K scale prefetch distance");
     static_assert(NBUF == 2 || (NS == 2 && SP <= 3), "single Q4_K scale buffer: pieces on steps 4b+1 .. 4b+3");
     constexpr int LDS_MAIN = PIPE == 2 ? SBUF_OFF + SBUF_BYTES + 512 : PIPE ? (BLK ? SBUF_OFF + SBUF_BYTES : 2 * OPB) : NS * OPB + SCALE_LDS;
@@ -766,9 +768,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (__builtin_amdgcn_s_memrealtime() - t0 < dt) __builtin_amdgcn_s_sleep(8);
     }
-    constexpr bool GROUPABLE = !PIPE && !BF && (BLK == 0 || BLK == 256) && EPI == Q2A_EPI_STORE_F;
+    constexpr bool GROUPABLE = !PIPE && !BF && !EX && (BLK == 0 || BLK == 256) && EPI == Q2A_EPI_STORE_F;
     const int ngrp = (GROUPABLE && p.ngroup == 2) ? 2 : 1;
-    const int ksplit = (!PIPE && (BLK == 0 || BLK == 32) && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) &&
+    const int ksplit = (!PIPE && !EX && (BLK == 0 || BLK == 32) && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) &&
                         p.ksplit > 1 && ngrp == 1) ? p.ksplit : 1;
     const int nbn = p.N / BN, nbm = (p.M - p.m_base + BM - 1) / BM, ntl = nbn * nbm, nwg = ntl * ksplit * ngrp;
     const int bid = blockIdx.x, xcd = bid & 7, qq = nwg >> 3, rr = nwg & 7;
@@ -962,12 +964,20 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
         };
 
         // Q8_0 / Q4_0 (BLK = 32): a fresh accumulator per 32-block, combined acc += (dx*dy)*blk after each
-        f4 blk[BLK == 32 ? MI : 1][BLK == 32 ? NJ : 1];
-        if (BLK == 32) {
+        // exact mode (EX): the same fresh accumulator per 64-deep K-step, added into acc64 after it
+        constexpr bool FRESH = BLK == 32 || EX;
+        f4 blk[FRESH ? MI : 1][FRESH ? NJ : 1];
+        double acc64[EX ? MI : 1][EX ? NJ : 1][4];
+        if (FRESH) {
     #pragma unroll
-            for (int i = 0; i < (BLK == 32 ? MI : 1); ++i)
+            for (int i = 0; i < (FRESH ? MI : 1); ++i)
     #pragma unroll
-                for (int j = 0; j < (BLK == 32 ? NJ : 1); ++j) blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+                for (int j = 0; j < (FRESH ? NJ : 1); ++j) {
+                    blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+                    if (EX)
+    #pragma unroll
+                        for (int r = 0; r < 4; ++r) acc64[i][j][r] = 0.0;
+                }
         }
         // Q4_K (BLK = 256): the block-ratio recurrence of the 8-phase kernel (kq_rescale), op for op
         auto kq_block_start = [&](const char * sb, auto first) {   // first: std::true_type for block 0 (acc = 0)
@@ -1054,7 +1064,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     #pragma unroll
                     for (int j = 0; j < NJ; ++j) {
                         // W as the A operand: C^T tiles (lane = 4 consecutive columns of one row, see the epilogue)
-                        if (BLK != 32) acc[i][j] = mma16<BF>(b[j], a, acc[i][j]);
+                        if (!FRESH) acc[i][j] = mma16<BF>(b[j], a, acc[i][j]);
                         else blk[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], a, blk[i][j], 0, 0, 0);
                     }
                 }
@@ -1077,6 +1087,16 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                         }
                     }
                 }
+            }
+            if constexpr (EX) {   // this K-step's 64-deep partial into the f64 sums
+    #pragma unroll
+                for (int i = 0; i < MI; ++i)
+    #pragma unroll
+                    for (int j = 0; j < NJ; ++j) {
+    #pragma unroll
+                        for (int r = 0; r < 4; ++r) acc64[i][j][r] += (double) blk[i][j][r];
+                        blk[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+                    }
             }
             // stage kt + 1 must have landed before the barrier; the NS - 2 younger stages stay in flight (raw
             // s_barrier: __syncthreads would drain them). Steps that fetched scales into registers drain fully.
@@ -1125,6 +1145,14 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                     for (int r = 0; r < 4; ++r) acc[i][j][r] = kq_final(acc[i][j][r], yc, dx4[r]);
                 }
             }
+        }
+        if constexpr (EX) {   // the f64 sums rounded to f32 once: the epilogue then runs unchanged
+    #pragma unroll
+            for (int i = 0; i < MI; ++i)
+    #pragma unroll
+                for (int j = 0; j < NJ; ++j)
+    #pragma unroll
+                    for (int r = 0; r < 4; ++r) acc[i][j][r] = (float) acc64[i][j][r];
         }
     }
 
@@ -1838,6 +1866,10 @@ hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
             if (p8) return launch_pipe8<EPI, 0>(a, s);
             if (narrow) return launch_cfg<64, 128, 2, 2, EPI, 0>(a, s);
             return big ? launch_cfg<256, 256, 2, 4, EPI, 0>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 0>(a, s);
+        }
+        if constexpr (EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_CONV2 || EPI == Q2A_EPI_STORE_F) {
+            // the conv GEMMs' exact accumulation: 64x128 tiles in every regime (one K order, batch invariant)
+            if (blk == Q2A_BLK_EXACT) return launch_cfg<64, 128, 2, 2, EPI, Q2A_BLK_EXACT>(a, s);
         }
         if (blk == 256) {
             if (!a.beta || !a.gamma) return hipErrorInvalidValue;   // the block recurrence needs beta / gamma

@@ -105,6 +105,11 @@ int q2a_gemm_kq_ksplit(int M, int N, int K, int blk);
 // blk: 0 (plain fp16 GEMM), 256 (Q4_K x Q8_K), 32 (Q8_0/Q4_0 x Q8_0), Q2A_BLK_BF16 (bf16 x bf16 MFMA, no block
 // scales: the bf16-activation mode, whose fp16-typed operand and output pointers then hold bf16 bits)
 constexpr int Q2A_BLK_BF16 = 1;
+// Q2A_BLK_EXACT: fp16 x fp16 (like blk 0) with each 64-deep K-step's MFMA sum (two chained 16x16x32) added into f64
+// accumulators, rounded to f32 once before the epilogue — the conv GEMMs (q2a_engine conv1 / conv2, the ggml
+// backend's conv MUL_MAT): summed this way the conv output is within rounding of the exact dot product instead of
+// carrying a 120-deep f32 accumulation chain ("the conv's own summation")
+constexpr int Q2A_BLK_EXACT = 2;
 hipError_t q2a_launch_gemm(const q2a_gemm_args & a, int epi, int blk, hipStream_t s);
 // true when the launcher will use the 256-column tile configuration for this shape (Q2A_EPI_GELU_Q8K needs it)
 bool q2a_gemm_wide_tiles(int M, int N, int blk);

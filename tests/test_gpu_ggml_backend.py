@@ -18,13 +18,11 @@ from conftest import ROOT, full_ref_samples, rel_errors, tiny_ref_rows
 
 pytestmark = pytest.mark.gpu
 
-# The drop-in path's F16 model lands just beyond the widest clip-averaged pair of reference builds (round 3, DESIGN.md
-# §2: tiny rel-L2 1.957e-5 against 1.936e-5, full-size max-rel 4.67e-4 against 4.41e-4; the engine, the product
-# path, sits inside at x1.0 on the same clips). Every op of this path is F32-class and its distance to the engine is
-# as large as its distance to the golden build (1.9e-5): an independent-rounding implementation whose F16 draw sits
-# at 1.01-1.06x the reference builds' widest one, the cause not yet isolated (diag/backend_tiny_variants.py). Held to
-# this measured factor, stated here rather than hidden in the bar; quantized files stay at x1.0.
-BACKEND_F16_FACTOR = 1.07
+# Every statistic at x1.0 of the reference builds' clip-averaged spread, F16 included. Round 3 needed a factor of 1.07
+# for the F16 model here: the conv MUL_MATs summed 3 840 products in one f32 MFMA chain and carried twice a CPU build's
+# own conv error (diag/backend_l0_trace.py: 1 333 fp16 flips at the conv output against 428-846 between CPU builds),
+# which GELU's fp16 table turned into flips downstream; with every 64-deep K-step's partial summed in f64
+# (Q2A_BLK_EXACT) the path sits at 0.90 / 0.92 of the tiny / full-size bars.
 
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "ggml_harness")
 
@@ -67,8 +65,7 @@ def test_reference_whisper_full_on_backend_tiny(harness, make_model, make_clip, 
     # clip-averaged, within the reference's own widest clip-averaged cross-build disagreement (tiny_avg_bar, x1.0)
     st = [rel_errors(e[g["rows_stride5"]], tiny_ref_rows(g, xclips, wt, c)) for (e, _), c in zip(embs, bar["clips"])]
     mx, l2 = float(np.mean([x[0] for x in st])), float(np.mean([x[1] for x in st]))
-    f = BACKEND_F16_FACTOR if wt == "f16" else 1.0
-    assert mx <= f * bar["max_rel"] and l2 <= f * bar["rel_l2"], (mx, l2, st, bar)
+    assert mx <= bar["max_rel"] and l2 <= bar["rel_l2"], (mx, l2, st, bar)
 
 
 def test_backend_unfused_attention_path(harness, make_model, make_clip, golden, tmp_path):
@@ -93,8 +90,7 @@ def test_reference_whisper_full_on_backend_full_size(harness, make_model, make_c
     mxs, l2s = float(np.mean([x[0] for x in st])), float(np.mean([x[1] for x in st]))
     rn = np.linalg.norm(emb.astype(np.float64), axis=1)
     rnerr = np.abs(rn - g[f"full_{wt}_c0_rownorm"]).max() / g[f"full_{wt}_c0_rownorm"].max()
-    f = BACKEND_F16_FACTOR if wt == "f16" else 1.0
-    assert mxs <= f * bar["max_rel"] and l2s <= f * bar["rel_l2"], (mxs, l2s, st, bar)
+    assert mxs <= bar["max_rel"] and l2s <= bar["rel_l2"], (mxs, l2s, st, bar)
     assert rnerr < 20 * xbuild_bar(wt)["rownorm_rel"], rnerr
     if wt == "f16":
         assert all(x[0] < 1e-3 and x[1] < 1e-3 for x in st), st
