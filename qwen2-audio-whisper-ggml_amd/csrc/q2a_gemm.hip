@@ -67,6 +67,13 @@ __device__ __forceinline__ void q2a_st(const V & v, V * ptr) {
 // per workgroup, a diagnostic build). Round 4 (diag/gpurun_r04d.sh): fc1 1.268 ms per launch (rocprof) against 1.341
 // one-tile-per-workgroup; same-box bench A/B fc1 39.5 / 40.4 against 41.1 / 40.7 ms per step; outputs bit-identical
 // (64-clip batch-invariance tests)
+// exact-accumulation conv GEMMs (Q2A_BLK_EXACT): LDS stages and tile (0: 64x128, 1: 128x128); diagnostic A/B knobs
+#ifndef Q2A_GEMM_EXACT_NS
+#define Q2A_GEMM_EXACT_NS 2
+#endif
+#ifndef Q2A_GEMM_EXACT_TILE
+#define Q2A_GEMM_EXACT_TILE 0
+#endif
 #ifndef Q2A_GEMM_PERSIST
 #define Q2A_GEMM_PERSIST 1
 #endif
@@ -749,7 +756,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     constexpr int NS_MAX = BLK == 256 ? 6 - SP : 5;
     // deep pipelines only on the narrow 64-row tiles (grids under one workgroup per CU); the 128-row tiles keep two
     // stages so two workgroups share a CU (their grids have several tiles per CU)
-    constexpr int NS = PIPE || BLK == 32 || EX || BM > 64 ? 2 : (NS_FIT >= NS_MAX ? NS_MAX : NS_FIT >= 2 ? NS_FIT : 2);
+    constexpr int NS = EX ? Q2A_GEMM_EXACT_NS : PIPE || BLK == 32 || BM > 64 ? 2 : (NS_FIT >= NS_MAX ? NS_MAX : NS_FIT >= 2 ? NS_FIT : 2);
     static_assert(PIPE || BLK != 256 || SP + NS <= 6, "Q4_K scale prefetch distance");
     static_assert(NBUF == 2 || (NS == 2 && SP <= 3), "single Q4_K scale buffer: pieces on steps 4b+1 .. 4b+3");
     constexpr int LDS_MAIN = PIPE == 2 ? SBUF_OFF + SBUF_BYTES + 512 : PIPE ? (BLK ? SBUF_OFF + SBUF_BYTES : 2 * OPB) : NS * OPB + SCALE_LDS;
@@ -1869,7 +1876,10 @@ hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
         }
         if constexpr (EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_CONV2 || EPI == Q2A_EPI_STORE_F) {
             // the conv GEMMs' exact accumulation: 64x128 tiles in every regime (one K order, batch invariant)
-            if (blk == Q2A_BLK_EXACT) return launch_cfg<64, 128, 2, 2, EPI, Q2A_BLK_EXACT>(a, s);
+            if (blk == Q2A_BLK_EXACT) {
+                if (Q2A_GEMM_EXACT_TILE) return launch_cfg<128, 128, 2, 2, EPI, Q2A_BLK_EXACT>(a, s);
+                return launch_cfg<64, 128, 2, 2, EPI, Q2A_BLK_EXACT>(a, s);
+            }
         }
         if (blk == 256) {
             if (!a.beta || !a.gamma) return hipErrorInvalidValue;   // the block recurrence needs beta / gamma
