@@ -54,7 +54,9 @@ __global__ __launch_bounds__(256) void k_mel_frames(const q2a_mel_args p) {
         const float v = (float) log10(1e-10);
         if (in_win)
             for (int j = lane; j < p.n_mel; j += 64) mel_out[(int64_t) j * p.n_frames_win + win] = v;
-        if (lane == 0) atomicMax(p.clip_max + c, f2ord(v));
+        // every constant frame has the same value: its first one alone enters the clip maximum (thousands of
+        // same-address atomics per clip serialised at L2 were most of this kernel's time)
+        if (lane == 0 && i == n_fft_frames) atomicMax(p.clip_max + c, f2ord(v));
     }
     // every wave reaches every barrier below; inactive waves just skip the work
     // windowed input: samples_padded = [reflect(200) | pcm | zeros], read up to n_s (:2526-2533)
@@ -116,11 +118,10 @@ __global__ __launch_bounds__(256) void k_mel_frames(const q2a_mel_args p) {
     if (do_fft)
         for (int j = lane; j < p.n_bins; j += 64) s_pow[w][j] = cur[2 * j] * cur[2 * j] + cur[2 * j + 1] * cur[2 * j + 1];
     __syncthreads();
-    if (!do_fft) return;
     // mel filterbank in double with the reference's 4-way unrolled float partial sums (:2545-2561)
     float lmax = -INFINITY;
     const float * P = s_pow[w];
-    for (int j = lane; j < p.n_mel; j += 64) {
+    for (int j = lane; do_fft && j < p.n_mel; j += 64) {
         const float * f = p.filters + (int64_t) j * p.n_bins;
         double sum = 0.0;
         int k = 0;
@@ -135,7 +136,14 @@ __global__ __launch_bounds__(256) void k_mel_frames(const q2a_mel_args p) {
         lmax = fmaxf(lmax, v);
     }
     for (int o = 32; o > 0; o >>= 1) lmax = fmaxf(lmax, __shfl_xor(lmax, o));
-    if (lane == 0) atomicMax(p.clip_max + c, f2ord(lmax));
+    // one atomic per workgroup (its four frames' maximum) instead of one per frame
+    __shared__ float s_wmax[4];
+    if (lane == 0) s_wmax[w] = lmax;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float m4 = fmaxf(fmaxf(s_wmax[0], s_wmax[1]), fmaxf(s_wmax[2], s_wmax[3]));
+        if (m4 != -INFINITY) atomicMax(p.clip_max + c, f2ord(m4));
+    }
 }
 
 // clamp to (max - 8), (x + 4) / 4 (:2633-2649), then write the conv1 operand rows as three fp16 parts. F16 conv kernels:
