@@ -200,6 +200,16 @@ def host_cpu_info() -> dict:
     return info
 
 
+# The profile set measured on the current tree; its summaries are cited ahead of older rounds' (tags do not sort
+# by date: r04y was taken after r04z).
+PROFILE_TAG = "r04y"
+
+
+def _profile_files(names) -> list:
+    """Committed summaries, oldest first by tag, the PROFILE_TAG set last (the one the line cites)."""
+    return sorted(names, key=lambda f: (f.startswith(PROFILE_TAG + "_"), f))
+
+
 def fc1_kernel_label(wt: str, bf16: bool, M: int) -> str:
     """The k_gemm instantiation the engine launches for fc1 (N = 5120, K = 1280), mirroring q2a_gemm.hip's tile
     regimes: 256x256 8-phase tiles once ceil(M/256) x 20 tiles >= 512 (M >= 6401), persistent (PIPE 2) for the Q4_K
@@ -396,7 +406,7 @@ def main():
     # HBM traffic of the same kernel from the committed rocprofv3 PMC passes of this workload (FETCH_SIZE and
     # WRITE_SIZE in separate passes, FETCH_SIZE x2 gfx950 correction); null when no summary matches.
     traffic, traffic_src = None, None
-    pmc_files = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith(f"_{args.config}_pmc_traffic.json")) \
+    pmc_files = _profile_files(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith(f"_{args.config}_pmc_traffic.json")) \
         if os.path.isdir(os.path.join(ROOT, "profiles")) else []
     if pmc_files and clips_per_gpu == CONFIGS[args.config][1]:
         with open(os.path.join(ROOT, "profiles", pmc_files[-1])) as f:
@@ -407,7 +417,7 @@ def main():
     # MFMA busy fraction of the same kernel from the committed SQ counter pass (profiles/collect_sq.sh +
     # sq_summary.py): SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs), rocprof's MfmaUtil
     mfma_busy, mfma_src = None, None
-    sq_files = sorted(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith(f"_{args.config}_sq_mfma.json")) \
+    sq_files = _profile_files(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith(f"_{args.config}_sq_mfma.json")) \
         if os.path.isdir(os.path.join(ROOT, "profiles")) else []
     if sq_files:
         with open(os.path.join(ROOT, "profiles", sq_files[-1])) as f:
