@@ -533,6 +533,31 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
                 for (int j = 0; j < 2; ++j)
                     acc[qm * 4 + i][qn * 2 + j] = mma16<BF>(bf[qn][j][s2], af[i][s2], acc[qm * 4 + i][qn * 2 + j]);
     };
+#ifdef Q2A_DIAG_U8_UNPACK
+    // timing diagnostic (results unchanged): the VALU that biased-uint8 activation codes would add — per 8-code
+    // fragment 4 v_perm_b32 (code byte | 0x64 -> fp16 1024 + u) and 4 v_pk_add_f16 (-1152) — issued as identity
+    // operations on the fp16 fragments between the fragment reads' wait and the MFMAs that consume them
+    auto unpack_a = [&]() {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) {
+                typedef uint32_t u4v __attribute__((ext_vector_type(4)));
+                u4v u = __builtin_bit_cast(u4v, af[i][s2]);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    uint32_t w = u[k];
+                    asm volatile("v_perm_b32 %0, %0, %0, %1" : "+v"(w) : "s"(0x03020100u));
+                    asm volatile("v_pk_add_f16 %0, %0, %1" : "+v"(w) : "s"(0x80008000u));
+                    u[k] = w;
+                }
+                af[i][s2] = __builtin_bit_cast(half8, u);
+            }
+    };
+#define Q2A_U8U() unpack_a()
+#else
+#define Q2A_U8U() do { } while (0)
+#endif
 #if Q2A_GEMM_WSTAGGER
     // staggered halves: the fragment reads retire BEFORE the barrier, so an image restaged the phase after its last
     // read (A_q0) cannot overtake the other half's reads, which now run one barrier later (cdna_hip_programming.md
@@ -557,9 +582,9 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     asm volatile("" ::: "memory")
 // the four phases of one K-step in buffer B; S1..S4 = the stage statements issued in each phase
 #define Q2A_KSTEP(B, S1, S2, S3, S4, V1, V2, V3, V4)                                      \
-    read_b(B, 0); read_a(B, 0); S1; Q2A_PB(V1); mma(0, 0); Q2A_PE();                      \
+    read_b(B, 0); read_a(B, 0); S1; Q2A_PB(V1); Q2A_U8U(); mma(0, 0); Q2A_PE();           \
     read_b(B, 1);               S2; Q2A_PB(V2); mma(0, 1); Q2A_PE();                      \
-    read_a(B, 1);               S3; Q2A_PB(V3); mma(1, 1); Q2A_PE();                      \
+    read_a(B, 1);               S3; Q2A_PB(V3); Q2A_U8U(); mma(1, 1); Q2A_PE();           \
                                 S4; Q2A_PB(V4); mma(1, 0); Q2A_PE()
 
     // prologue: the images "phases 2..8 of iteration -1" would have staged (block 0's scales before them)
