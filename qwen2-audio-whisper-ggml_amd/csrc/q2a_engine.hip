@@ -1325,7 +1325,7 @@ int q2a_get_info(const q2a_engine * e, q2a_info * info) {
 }
 
 int q2a_reserve(q2a_engine * e, int max_clips, int64_t max_samples) {
-    if (!e || max_clips <= 0) return Q2A_ERR_ARG;
+    if (!e || max_clips <= 0) { set_err("invalid arguments"); return Q2A_ERR_ARG; }
     (void) max_samples;
     return reserve(e, max_clips);
 }

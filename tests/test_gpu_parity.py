@@ -204,6 +204,38 @@ def test_short_audio_is_skipped_like_reference(engines, make_clip):
     assert not np.all(out[1] == 7.0)
 
 
+def test_invalid_arguments_rejected(engines, make_clip):
+    """Argument errors come back as Q2A_ERR_ARG (-4, include/q2a_encoder.h) before any launch — an empty batch, a
+    negative sample count, a clip longer than its PCM row, a negative offset, a zero reservation — and leave the
+    engine usable: the next valid call is bit-identical to one made before the errors."""
+    import q2a
+    e = engines("tiny", "f16")
+    clip = make_clip(0)
+    ref, st = e.encode_host([clip])
+    assert list(st) == [0]
+    pcm = torch.from_numpy(clip).cuda()
+    out = torch.empty((1,) + e.out_shape, dtype=torch.float32, device="cuda")
+    bad = [
+        lambda: e.encode_host([]),
+        lambda: e.encode_device(pcm.data_ptr(), pcm.numel(), [-1], out.data_ptr()),
+        lambda: e.encode_device(pcm.data_ptr(), pcm.numel(), [pcm.numel() + 1], out.data_ptr()),
+        lambda: e.encode_device(pcm.data_ptr(), pcm.numel(), [pcm.numel()], out.data_ptr(), offset_ms=-10),
+        lambda: e.encode_device(pcm.data_ptr(), pcm.numel(), [pcm.numel()], 0),
+        lambda: e.reserve(0),
+    ]
+    for call in bad:
+        with pytest.raises(q2a.Q2AError, match=r"q2a error -4"):
+            call()
+    torch.cuda.synchronize()
+    again, st = e.encode_host([clip])
+    assert list(st) == [0]
+    assert np.array_equal(again, ref)
+    st = e.encode_device(pcm.data_ptr(), pcm.numel(), [pcm.numel()], out.data_ptr())
+    torch.cuda.synchronize()
+    assert list(st) == [0]
+    assert np.array_equal(out.cpu().numpy(), ref)
+
+
 @pytest.mark.parametrize("compact", [False, True])
 def test_device_blob_path_matches_file_path(engines, make_model, make_clip, compact):
     """The multi-GPU path (pack on host -> device copy (RCCL broadcast) -> open on the device blob) must give
