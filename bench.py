@@ -402,6 +402,14 @@ def main():
     achieved = fc1_flop / fc1_avg_s / 1e12
     gemm_ms = prof_ms[4] + prof_ms[7] + prof_ms[8] + prof_ms[9]
     gemm_tf = FLOP_WEIGHT_GEMMS_PER_CLIP * clips_per_gpu * brk_steps / (gemm_ms / 1e3) / 1e12
+    # every matrix-core kernel class against the same fp16 MFMA peak, ALGORITHMIC flops: the
+    # attention's F32-class contract issues 3 MFMA terms per product and the conv's exact accumulation 3 operand
+    # parts, neither counted here
+    for i, fl in ((1, 2.0 * (2 * T) * D * 3 * 128), (2, 2.0 * T * D * 3 * D), (4, 2.0 * T * 3 * D * D * L),
+                  (5, 2 * 2.0 * T * T * D * L), (7, 2.0 * T * D * D * L), (8, FLOP_FC1_PER_CLIP * L), (9, 2.0 * T * D * F * L)):
+        if prof_ms[i] > 0:
+            tf = fl * clips_per_gpu * brk_steps / (prof_ms[i] / 1e3) / 1e12
+            per_kernel[PROF_NAMES[i]].update({"tflops": round(tf, 1), "mfma_frac": round(tf / PEAK_FP16_MFMA_TFLOPS, 4)})
 
     # HBM traffic of the same kernel from the committed rocprofv3 PMC passes of this workload (FETCH_SIZE and
     # WRITE_SIZE in separate passes, FETCH_SIZE x2 gfx950 correction); null when no summary matches.
