@@ -80,3 +80,24 @@ def test_bench_rccl_world_size_one(tmp_path):
     assert res["setup_s"]["collective_backend"] == "nccl"
     assert res["n_gpus"] == 1 and res["config"]["parallelism"] == "dp1" and res["value"] > 0
     assert res["setup_s"]["weight_h2d_plus_rccl_broadcast"] > 0
+
+
+def test_bench_constants_and_profile_selection():
+    """CPU-only: the bench's algorithmic work per clip is SURVEY.md §8d's (2 273.77 GFLOP; weight GEMMs 1 887.44,
+    fc1 19.66 per layer), and the committed PMC / SQ summaries it cites are the PROFILE_TAG set, which must exist for
+    the default workload (tags do not sort by date)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert abs(bench.FLOP_PER_CLIP / 1e9 - 2273.77) < 0.01
+    assert abs(bench.FLOP_WEIGHT_GEMMS_PER_CLIP / 1e9 - 1887.44) < 0.01
+    assert abs(bench.FLOP_FC1_PER_CLIP / 1e9 - 19.6608) < 1e-6
+    names = os.listdir(os.path.join(ROOT, "profiles"))
+    for suffix in ("_q4k64_pmc_traffic.json", "_q4k64_sq_mfma.json"):
+        picked = bench._profile_files(f for f in names if f.endswith(suffix))[-1]
+        assert picked == bench.PROFILE_TAG + suffix, picked
+        with open(os.path.join(ROOT, "profiles", picked)) as f:
+            kernels = json.load(f)["kernels"]
+        if "pmc" in suffix:
+            assert kernels["gemm_fc1"]["hbm_bytes_per_launch_corrected"] > 1.24e9   # >= the algorithmic bytes
+        else:
+            assert any(e.get("class") == "gemm_fc1" and 0 < e["mfma_busy_frac"] < 1 for e in kernels.values())
