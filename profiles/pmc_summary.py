@@ -31,8 +31,6 @@ def classify(name: str) -> str:
         return "gemm_o+gemm_fc2"
     if epi == 3:
         return "conv2"
-    if epi == 2 and blk == 0:
-        return "gelu_h_fp16 (conv1, and fc1 on F16 models)"
     if epi in (2, 4, 6, 7):
         return "gemm_fc1"
     return EPI.get(epi, str(epi))
