@@ -376,21 +376,34 @@ __global__ __launch_bounds__(GQ_THREADS) void k_gelu_quant_q8k_h16(const q2a_hal
     const int lane = threadIdx.x & 63, sub = lane & 15, grp = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t K = (int64_t) bpr * 256;
-    const int64_t nunits = (int64_t) ((M + 15) / 16) * bpr;
-    const int64_t stride = (int64_t) gridDim.x * GQ_WAVES;
-    auto unit_of = [&](int64_t t) -> int64_t { return (int64_t) blockIdx.x * GQ_WAVES + wave + (t >> 2) * stride; };
-    // rows r0 .. r0 + 3 of block column bf for iteration t (wave-uniform)
-    auto place = [&](int64_t t, int & r0, int & bf) {
-        const int64_t U = min(unit_of(t), nunits - 1);
-        const int c = (int) (U / bpr);
-        bf = (int) (U - (int64_t) c * bpr);
-        r0 = c * 16 + (int) (t & 3) * 4;
+    // work position of iteration t, wave-uniform: unit u = blockIdx * GQ_WAVES + wave + (t >> 2) * stride = block
+    // column bf of the 16-row group c (u = c * bpr + bf), quarter q = t & 3. Advanced incrementally — a division per
+    // iteration was a 64-bit divide expansion of ~170 scalar instructions, twice per iteration (M * K < 2^31: 32 bits)
+    const int nunits = ((M + 15) / 16) * bpr;
+    const int stride = (int) gridDim.x * GQ_WAVES;
+    const int s_c = stride / bpr, s_bf = stride - s_c * bpr;
+    const int c_last = (nunits - 1) / bpr, bf_last = nunits - 1 - c_last * bpr;
+    struct pos_t { int u, c, bf, q; };
+    auto advance = [&](pos_t & w) {
+        if (++w.q == 4) {
+            w.q = 0;
+            w.u += stride;
+            w.c += s_c;
+            w.bf += s_bf;
+            if (w.bf >= bpr) { w.bf -= bpr; ++w.c; }
+        }
+    };
+    // rows r0 .. r0 + 3 of block column bf for a position (past the last unit: the last unit, a harmless re-load)
+    auto place = [&](const pos_t & w, int & r0, int & bf) {
+        const bool past = w.u > nunits - 1;
+        bf = past ? bf_last : w.bf;
+        r0 = (past ? c_last : w.c) * 16 + w.q * 4;
     };
     char * st = &stage[wave][0];
     // 2 x 1 KiB pieces: piece i = rows r0 + 2i (lanes 0-31) and r0 + 2i + 1 (lanes 32-63), 16 B per lane
-    auto dma = [&](int64_t t) {
+    auto dma = [&](const pos_t & w) {
         int r0, bf;
-        place(t, r0, bf);
+        place(w, r0, bf);
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int row = min(r0 + 2 * i + (lane >> 5), M - 1);   // past the end: harmless re-loads keep the counts
@@ -402,10 +415,17 @@ __global__ __launch_bounds__(GQ_THREADS) void k_gelu_quant_q8k_h16(const q2a_hal
     const uint32_t lut0 = (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) char *) lut;
     typedef _Float16 h8_t __attribute__((ext_vector_type(8)));
     typedef _Float16 h2_t __attribute__((ext_vector_type(2)));
-    if (unit_of(0) < nunits) dma(0);
+    pos_t cur;
+    cur.u = (int) blockIdx.x * GQ_WAVES + wave;
+    cur.c = cur.u / bpr;
+    cur.bf = cur.u - cur.c * bpr;
+    cur.q = 0;
+    pos_t nxt = cur;
+    advance(nxt);
+    if (cur.u < nunits) dma(cur);
     bool wait_all = true;
     float dd = 0.f;   // lane L (0..15): d of row 16c + L, filled over the unit's four iterations
-    for (int64_t t = 0; unit_of(t) < nunits; ++t) {
+    for (; cur.u < nunits; cur = nxt, advance(nxt)) {
         // this iteration's DMA; the previous iteration's 3 or 4 stores may still be out (all of them after a ragged one)
         if (wait_all) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
@@ -415,13 +435,13 @@ __global__ __launch_bounds__(GQ_THREADS) void k_gelu_quant_q8k_h16(const q2a_hal
         asm volatile("ds_read_b128 %0, %1" : "=v"(h0) : "v"(a));
         asm volatile("ds_read_b128 %0, %1 offset:16" : "=v"(h1) : "v"(a));
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(h0), "+v"(h1) :: "memory");
-        dma(t + 1);                                          // the buffer's next fill (its data is in registers)
+        dma(nxt);                                            // the buffer's next fill (its data is in registers)
         // the vmcnt(3) at the top of the next iteration counts on this DMA being issued BEFORE this iteration's 3
         // stores: pin the order (no IR motion of memory ops across the fence, no machine scheduling across the barrier)
         asm volatile("" ::: "memory");
         __builtin_amdgcn_sched_barrier(0);
         int r0, bf;
-        place(t, r0, bf);
+        place(cur, r0, bf);
         wait_all = r0 + 4 > M;
         // 16 table reads back to back behind one wait (a compiler-visible lookup is placed per element with its own
         // wait); the index is the element's own bits
@@ -452,7 +472,7 @@ __global__ __launch_bounds__(GQ_THREADS) void k_gelu_quant_q8k_h16(const q2a_hal
             const int lo = sb - 64 * hi;
             *(h2_t *) (aext + ((int64_t) bf * ld + row) * 16 + sub) = h2_t{(_Float16) (float) hi, (_Float16) (float) lo};
         }
-        const int q = (int) (t & 3);
+        const int q = cur.q;
         const float dq = __shfl(d, (lane & 3) * 16);         // d of row r0 + (lane & 3)
         if ((lane >> 2) == q) dd = dq;
         if (q == 3) {   // d of the unit's 16 rows: one 64-B store
