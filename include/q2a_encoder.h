@@ -106,8 +106,11 @@ int q2a_reserve(q2a_engine * e, int max_clips, int64_t max_samples);
  *   offset_ms  whisper_full_params.offset_ms (window start = offset_ms / 10 mel frames)
  *   out_dev    [n_clips][n_out][n_audio_state] f32 (embd_enc of each clip)
  *   status     host array [n_clips] (Q2A_CLIP_*), may be NULL
- *   stream     hipStream_t to run on (NULL = the engine's own stream); the call is asynchronous w.r.t. the
- *              host except for the small per-batch metadata upload, synchronise the stream before reading out_dev.
+ *   stream     hipStream_t to run on, or NULL: the engine's own stream, ordered as if the work had been issued on
+ *              the legacy default stream 0 (it starts after everything queued there before the call, and work queued
+ *              there afterwards starts after it) — the same rule for every device-pointer entry point below and
+ *              q2a_projector_apply. The call is asynchronous w.r.t. the host except for the small per-batch
+ *              metadata upload: synchronise (the given stream, or stream 0) before reading out_dev on the host.
  * Audio longer than 30 s is truncated to one 30 s window, as in the reference (qwen2-whisper.cpp:2366-2372). */
 int q2a_encode_device(q2a_engine * e, const float * pcm_dev, int64_t pcm_stride, const int32_t * n_samples,
                       int n_clips, int offset_ms, float * out_dev, int32_t * status, void * stream);
@@ -128,6 +131,32 @@ int q2a_encode_host_ex(q2a_engine * e, const float * const * pcm, const int32_t 
 /* log-mel of one clip (whisper_pcm_to_mel semantics): writes [n_mels][n_len] into mel_out (capacity
  * mel_cap floats) and *n_len. Runs the same kernels as the encoder on the engine's device. */
 int q2a_pcm_to_mel(q2a_engine * e, const float * pcm, int n_samples, float * mel_out, int64_t mel_cap, int * n_len);
+
+/* ---- one process, several GPUs (ncclCommInitAll + a host thread per device) -----------------------
+ * Replaces the single-device choice of whisper_backend_init_gpu (qwen2-whisper.cpp:1217-1279) for batches of
+ * independent clips, and is what whisper_full_parallel (declared, never defined, include/qwen2-whisper.h:464-469)
+ * runs on when more than one device is visible (include/q2a_whisper.h). */
+typedef struct q2a_group q2a_group;
+int q2a_device_count(void);   /* visible HIP devices (0 when none) */
+/* Open one engine per device of devices[0..n_devices) (n_devices = 0: every visible device). The model is packed
+ * once on the host into its compact transport form, uploaded to devices[0] and sent to the others by ONE
+ * ncclBroadcast over xGMI (RCCL communicators from ncclCommInitAll); each device expands its copy into the device
+ * layout. act: Q2A_ACT_REFERENCE / Q2A_ACT_BF16. NULL on error (q2a_last_error). */
+q2a_group * q2a_group_open(const char * model_path, const int * devices, int n_devices, int act);
+void q2a_group_close(q2a_group * g);
+int q2a_group_size(const q2a_group * g);
+q2a_engine * q2a_group_engine(q2a_group * g, int i);   /* the engine of the group's i-th device (owned by the group) */
+/* The contiguous clip range [*first, *first + *count) the group gives its i-th device out of n_clips: near-equal,
+ * the first n_clips % n_devices ranges one clip longer. Pure host arithmetic. */
+int q2a_group_split(int n_clips, int n_devices, int i, int * first, int * count);
+/* q2a_encode_host_ex over the group: every device encodes its clip range on its own host thread (no collective on
+ * the data path); outputs and statuses land at the clips' own positions. offsets_ms may be NULL (offset_ms for all).
+ * On error the first failing device's code is returned; its clips and every clip whose output never reached
+ * out_host report Q2A_CLIP_FAILED. */
+int q2a_group_encode_host(q2a_group * g, const float * const * pcm, const int32_t * n_samples, const int32_t * offsets_ms,
+                          int n_clips, int offset_ms, float * out_host, int32_t * status);
+/* Start-up cost of q2a_group_open: host pack, H2D + broadcast, per-device expand (seconds), transport bytes. */
+int q2a_group_setup_times(const q2a_group * g, double * pack_s, double * broadcast_s, double * open_s, int64_t * blob_bytes);
 
 /* ---- per-kernel timing (HIP events recorded on the launch stream around every kernel of a class) ---- */
 enum {

@@ -177,6 +177,28 @@ compact_layout compact_of(const blob_header & h) {
     return c;
 }
 
+// A header that arrives from outside the packer (a device blob, an RCCL-broadcast buffer, a caller's host copy) is
+// checked before anything is derived from it: compact_of and expand_blob index fixed [MAX_LAYERS] arrays by its layer
+// count and address device memory by its offsets. Magic, version, the shape rules pack() enforces, and every offset
+// equal to what plan() lays out for those hparams. nullptr = valid, else the reason.
+const char * header_problem(const blob_header & h) {
+    if (h.magic != BLOB_MAGIC || h.version != BLOB_VERSION) return "not a q2a weight blob";
+    const dims d = dims_of(h.hp);
+    if (d.L <= 0 || d.L > MAX_LAYERS) return "not a q2a weight blob (layer count out of range)";
+    if (d.D <= 0 || d.D % 128 || d.D != d.H * 64 || d.T <= 0 || d.T % 2 || d.M <= 0 || d.M % 4 || d.T > (1 << 20) ||
+        d.M > 4096)
+        return "not a q2a weight blob (unsupported shapes)";
+    if ((h.compact != 0 && h.compact != 1) || (h.act != Q2A_ACT_REFERENCE && h.act != Q2A_ACT_BF16) ||
+        q2a_row_size(h.wtype, d.D) == 0 || (blk_of(h.wtype) == 256 && d.D % 256))
+        return "not a q2a weight blob (bad type fields)";
+    blob_header p;
+    if (!plan(p, h.hp, h.wtype, h.act)) return "not a q2a weight blob (layout)";
+    if (p.total != h.total || p.blk != h.blk || p.n_bins != h.n_bins || memcmp(p.goff, h.goff, sizeof(p.goff)) ||
+        memcmp(p.loff, h.loff, sizeof(p.loff[0]) * d.L))
+        return "not a q2a weight blob (inconsistent layout)";
+    return nullptr;
+}
+
 inline void scale_min_k4(int j, const uint8_t * q, uint8_t * dd, uint8_t * mm) {   // ggml-quants.c:1898
     if (j < 4) { *dd = q[j] & 63; *mm = q[j + 4] & 63; }
     else {
@@ -323,9 +345,21 @@ int pack(const char * path, std::vector<uint8_t> & out, int act = 0, bool compac
     if (mf->n_mel_filt != d.M || mf->n_fft_filt != 201) { set_err("bad mel filter shape"); return Q2A_ERR_FORMAT; }
     blob_header h;
     if (!plan(h, hp, wtype, act)) { set_err("too many layers"); return Q2A_ERR_UNSUPPORTED; }
-    out.assign(h.total, 0);
+    // the compact transport form is written directly (its size, not the device layout's: 0.38 vs 1.40 GB for Q4_K)
+    compact_layout c;
+    if (compact) { h.compact = 1; c = compact_of(h); }
+    out.assign(compact ? c.total : h.total, 0);
     uint8_t * blob = out.data();
     memcpy(blob, &h, sizeof(h));
+    // a small section's device-layout offset -> its bytes in `out` (the compact form keeps the global run and each
+    // layer's bias / LayerNorm run verbatim, packed one after the other)
+    auto at = [&](uint64_t off) -> uint8_t * {
+        if (!compact) return blob + off;
+        if (off < h.loff[0][L_BQKV]) return blob + c.g_off + (off - HEADER_BYTES);
+        int l = d.L - 1;
+        while (l > 0 && off < h.loff[l][L_BQKV]) --l;
+        return blob + c.l_off[l] + (off - h.loff[l][L_BQKV]);
+    };
 
     auto T = [&](const std::string & name, int type, std::initializer_list<int64_t> ne) -> const uint8_t * {
         const q2a_tensor_desc * t = q2a_model_file_find(mf, name.c_str());
@@ -338,7 +372,7 @@ int pack(const char * path, std::vector<uint8_t> & out, int act = 0, bool compac
         }
         return mf->data + t->offset;
     };
-    auto cpy = [&](uint64_t off, const uint8_t * src, size_t n) { memcpy(blob + off, src, n); };
+    auto cpy = [&](uint64_t off, const uint8_t * src, size_t n) { memcpy(at(off), src, n); };
 
     // conv kernels are F16 in every file but the all-F32 one (vtype, qwen2-whisper.cpp:1542-1543)
     const bool f32 = wtype == Q2A_TYPE_F32;
@@ -362,7 +396,7 @@ int pack(const char * path, std::vector<uint8_t> & out, int act = 0, bool compac
         // conv1: [oc][ic][k] -> k-major taps against the mel operand rows: F16 [w | w | w] x [mel_h | mel_m | mel_l]
         // (exact); F32 [wh | wh | wl] x [mel_h | mel_l | mel_h]
         const int P1 = 3;
-        uint16_t * w = (uint16_t *) (blob + h.goff[G_CONV1_W]);
+        uint16_t * w = (uint16_t *) at(h.goff[G_CONV1_W]);
         for (int oc = 0; oc < d.D; ++oc)
             for (int ic = 0; ic < d.M; ++ic)
                 for (int k = 0; k < 3; ++k) {
@@ -375,7 +409,7 @@ int pack(const char * path, std::vector<uint8_t> & out, int act = 0, bool compac
                 }
         // conv2: k-major taps over three consecutive conv1 output rows: F16 [w]; F32 [wh | wl] x rows [y | y]
         const int P2 = f32 ? 2 : 1;
-        uint16_t * w2 = (uint16_t *) (blob + h.goff[G_CONV2_W]);
+        uint16_t * w2 = (uint16_t *) at(h.goff[G_CONV2_W]);
         for (int oc = 0; oc < d.D; ++oc)
             for (int ic = 0; ic < d.D; ++ic)
                 for (int k = 0; k < 3; ++k) {
@@ -392,13 +426,13 @@ int pack(const char * path, std::vector<uint8_t> & out, int act = 0, bool compac
     cpy(h.goff[G_LNP_W], lnw, (size_t) d.D * 4);
     cpy(h.goff[G_LNP_B], lnb, (size_t) d.D * 4);
     cpy(h.goff[G_FILT], (const uint8_t *) mf->filters, (size_t) d.M * 201 * 4);
-    q2a_make_mel_tables((float *) (blob + h.goff[G_TAB]));
-    q2a_make_gelu_table((uint16_t *) (blob + h.goff[G_GELU]));
+    q2a_make_mel_tables((float *) at(h.goff[G_TAB]));
+    q2a_make_gelu_table((uint16_t *) at(h.goff[G_GELU]));
     {   // compact |x| <= 10 image of the table for the LDS-resident epilogue lookups: [+0 .. +10] | [-0 .. -10]
-        const uint16_t * t = (const uint16_t *) (blob + h.goff[G_GELU]);
-        uint16_t * c = (uint16_t *) (blob + h.goff[G_GELU_C]);
-        memset(c, 0, Q2A_GELU_C_BYTES);
-        for (int i = 0; i < Q2A_GELU_C_HALF; ++i) { c[i] = t[i]; c[Q2A_GELU_C_HALF + i] = t[0x8000 + i]; }
+        const uint16_t * t = (const uint16_t *) at(h.goff[G_GELU]);
+        uint16_t * cg = (uint16_t *) at(h.goff[G_GELU_C]);
+        memset(cg, 0, Q2A_GELU_C_BYTES);
+        for (int i = 0; i < Q2A_GELU_C_HALF; ++i) { cg[i] = t[i]; cg[Q2A_GELU_C_HALF + i] = t[0x8000 + i]; }
     }
 
     struct job { const uint8_t * src; int K, Ntot, r0, r1; const uint64_t * a; int dst0; };
@@ -423,7 +457,7 @@ int pack(const char * path, std::vector<uint8_t> & out, int act = 0, bool compac
         const uint8_t * l2b = T(p + "final_layer_norm.bias", Q2A_TYPE_F32, {d.D});
         if (!wq || !bq || !wk || !wv || !bv || !wo || !bo || !l1w || !l1b || !w1 || !b1 || !w2 || !b2 || !l2w || !l2b)
             return Q2A_ERR_FORMAT;
-        float * bqkv = (float *) (blob + lo[L_BQKV]);
+        float * bqkv = (float *) at(lo[L_BQKV]);
         memcpy(bqkv, bq, (size_t) d.D * 4);                 // q bias; k has no bias (qwen2-whisper.cpp:2037)
         memcpy(bqkv + 2 * d.D, bv, (size_t) d.D * 4);
         cpy(lo[L_BO], bo, (size_t) d.D * 4);
@@ -441,26 +475,18 @@ int pack(const char * path, std::vector<uint8_t> & out, int act = 0, bool compac
         jobs.push_back({w1, d.D, d.F, 0, d.F, lo + L_MAT0 + 2 * A_COUNT, 0});
         jobs.push_back({w2, d.F, d.D, 0, d.D, lo + L_MAT0 + 3 * A_COUNT, 0});
     }
-    if (compact) {   // the transport form: small sections verbatim, linear weights as the file's ggml rows
-        h.compact = 1;
-        const compact_layout c = compact_of(h);
-        std::vector<uint8_t> cb(c.total, 0);
-        memcpy(cb.data(), &h, sizeof(h));
-        memcpy(cb.data() + c.g_off, blob + HEADER_BYTES, c.g_len);
-        for (int l = 0; l < d.L; ++l) {
-            memcpy(cb.data() + c.l_off[l], blob + h.loff[l][L_BQKV], c.l_len[l]);
+    if (compact) {   // the transport form: small sections written above, linear weights as the file's ggml rows
+        for (int l = 0; l < d.L; ++l)
             for (int w = 0; w < 4; ++w) {   // jobs[6l..6l+5] = q, k, v, o, fc1, fc2
                 const int j0 = w == 0 ? 0 : w + 2, nj = w == 0 ? 3 : 1;
                 uint64_t o = c.raw_off[l][w];
                 for (int q = 0; q < nj; ++q) {
                     const job & jb = jobs[6 * l + j0 + q];
                     const size_t n = (size_t) (jb.r1 - jb.r0) * q2a_row_size(wtype, jb.K);
-                    memcpy(cb.data() + o, jb.src, n);
+                    memcpy(blob + o, jb.src, n);
                     o += n;
                 }
             }
-        }
-        out.swap(cb);
         return Q2A_OK;
     }
     const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -654,6 +680,8 @@ int expand_blob(const uint8_t * cb, const blob_header & h, uint8_t * out, hipStr
     const compact_layout c = compact_of(h);
     const dims d = dims_of(h.hp);
     std::vector<uint8_t> head(HEADER_BYTES, 0);
+    // on every return (errors included) the stream drains before `head`, which an async copy may still read, is freed
+    struct drain { hipStream_t s; ~drain() { (void) hipStreamSynchronize(s); } } dr{s};
     blob_header hx = h;
     hx.compact = 0;
     memcpy(head.data(), &hx, sizeof(hx));
@@ -765,6 +793,32 @@ struct q2a_engine {
 
 namespace {
 
+// A NULL `stream` argument of the device-pointer entry points (q2a_encode_device*, q2a_test_*, q2a_projector_apply):
+// the work runs on the handle's own non-blocking stream, ordered as if it had been issued on the caller's legacy
+// default stream (stream 0, torch's default stream): it starts after everything already queued there, and everything
+// queued there afterwards starts after it. Inputs written and outputs read on stream 0 need no extra synchronisation.
+struct null_stream_order {
+    hipStream_t own;
+    hipEvent_t ev = nullptr;
+    null_stream_order(const void * stream, hipStream_t own_stream) : own(own_stream) {
+        if (stream) return;
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
+            (void) hipGetLastError();
+            ev = nullptr;
+            (void) hipDeviceSynchronize();   // (no event: order by draining instead)
+            return;
+        }
+        (void) hipEventRecord(ev, 0);
+        (void) hipStreamWaitEvent(own, ev, 0);
+    }
+    ~null_stream_order() {
+        if (!ev) return;
+        (void) hipEventRecord(ev, own);
+        (void) hipStreamWaitEvent(0, ev, 0);
+        (void) hipEventDestroy(ev);
+    }
+};
+
 int engine_init(q2a_engine * e, int device) {
     int n = 0;
     HIP_TRY(hipGetDeviceCount(&n));
@@ -777,7 +831,7 @@ int engine_init(q2a_engine * e, int device) {
 }
 
 int engine_adopt_header(q2a_engine * e) {
-    if (e->h.magic != BLOB_MAGIC || e->h.version != BLOB_VERSION) { set_err("not a q2a weight blob"); return Q2A_ERR_FORMAT; }
+    if (const char * why = header_problem(e->h)) { set_err("%s", why); return Q2A_ERR_FORMAT; }
     e->d = dims_of(e->h.hp);
     e->wtype = e->h.wtype;
     e->blk = e->h.blk;
@@ -1180,6 +1234,9 @@ extern "C" {
 
 const char * q2a_last_error(void) { return g_err.c_str(); }
 
+// (q2a_internal.h) the calling thread's q2a_last_error text, for the library's other translation units
+void q2a_internal_set_error(const char * msg) { g_err = msg ? msg : ""; }
+
 int64_t q2a_pack_model(const char * path, void ** host_blob) { return q2a_pack_model_ex(path, Q2A_ACT_REFERENCE, host_blob); }
 
 int64_t q2a_pack_model_ex(const char * path, int act, void ** host_blob) {
@@ -1210,17 +1267,21 @@ int64_t q2a_blob_device_size(const void * host_header, int64_t header_bytes, int
     blob_header h;
     if (!host_header || header_bytes < (int64_t) sizeof(h)) { set_err("invalid arguments"); return Q2A_ERR_ARG; }
     memcpy(&h, host_header, sizeof(h));
-    if (h.magic != BLOB_MAGIC || h.version != BLOB_VERSION) { set_err("not a q2a weight blob"); return Q2A_ERR_FORMAT; }
+    if (const char * why = header_problem(h)) { set_err("%s", why); return Q2A_ERR_FORMAT; }
     if (transport_bytes) *transport_bytes = h.compact ? (int64_t) compact_of(h).total : (int64_t) h.total;
     return (int64_t) h.total;
 }
 
 int q2a_expand_blob(const void * dev_blob, int64_t size, void * dev_out, int64_t out_bytes, int device, void * stream) {
     if (!dev_blob || !dev_out || size < (int64_t) HEADER_BYTES) { set_err("invalid arguments"); return Q2A_ERR_ARG; }
+    int prev = -1;
+    HIP_TRY(hipGetDevice(&prev));
+    struct restore { int d; ~restore() { if (d >= 0) (void) hipSetDevice(d); } } rs{prev};   // the caller's device back
     HIP_TRY(hipSetDevice(device));
     blob_header h;
     HIP_TRY(hipMemcpy(&h, dev_blob, sizeof(h), hipMemcpyDeviceToHost));
-    if (h.magic != BLOB_MAGIC || h.version != BLOB_VERSION || !h.compact) { set_err("not a compact q2a weight blob"); return Q2A_ERR_FORMAT; }
+    if (const char * why = header_problem(h)) { set_err("%s", why); return Q2A_ERR_FORMAT; }
+    if (!h.compact) { set_err("not a compact q2a weight blob"); return Q2A_ERR_FORMAT; }
     if ((int64_t) compact_of(h).total != size || out_bytes < (int64_t) h.total) { set_err("blob size mismatch"); return Q2A_ERR_ARG; }
     return expand_blob((const uint8_t *) dev_blob, h, (uint8_t *) dev_out, stream ? (hipStream_t) stream : nullptr);
 }
@@ -1261,10 +1322,10 @@ q2a_engine * q2a_open_device_blob(const void * dev_blob, int64_t size, int devic
         q2a_close(e);
         return nullptr;
     }
-    g_err.clear();
+    if (engine_adopt_header(e)) { q2a_close(e); return nullptr; }   // (validates before any size is derived)
     const int64_t want = e->h.compact ? (int64_t) compact_of(e->h).total : (int64_t) e->h.total;
-    if (engine_adopt_header(e) || want != size) {
-        if (g_err.empty()) set_err("blob size mismatch");
+    if (want != size) {
+        set_err("blob size mismatch");
         q2a_close(e);
         return nullptr;
     }
@@ -1333,14 +1394,18 @@ int q2a_reserve(q2a_engine * e, int max_clips, int64_t max_samples) {
 int q2a_encode_device(q2a_engine * e, const float * pcm_dev, int64_t pcm_stride, const int32_t * n_samples,
                       int n_clips, int offset_ms, float * out_dev, int32_t * status, void * stream) {
     if (!e) return Q2A_ERR_ARG;
+    HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = stream ? (hipStream_t) stream : e->stream;
+    null_stream_order nso(stream, s);
     return encode_impl(e, pcm_dev, pcm_stride, n_samples, n_clips, offset_ms, nullptr, out_dev, status, s);
 }
 
 int q2a_encode_device_ex(q2a_engine * e, const float * pcm_dev, int64_t pcm_stride, const int32_t * n_samples,
                          const int32_t * offsets_ms, int n_clips, float * out_dev, int32_t * status, void * stream) {
     if (!e || !offsets_ms) { set_err("invalid arguments"); return Q2A_ERR_ARG; }
+    HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = stream ? (hipStream_t) stream : e->stream;
+    null_stream_order nso(stream, s);
     return encode_impl(e, pcm_dev, pcm_stride, n_samples, n_clips, 0, offsets_ms, out_dev, status, s);
 }
 
@@ -1352,6 +1417,12 @@ int q2a_encode_host(q2a_engine * e, const float * const * pcm, const int32_t * n
 int q2a_encode_host_ex(q2a_engine * e, const float * const * pcm, const int32_t * n_samples, const int32_t * offsets_ms,
                        int n_clips, int offset_ms, float * out_host, int32_t * status) {
     if (!e || !pcm || !n_samples || !out_host || n_clips <= 0) { set_err("invalid arguments"); return Q2A_ERR_ARG; }
+    for (int c = 0; c < n_clips; ++c)   // (checked before any copy: a negative count would be a huge memcpy)
+        if (n_samples[c] < 0 || (n_samples[c] > 0 && !pcm[c])) {
+            set_err("clip %d: bad samples (%d, %p)", c, n_samples[c], (const void *) pcm[c]);
+            if (status) for (int k = 0; k < n_clips; ++k) status[k] = Q2A_CLIP_FAILED;
+            return Q2A_ERR_ARG;
+        }
     HIP_TRY(hipSetDevice(e->device));
     // Chunks of clips through two staging sets: chunk k's host->pinned copy and H2D (copy stream) run while chunk k-1
     // encodes (compute stream), and chunk k-1's D2H + pinned->host copy while chunk k encodes. One chunk below 32
@@ -1509,6 +1580,7 @@ int q2a_test_linear(q2a_engine * e, int layer, int which, const float * x, int M
     if (!e || layer < 0 || layer >= e->d.L || which < 0 || which > 3 || M <= 0) return Q2A_ERR_ARG;
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = stream ? (hipStream_t) stream : e->stream;
+    null_stream_order nso(stream, s);
     const dims & d = e->d;
     int rc = reserve(e, (M + d.T - 1) / d.T);
     if (rc) return rc;
@@ -1539,6 +1611,7 @@ int q2a_test_block(q2a_engine * e, int layer, float * x, int n_clips, void * str
     if (!e || layer < 0 || layer >= e->d.L || n_clips <= 0) return Q2A_ERR_ARG;
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = stream ? (hipStream_t) stream : e->stream;
+    null_stream_order nso(stream, s);
     int rc = reserve(e, n_clips);
     if (rc) return rc;
     const size_t bytes = (size_t) n_clips * e->d.T * e->d.D * 4;
@@ -1562,6 +1635,7 @@ int q2a_test_frontend(q2a_engine * e, const float * pcm_dev, int64_t pcm_stride,
     if (!e || !pcm_dev || !n_samples || !x_dev || n_clips <= 0) return Q2A_ERR_ARG;
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = stream ? (hipStream_t) stream : e->stream;
+    null_stream_order nso(stream, s);
     int rc = reserve(e, n_clips);
     if (rc) return rc;
     int max_frames = 0;
@@ -1577,6 +1651,7 @@ int q2a_test_pool_ln(q2a_engine * e, const float * x_dev, int n_clips, float * o
     if (!e || !x_dev || !out_dev || n_clips <= 0) return Q2A_ERR_ARG;
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = stream ? (hipStream_t) stream : e->stream;
+    null_stream_order nso(stream, s);
     int rc = reserve(e, n_clips);
     if (rc) return rc;
     HIP_TRY(hipEventSynchronize(e->meta_evt));
@@ -1601,6 +1676,7 @@ int q2a_test_attention(q2a_engine * e, const float * q, const float * k, const f
     if (!e || n_clips <= 0) return Q2A_ERR_ARG;
     HIP_TRY(hipSetDevice(e->device));
     hipStream_t s = stream ? (hipStream_t) stream : e->stream;
+    null_stream_order nso(stream, s);
     int rc = reserve(e, n_clips);
     if (rc) return rc;
     const dims & d = e->d;
@@ -1700,6 +1776,7 @@ int q2a_projector_apply(q2a_projector * p, const float * x, int64_t rows, float 
     if (!p || !x || !y || rows <= 0 || rows > (1 << 30) / 4) return Q2A_ERR_ARG;
     HIP_TRY(hipSetDevice(p->device));
     hipStream_t s = stream ? (hipStream_t) stream : p->stream;
+    null_stream_order nso(stream, s);
     const int M = (int) rows, K = p->d_in, N = p->d_out, blk = p->blk;
     const int64_t MP = (rows + 255) / 256 * 256;
     const size_t a_bytes = ((size_t) M * K * 2 + 255) & ~size_t(255);

@@ -83,6 +83,10 @@ __device__ __forceinline__ void q2a_st(const V & v, V * ptr) {
 #ifndef Q2A_GEMM_WSTAGGER
 #define Q2A_GEMM_WSTAGGER 1
 #endif
+// 8-phase kernel with two phases of 32 MFMAs per K-step (four barrier intervals) instead of four of 16 (eight)
+#ifndef Q2A_GEMM_P2
+#define Q2A_GEMM_P2 0
+#endif
 
 // Timing diagnostic Q2A_DIAG_STAMPS=<epi>: the 8-phase kernels of epilogue <epi> record s_memtime at fixed points of
 // every workgroup's tile (waves 0 and 4, lane 0) into g_q2a_stamps, read back by q2a_diag_stamps (diag/tile_stamps.py):
@@ -337,7 +341,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #pragma unroll
         for (int u = 0; u < 3; ++u) {
             const int k = sb_prev[u] ? max(kb - 1, 0) : kb;
-            const char * src = sb_base[u] + (int64_t) (k * sb_stride[u]) + l16;
+            const char * src = sb_base[u] + (int64_t) k * sb_stride[u] + l16;   // (64-bit product: aext strides reach 2^31)
             __builtin_amdgcn_global_load_lds((const void *) src, (lds_ptr_t) (sbuf + (wave * 3 + u) * 1024), 16, 0, 0);
         }
     };
@@ -365,7 +369,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
                     const int nc = (pc >= 2 && pc <= 4) ? 4 : pc >= 13 ? 32 : 0;
                     sb_base[u] += (int64_t) (tm0 - m0) * mc + (int64_t) (tn0 - n0) * nc;
                 }
-                sl_src[u] = sb_base[u] + (int64_t) ((sb_prev[u] ? max(kb - 1, 0) : kb) * sb_stride[u]);
+                sl_src[u] = sb_base[u] + (int64_t) (sb_prev[u] ? max(kb - 1, 0) : kb) * sb_stride[u];
             }
             asm volatile("" : "+s"(sl_src[u]));
         }
@@ -587,11 +591,26 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     read_a(B, 1);               S3; Q2A_PB(V3); Q2A_U8U(); mma(1, 1); Q2A_PE();           \
                                 S4; Q2A_PB(V4); mma(1, 0); Q2A_PE()
 
+#if Q2A_GEMM_P2
+    // two phases per K-step, 32 MFMAs each (one barrier interval = one SIMD's 32 MFMAs beside its partner's reads):
+    //   phase a: B_q0, B_q1, A_q0 fragments | stage A_q1 of step t+1        | mma(0,0), mma(0,1)
+    //   phase b: A_q1 fragments             | stage A_q0, B_q0, B_q1 of t+2 | mma(1,1), mma(1,0)
+    // With the halves one barrier apart, an image's last read (waves 4-7) ends one interval after the first half's,
+    // so A_q0 / B_q0 / B_q1 of buffer t%2 are free from phase b of step t on, A_q1 from phase a of step t+1. Every
+    // group waits one K-step (four barrier intervals): vmcnt(8) = the 2 + 6 younger glds of the last two phases.
+#define Q2A_KSTEP2(B, SA, SB, VA, VB)                                                                \
+    read_b(B, 0); read_b(B, 1); read_a(B, 0); SA; Q2A_PB(VA); mma(0, 0); mma(0, 1); Q2A_PE();      \
+    read_a(B, 1);                             SB; Q2A_PB(VB); mma(1, 1); mma(1, 0); Q2A_PE()
+#endif
     // prologue: the images "phases 2..8 of iteration -1" would have staged (block 0's scales before them)
     if constexpr (BLK == 256) stage_scales(0);
     stage(0, 0, 0); stage(0, 2, 0); stage(0, 3, 0); stage(0, 1, 0);
     stage(1, 0, 1); stage(1, 2, 1); stage(1, 3, 1);
+#if Q2A_GEMM_P2
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // A_q0, B_q0, B_q1 of step 0 (and block 0's scales) landed
+#else
     asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+#endif
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     // wave stagger: the M-half wm = 1 (waves 4-7, the SIMD partners of waves 0-3) runs one barrier behind, so each
@@ -601,6 +620,92 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     auto stagger_in = [&]() { if (Q2A_GEMM_WSTAGGER && wm == 1) { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); } };
     auto stagger_out = [&]() { if (Q2A_GEMM_WSTAGGER && wm == 0) { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); } };
 
+#if Q2A_GEMM_P2
+    // glds stream per wave and K-step t: phase a {A_q1(t+1)} 2, phase b {A_q0, B_q0, B_q1 (t+2)} 6 (+3 block scales in
+    // phase b of a block's first K-step). Steady count 8; the scale pieces raise the next three waits to 11 (they are
+    // retired by phase a of the block's third K-step, whose phase b computes the next block's alpha from them).
+    if constexpr (BLK == 0) {
+        stagger_in();
+        int kt = 0;
+        for (; kt < nk - 2; kt += 2) {
+            Q2A_KSTEP2(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage(0, 2, kt + 2), stage(0, 3, kt + 2)), 8, 8);
+            Q2A_KSTEP2(1, stage(0, 1, kt + 2), (stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3)), 8, 8);
+        }
+        Q2A_KSTEP2(0, stage(1, 1, kt + 1), (stage_tail(0, 0), stage_tail(0, 2), stage_tail(0, 3)), 8, 8);
+        Q2A_KSTEP2(1, stage_tail(0, 1), (stage_tail(1, 0), stage_tail(1, 2), stage_tail(1, 3)), 8, 8);
+    } else if constexpr (PERS) {
+        static_assert(BLK == 256, "persistent 8-phase loop: Q4_K only");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        alpha_compute();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        stagger_in();
+        for (;;) {
+            int m0n = 0, n0n = 0;
+            const bool has_next = next(m0n, n0n);
+            auto stage_next = [&](int b, int h) { stage(b, h, has_next ? b : nk - 1); };
+            int kt = 0;
+            block_start(std::true_type{});
+            asm volatile("" ::: "memory");
+            // block 0: the previous tile's S_EPI epilogue stores sit between its last phase b and this phase a
+            Q2A_KSTEP2(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage(0, 2, kt + 2), stage(0, 3, kt + 2), stage_scales(kt / 4 + 1)),
+                       24, 27);
+            Q2A_KSTEP2(1, stage(0, 1, kt + 2), (stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3)), 11, 11);
+            Q2A_KSTEP2(0, stage(1, 1, kt + 3), (alpha_compute(), stage(0, 0, kt + 4), stage(0, 2, kt + 4), stage(0, 3, kt + 4)), 8, 8);
+            Q2A_KSTEP2(1, stage(0, 1, kt + 4), (stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5)), 8, 8);
+            for (kt = 4; kt < nk - 4; kt += 4) {
+                block_start(std::false_type{});
+                asm volatile("" ::: "memory");
+                Q2A_KSTEP2(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage(0, 2, kt + 2), stage(0, 3, kt + 2), stage_scales(kt / 4 + 1)),
+                           8, 11);
+                Q2A_KSTEP2(1, stage(0, 1, kt + 2), (stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3)), 11, 11);
+                Q2A_KSTEP2(0, stage(1, 1, kt + 3), (alpha_compute(), stage(0, 0, kt + 4), stage(0, 2, kt + 4), stage(0, 3, kt + 4)), 8, 8);
+                Q2A_KSTEP2(1, stage(0, 1, kt + 4), (stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5)), 8, 8);
+            }
+            prep_scales_last(has_next, m0n, n0n);
+            block_start(std::false_type{});   // (nk >= 8: the last block is never block 0)
+            asm volatile("" ::: "memory");
+            Q2A_KSTEP2(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage(0, 2, kt + 2), stage(0, 3, kt + 2), stage_scales_last()), 8, 11);
+            Q2A_KSTEP2(1, stage(0, 1, kt + 2), (stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3)), 11, 11);
+            Q2A_KSTEP2(0, (stage(1, 1, kt + 3), (has_next ? set_offsets(m0n, n0n) : (void) 0)),
+                       (stage_next(0, 0), stage_next(0, 2), stage_next(0, 3)), 8, 8);
+            Q2A_KSTEP2(1, stage_next(0, 1), (stage_next(1, 0), stage_next(1, 2), stage_next(1, 3)), 8, 8);
+            __builtin_amdgcn_sched_barrier(0);
+            epi(acc, m0, n0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (!has_next) break;
+            m0 = m0n;
+            n0 = n0n;
+        }
+    } else {
+        static_assert(BLK == 256, "8-phase k-quant loop is Q4_K only");
+        alpha_compute();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        stagger_in();
+        int kt = 0;
+        for (; kt < nk - 4; kt += 4) {
+            if (kt == 0) block_start(std::true_type{});
+            else block_start(std::false_type{});
+            asm volatile("" ::: "memory");
+            Q2A_KSTEP2(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage(0, 2, kt + 2), stage(0, 3, kt + 2), stage_scales(kt / 4 + 1)),
+                       8, 11);
+            Q2A_KSTEP2(1, stage(0, 1, kt + 2), (stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3)), 11, 11);
+            Q2A_KSTEP2(0, stage(1, 1, kt + 3), (alpha_compute(), stage(0, 0, kt + 4), stage(0, 2, kt + 4), stage(0, 3, kt + 4)), 8, 8);
+            Q2A_KSTEP2(1, stage(0, 1, kt + 4), (stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5)), 8, 8);
+        }
+        if (kt == 0) block_start(std::true_type{});
+        else block_start(std::false_type{});
+        asm volatile("" ::: "memory");
+        Q2A_KSTEP2(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage(0, 2, kt + 2), stage(0, 3, kt + 2), stage_scales(kt / 4)), 8, 11);
+        Q2A_KSTEP2(1, stage(0, 1, kt + 2), (stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3)), 11, 11);
+        Q2A_KSTEP2(0, stage(1, 1, kt + 3), (stage_tail(0, 0), stage_tail(0, 2), stage_tail(0, 3)), 8, 8);
+        Q2A_KSTEP2(1, stage_tail(0, 1), (stage_tail(1, 0), stage_tail(1, 2), stage_tail(1, 3)), 8, 8);
+    }
+#undef Q2A_KSTEP2
+#else
     if constexpr (BLK == 0) {
         stagger_in();
         int kt = 0;
@@ -700,6 +805,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
         Q2A_KSTEP(0, stage(1, 1, kt + 3), stage_tail(0, 0), stage_tail(0, 2), stage_tail(0, 3), 10, 10, 10, 10);
         Q2A_KSTEP(1, stage_tail(0, 1), stage_tail(1, 0), stage_tail(1, 2), stage_tail(1, 3), 10, 10, 10, 10);
     }
+#endif
 #undef Q2A_KSTEP
 #undef Q2A_PB
 #undef Q2A_PE

@@ -7,6 +7,9 @@
 
 typedef _Float16 q2a_half;
 
+// sets the calling thread's q2a_last_error() text (defined with the engine; used by q2a_group.cpp)
+extern "C" void q2a_internal_set_error(const char * msg);
+
 // Epilogue kinds of the fused weight GEMM (one template instantiation each)
 enum q2a_epi {
     Q2A_EPI_QKV = 0,        // +bias, Q*(1/sqrt(dh)) -> Qh/Ql, K -> Kh/Kl (fp16 hi/lo), V -> Vt (fp16, [clip][head][d][TP])

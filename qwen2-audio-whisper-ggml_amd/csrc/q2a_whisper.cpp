@@ -33,6 +33,9 @@ struct whisper_state {
 
 struct whisper_context {
     q2a_engine * eng = nullptr;   // owns the device weights
+    std::string path;             // model file and activation contract, for the multi-device group
+    int act = Q2A_ACT_REFERENCE;
+    q2a_group * group = nullptr;  // whisper_full_parallel on > 1 visible device (opened on first use)
     q2a_info info{};
     int n_vocab = 0, ftype = 0;
     whisper_state * state = nullptr;
@@ -184,6 +187,8 @@ struct whisper_context * whisper_init_from_file_with_params_no_state(const char 
     if (!e) { wlog(GGML_LOG_LEVEL_ERROR, "whisper_init: %s\n", q2a_last_error()); return nullptr; }
     whisper_context * ctx = new whisper_context();
     ctx->eng = e;
+    ctx->path = path_model;
+    ctx->act = act;
     q2a_get_info(e, &ctx->info);
     ctx->n_vocab = hp[0];
     ctx->ftype = hp[10];
@@ -215,6 +220,7 @@ void whisper_free_state(struct whisper_state * state) {
 void whisper_free(struct whisper_context * ctx) {
     if (!ctx) return;
     whisper_free_state(ctx->state);   // states first: they share the context's weights
+    q2a_group_close(ctx->group);
     q2a_close(ctx->eng);
     delete ctx;
 }
@@ -303,8 +309,22 @@ int whisper_full_parallel(struct whisper_context * ctx, struct whisper_full_para
     const size_t per_out = (size_t) ctx->info.n_out * ctx->info.n_audio_state;
     st->chunks.assign(per_out * n_processors, 0.0f);
     st->chunk_status.assign(n_processors, Q2A_CLIP_SKIPPED);
+    // more than one visible device: the chunks are spread over every device (q2a_group: one RCCL broadcast of the
+    // weights at first use, contiguous chunk ranges, a host thread per device); one device: one batch on the state
+    if (!ctx->group && q2a_device_count() > 1) {
+        ctx->group = q2a_group_open(ctx->path.c_str(), nullptr, 0, ctx->act);
+        if (!ctx->group) {
+            wlog(GGML_LOG_LEVEL_ERROR, "whisper_full_parallel: multi-device open failed: %s\n", q2a_last_error());
+            return -1;
+        }
+        wlog(GGML_LOG_LEVEL_INFO, "whisper_full_parallel: %d devices\n", q2a_group_size(ctx->group));
+    }
     const int64_t t0 = now_us();
-    if (q2a_encode_host(st->eng, ptr.data(), ns.data(), n_processors, 0, st->chunks.data(), st->chunk_status.data()) != Q2A_OK) {
+    const int erc = ctx->group ? q2a_group_encode_host(ctx->group, ptr.data(), ns.data(), nullptr, n_processors, 0,
+                                                        st->chunks.data(), st->chunk_status.data())
+                               : q2a_encode_host(st->eng, ptr.data(), ns.data(), n_processors, 0, st->chunks.data(),
+                                                 st->chunk_status.data());
+    if (erc != Q2A_OK) {
         wlog(GGML_LOG_LEVEL_ERROR, "whisper_full_parallel: failed to encode: %s\n", q2a_last_error());
         return -1;
     }

@@ -18,13 +18,17 @@ TOOL_PATH = os.path.join(PKG_DIR, "bin", "q2a_tool")
 EXPORTS = (
     "q2a_last_error", "q2a_open", "q2a_pack_model", "q2a_free_host_blob", "q2a_open_device_blob", "q2a_close",
     "q2a_get_info", "q2a_reserve", "q2a_encode_device", "q2a_encode_host", "q2a_pcm_to_mel",
-    "q2a_test_linear", "q2a_test_block", "q2a_test_block_taps", "q2a_test_attention", "q2a_test_fc1_path",
+    "q2a_encode_host_ex", "q2a_test_linear", "q2a_test_block", "q2a_test_block_taps", "q2a_test_attention", "q2a_test_fc1_path",
     "q2a_test_frontend", "q2a_test_pool_ln",
     "q2a_projector_open", "q2a_projector_close", "q2a_projector_get_dims", "q2a_projector_apply",
     "q2a_pack_model_compact", "q2a_blob_device_size", "q2a_expand_blob",
+    "q2a_device_count", "q2a_group_open", "q2a_group_close", "q2a_group_size", "q2a_group_engine", "q2a_group_split",
+    "q2a_group_encode_host", "q2a_group_setup_times",
 )
 
-CLIP_ENCODED, CLIP_SKIPPED = 0, 1
+# per-clip status of the encode calls (include/q2a_encoder.h): FAILED = the host call returned an error before this
+# clip's output reached the caller
+CLIP_ENCODED, CLIP_SKIPPED, CLIP_FAILED = 0, 1, 2
 
 
 class Q2AError(RuntimeError):
@@ -77,6 +81,7 @@ def lib() -> C.CDLL:
         L.q2a_reserve.argtypes = [vp, C.c_int, C.c_int64]
         L.q2a_encode_device.argtypes = [vp, vp, C.c_int64, i32p, C.c_int, C.c_int, vp, i32p, vp]
         L.q2a_encode_host.argtypes = [vp, C.POINTER(vp), i32p, C.c_int, C.c_int, vp, i32p]
+        L.q2a_encode_host_ex.argtypes = [vp, C.POINTER(vp), i32p, i32p, C.c_int, C.c_int, vp, i32p]
         L.q2a_pcm_to_mel.argtypes = [vp, vp, C.c_int, vp, C.c_int64, i32p]
         L.q2a_test_linear.argtypes = [vp, C.c_int, C.c_int, vp, C.c_int, vp, vp]
         L.q2a_test_block.argtypes = [vp, C.c_int, vp, C.c_int, vp]
@@ -88,6 +93,17 @@ def lib() -> C.CDLL:
                          ("q2a_test_pool_ln", [vp, vp, C.c_int, vp, vp])):
             if hasattr(L, name):
                 getattr(L, name).argtypes = at
+        if hasattr(L, "q2a_group_open"):   # round 5 (optional: earlier diagnostic builds load too)
+            L.q2a_group_open.restype = vp
+            L.q2a_group_open.argtypes = [C.c_char_p, i32p, C.c_int, C.c_int]
+            L.q2a_group_close.argtypes = [vp]
+            L.q2a_group_size.argtypes = [vp]
+            L.q2a_group_engine.restype = vp
+            L.q2a_group_engine.argtypes = [vp, C.c_int]
+            L.q2a_group_split.argtypes = [C.c_int, C.c_int, C.c_int, i32p, i32p]
+            L.q2a_group_encode_host.argtypes = [vp, C.POINTER(vp), i32p, i32p, C.c_int, C.c_int, vp, i32p]
+            L.q2a_group_setup_times.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                                C.POINTER(C.c_double), C.POINTER(C.c_int64)]
         L.q2a_projector_open.restype = vp
         L.q2a_projector_open.argtypes = [C.c_char_p, C.c_int]
         L.q2a_projector_close.argtypes = [vp]
@@ -147,16 +163,30 @@ class Engine:
                                        C.c_void_p(stream) if stream else None))
         return st
 
-    def encode_host(self, clips, offset_ms: int = 0, out: np.ndarray | None = None):
+    def encode_host(self, clips, offset_ms: int = 0, out: np.ndarray | None = None, offsets_ms=None,
+                    raise_on_error: bool = True):
+        """Encode host PCM clips. offsets_ms: per-clip window offsets (q2a_encode_host_ex). With raise_on_error=False a
+        failing call returns (out, status, rc) instead of raising: status then marks every clip whose output never
+        reached `out` as CLIP_FAILED."""
         clips = [np.ascontiguousarray(c, dtype=np.float32) for c in clips]
         n = len(clips)
         if out is None:
             out = np.zeros((n,) + self.out_shape, dtype=np.float32)
         ptrs = (C.c_void_p * n)(*[c.ctypes.data for c in clips])
         ns = np.array([len(c) for c in clips], dtype=np.int32)
-        st = np.zeros(n, dtype=np.int32)
-        _check(lib().q2a_encode_host(self.h, ptrs, ns.ctypes.data_as(C.POINTER(C.c_int32)), n, offset_ms,
-                                     C.c_void_p(out.ctypes.data), st.ctypes.data_as(C.POINTER(C.c_int32))))
+        st = np.full(n, -1, dtype=np.int32)
+        i32p = C.POINTER(C.c_int32)
+        if offsets_ms is None:
+            rc = lib().q2a_encode_host(self.h, ptrs, ns.ctypes.data_as(i32p), n, offset_ms,
+                                       C.c_void_p(out.ctypes.data), st.ctypes.data_as(i32p))
+        else:
+            offs = np.ascontiguousarray(offsets_ms, dtype=np.int32)
+            assert len(offs) == n
+            rc = lib().q2a_encode_host_ex(self.h, ptrs, ns.ctypes.data_as(i32p), offs.ctypes.data_as(i32p), n, offset_ms,
+                                          C.c_void_p(out.ctypes.data), st.ctypes.data_as(i32p))
+        if not raise_on_error:
+            return out, st, rc
+        _check(rc)
         return out, st
 
     def pcm_to_mel(self, pcm: np.ndarray) -> np.ndarray:
@@ -198,6 +228,64 @@ class Engine:
     def test_attention(self, q_ptr, k_ptr, v_ptr, n_clips, out_ptr, stream=None):
         _check(lib().q2a_test_attention(self.h, C.c_void_p(q_ptr), C.c_void_p(k_ptr), C.c_void_p(v_ptr), n_clips,
                                         C.c_void_p(out_ptr), C.c_void_p(stream) if stream else None))
+
+
+def group_split(n_clips: int, n_devices: int) -> list[range]:
+    """The contiguous clip ranges q2a_group gives each device (q2a_group_split)."""
+    out = []
+    for i in range(n_devices):
+        f, c = C.c_int32(), C.c_int32()
+        _check(lib().q2a_group_split(n_clips, n_devices, i, C.byref(f), C.byref(c)))
+        out.append(range(f.value, f.value + c.value))
+    return out
+
+
+class Group:
+    """Several GPUs in ONE process (q2a_group_*): one RCCL broadcast of the compact weight blob at open, then clip
+    batches split into contiguous ranges, a host thread per device. devices=None: every visible device."""
+
+    def __init__(self, model_path: str, devices=None, act: int = ACT_REFERENCE):
+        L = lib()
+        devs = np.ascontiguousarray(devices if devices is not None else [], dtype=np.int32)
+        self.h = L.q2a_group_open(model_path.encode(), devs.ctypes.data_as(C.POINTER(C.c_int32)) if len(devs) else None,
+                                  len(devs), act)
+        if not self.h:
+            raise Q2AError(L.q2a_last_error().decode())
+        self.size = L.q2a_group_size(self.h)
+        info = Info()
+        _check(L.q2a_get_info(L.q2a_group_engine(self.h, 0), C.byref(info)))
+        self.out_shape = (info.n_out, info.n_audio_state)
+
+    def setup_times(self) -> dict:
+        a, b, c, n = C.c_double(), C.c_double(), C.c_double(), C.c_int64()
+        _check(lib().q2a_group_setup_times(self.h, C.byref(a), C.byref(b), C.byref(c), C.byref(n)))
+        return {"pack_s": a.value, "broadcast_s": b.value, "open_s": c.value, "blob_bytes": n.value}
+
+    def encode_host(self, clips, offset_ms: int = 0, offsets_ms=None, out: np.ndarray | None = None):
+        clips = [np.ascontiguousarray(c, dtype=np.float32) for c in clips]
+        n = len(clips)
+        if out is None:
+            out = np.zeros((n,) + self.out_shape, dtype=np.float32)
+        ptrs = (C.c_void_p * n)(*[c.ctypes.data for c in clips])
+        ns = np.array([len(c) for c in clips], dtype=np.int32)
+        st = np.full(n, -1, dtype=np.int32)
+        i32p = C.POINTER(C.c_int32)
+        offs = None if offsets_ms is None else np.ascontiguousarray(offsets_ms, dtype=np.int32)
+        _check(lib().q2a_group_encode_host(self.h, ptrs, ns.ctypes.data_as(i32p),
+                                           offs.ctypes.data_as(i32p) if offs is not None else None, n, offset_ms,
+                                           C.c_void_p(out.ctypes.data), st.ctypes.data_as(i32p)))
+        return out, st
+
+    def close(self):
+        if self.h:
+            lib().q2a_group_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001
+            pass
 
 
 class Projector:

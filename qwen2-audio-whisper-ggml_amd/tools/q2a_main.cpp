@@ -19,7 +19,7 @@ namespace {
 struct cli {
     std::string model = "models/ggml-base.en.bin";
     std::vector<std::string> files;
-    int threads = 4, offset_ms = 0, duration_ms = 0, reps = 1, device = 0, processors = 1;
+    int threads = 4, offset_ms = 0, duration_ms = 0, reps = 1, device = 0, processors = 1, gpus = 0;
     bool no_prints = false, batch = false, long_audio = false, bf16 = false;
     std::string dump;
 };
@@ -37,6 +37,8 @@ void usage(const char * argv0) {
             "  -la,       --long-audio     encode every 30 s window of each file in one batch\n"
             "  -oemb F,   --output-emb F   write embd_enc (f32, [windows/files][750][1280]) to F\n"
             "  -dev N,    --device N       HIP device\n"
+            "  -ng N,     --gpus N         -b: spread the batch over the first N devices (default: every visible\n"
+            "                              device; one RCCL broadcast of the weights, a host thread per device)\n"
             "  -bf16,     --bf16-act       bf16-activation contract (Q2A_ACT_BF16, BASELINE configs[4]); not the\n"
             "                              reference's numerics: see DESIGN.md\n"
             "  -np,       --no-prints      only print results\n",
@@ -57,6 +59,7 @@ bool parse(int argc, char ** argv, cli & c) {
         else if (a == "-r" || a == "--reps") { if (!(v = next())) return false; c.reps = atoi(v); }
         else if (a == "-dev" || a == "--device") { if (!(v = next())) return false; c.device = atoi(v); }
         else if (a == "-p" || a == "--processors") { if (!(v = next())) return false; c.processors = atoi(v); }
+        else if (a == "-ng" || a == "--gpus") { if (!(v = next())) return false; c.gpus = atoi(v); }
         else if (a == "-oemb" || a == "--output-emb") { if (!(v = next())) return false; c.dump = v; }
         else if (a == "-b" || a == "--batch") c.batch = true;
         else if (a == "-bf16" || a == "--bf16-act") c.bf16 = true;
@@ -112,12 +115,28 @@ int main(int argc, char ** argv) {
         std::vector<const float *> ptr;
         std::vector<int32_t> ns;
         for (const auto & p : pcms) { ptr.push_back(p.data()); ns.push_back((int32_t) p.size()); }
-        q2a_engine * e = q2a_open_ex(c.model.c_str(), c.device, c.bf16 ? Q2A_ACT_BF16 : Q2A_ACT_REFERENCE);
-        if (!e) { fprintf(stderr, "error: %s\n", q2a_last_error()); return 3; }
+        // more than one device: a q2a_group (contiguous clip ranges, one host thread per device); else one engine
+        const int act = c.bf16 ? Q2A_ACT_BF16 : Q2A_ACT_REFERENCE;
+        const int ndev = c.gpus > 0 ? c.gpus : q2a_device_count();
+        q2a_group * grp = nullptr;
+        q2a_engine * e = nullptr;
+        if (c.gpus > 0 || ndev > 1) {   // (an explicit -ng always takes the group path, -ng 1 included)
+            std::vector<int> devs(ndev);
+            for (int i = 0; i < ndev; ++i) devs[i] = i;
+            grp = q2a_group_open(c.model.c_str(), devs.data(), ndev, act);
+            if (!grp) { fprintf(stderr, "error: %s\n", q2a_last_error()); return 3; }
+            if (!c.no_prints) fprintf(stderr, "%s: batch of %zu clips over %d devices\n", __func__, ptr.size(), ndev);
+        } else {
+            e = q2a_open_ex(c.model.c_str(), c.device, act);
+            if (!e) { fprintf(stderr, "error: %s\n", q2a_last_error()); return 3; }
+        }
         std::vector<float> out((size_t) ptr.size() * n_out * n_state);
         std::vector<int32_t> st(ptr.size());
         for (int r = 0; r < c.reps && rc == 0; ++r) {
-            if (q2a_encode_host(e, ptr.data(), ns.data(), (int) ptr.size(), c.offset_ms, out.data(), st.data()) != Q2A_OK) {
+            const int erc = grp ? q2a_group_encode_host(grp, ptr.data(), ns.data(), nullptr, (int) ptr.size(), c.offset_ms,
+                                                        out.data(), st.data())
+                                : q2a_encode_host(e, ptr.data(), ns.data(), (int) ptr.size(), c.offset_ms, out.data(), st.data());
+            if (erc != Q2A_OK) {
                 fprintf(stderr, "%s: failed to process audio: %s\n", argv[0], q2a_last_error());
                 rc = 10;
             }
@@ -125,6 +144,7 @@ int main(int argc, char ** argv) {
                 if (st[i] == Q2A_CLIP_ENCODED) print20(out.data() + i * n_out * n_state);
         }
         if (dump) fwrite(out.data(), 4, out.size(), dump);
+        q2a_group_close(grp);
         q2a_close(e);
     } else {
         whisper_full_params wp = whisper_full_default_params(WHISPER_SAMPLING_GREEDY);

@@ -204,6 +204,34 @@ def test_short_audio_is_skipped_like_reference(engines, make_clip):
     assert not np.all(out[1] == 7.0)
 
 
+def test_host_call_failure_reports_failed_clips(engines, make_clip):
+    """q2a_encode_host_ex on 40 clips (two chunks of 20) whose clip 30 carries a negative window offset: the second
+    chunk fails, so no clip's output reaches the caller and every status is Q2A_CLIP_FAILED (2) — none reads as a
+    stale ENCODED — and the caller's buffer is untouched. A negative sample count fails before any copy, the same way.
+    The engine stays usable afterwards."""
+    import q2a
+    e = engines("tiny", "f16")
+    clip = make_clip(0)
+    clips = [clip] * 40
+    offs = [0] * 40
+    offs[30] = -100
+    sentinel = np.full((40,) + e.out_shape, 7.0, dtype=np.float32)
+    out, st, rc = e.encode_host(clips, out=sentinel.copy(), offsets_ms=offs, raise_on_error=False)
+    assert rc == -4, rc
+    assert list(st) == [q2a.CLIP_FAILED] * 40
+    assert np.all(out == 7.0)
+    bad = [clip] * 3
+    ns_bad = np.array([len(clip), -5, len(clip)], dtype=np.int32)
+    st2 = np.full(3, -1, dtype=np.int32)
+    ptrs = (q2a.C.c_void_p * 3)(*[c.ctypes.data for c in bad])
+    i32p = q2a.C.POINTER(q2a.C.c_int32)
+    rc2 = q2a.lib().q2a_encode_host(e.h, ptrs, ns_bad.ctypes.data_as(i32p), 3, 0, q2a.C.c_void_p(out.ctypes.data),
+                                    st2.ctypes.data_as(i32p))
+    assert rc2 == -4 and list(st2) == [q2a.CLIP_FAILED] * 3
+    out2, st3 = e.encode_host([clip, clip], offsets_ms=[0, 0])
+    assert list(st3) == [q2a.CLIP_ENCODED] * 2 and np.array_equal(out2[0], out2[1])
+
+
 def test_invalid_arguments_rejected(engines, make_clip):
     """Argument errors come back as Q2A_ERR_ARG (-4, include/q2a_encoder.h) before any launch — an empty batch, a
     negative sample count, a clip longer than its PCM row, a negative offset, a zero reservation — and leave the
@@ -365,9 +393,9 @@ def test_linear_full_size_bench_shape_matches_oracle(engines, make_model, wt, wh
     g = torch.Generator(device="cuda").manual_seed(200 + which)
     xd = torch.randn((M, K), device="cuda", generator=g) * (1.0 if which != 3 else 0.3)
     yd = torch.empty((M, N), dtype=torch.float32, device="cuda")
-    torch.cuda.synchronize()   # x comes from torch's stream; the engine runs on its own (non-blocking) stream
+    # no synchronisation: with stream NULL the engine's work is ordered after torch's default stream (x) and before
+    # what torch queues there next (the row gather below) — include/q2a_encoder.h
     e.test_linear(7, which, xd.data_ptr(), M, yd.data_ptr())
-    torch.cuda.synchronize()
     rows = np.unique(np.concatenate([np.random.default_rng(which).choice(M, 352, replace=False),
                                      [0, 255, 256, 91647, 91648, 95999 - 1, 95999] + list(range(91640, 91664))]))
     ri = torch.from_numpy(rows).cuda()
@@ -449,3 +477,28 @@ def test_deferred_gelu_equals_epilogue_gelu(make_model, make_clip, n_clips):
     finally:
         for e in engines:
             e.close()
+
+
+def test_null_stream_is_ordered_with_the_default_stream(engines):
+    """include/q2a_encoder.h: a NULL stream runs on the engine's own stream ORDERED as if issued on stream 0. The input
+    comes out of a chain of torch kernels still queued on the default stream when the call is made, and the output is
+    consumed by a torch kernel queued right after it — no synchronisation anywhere; the result must equal the same
+    call made on fully drained inputs (ADVICE/VERDICT r04: the round-4 race at the bench shape)."""
+    e = engines("full", "f16")
+    M, K, N = 96000, 1280, 5120
+    g = torch.Generator(device="cuda").manual_seed(77)
+    base = torch.randn((M, K), device="cuda", generator=g)
+    torch.cuda.synchronize()
+    ref = torch.empty((M, N), dtype=torch.float32, device="cuda")
+    e.test_linear(3, 2, base.data_ptr(), M, ref.data_ptr())
+    torch.cuda.synchronize()
+    ref_sum = ref.double().sum().item()
+    for _ in range(3):
+        x = base * 0.5
+        for _ in range(20):   # ~20 more launches queued on stream 0 ahead of the engine's reads
+            x = x * 1.0 + 0.0
+        x = x * 2.0
+        y = torch.full((M, N), float("nan"), dtype=torch.float32, device="cuda")
+        e.test_linear(3, 2, x.data_ptr(), M, y.data_ptr())
+        got = torch.equal(y, ref)      # queued on stream 0 behind the engine's work
+        assert got and y.double().sum().item() == ref_sum

@@ -122,3 +122,25 @@ def test_compact_blob_is_the_file_rows_plus_small_sections(make_model, cfg, wt):
     mf = ggmlfile.read(path)
     qkv = b"".join(np.ascontiguousarray(mf.t(f"layers.0.self_attn.{n}_proj.weight").data).tobytes() for n in "qkv")
     assert comp[off:off + len(qkv)] == qkv
+
+
+def test_corrupt_header_is_refused_before_any_size_is_derived(make_model):
+    """a header with the right magic / version but a layer count past MAX_LAYERS (64), or offsets that are
+    not what the packer lays out, must come back as 'not a q2a weight blob' (Q2A_ERR_FORMAT) from q2a_blob_device_size
+    — the same check q2a_open_device_blob and q2a_expand_blob run first — instead of indexing the fixed per-layer
+    arrays with it."""
+    import q2a
+    blob = q2a.pack_model(make_model("tiny", "q4_k"), compact=True)
+    head = bytearray(blob[:32768])
+    assert q2a.blob_device_size(head)[1] == len(blob)
+    for mutate in (lambda h: struct.pack_into("<i", h, 8 + 4 * 4, 1000),          # n_audio_layer = 1000
+                   lambda h: struct.pack_into("<i", h, 8 + 4 * 4, 0),             # no layers
+                   lambda h: struct.pack_into("<i", h, 8 + 4 * 2, 250),           # D not a multiple of 128
+                   lambda h: struct.pack_into("<Q", h, OFF_TOTAL, 1 << 40),       # device size not the plan's
+                   lambda h: struct.pack_into("<Q", h, OFF_GOFF + 8 * G_COUNT, 7),  # layer 0's first offset moved
+                   lambda h: struct.pack_into("<i", h, OFF_COMPACT, 5),
+                   lambda h: struct.pack_into("<i", h, OFF_WTYPE, 99)):
+        bad = bytearray(head)
+        mutate(bad)
+        with pytest.raises(q2a.Q2AError, match="not a q2a weight blob"):
+            q2a.blob_device_size(bad)
