@@ -7,5 +7,5 @@ O=/root/repo/diag/$NAME
 mkdir -p $O
 F="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -I$R/../include -I$R/csrc -munsafe-fp-atomics -w $*"
 /opt/rocm/bin/hipcc $F -c $R/csrc/q2a_gemm.hip -o $O/q2a_gemm.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $O/libq2a.so $O/q2a_gemm.o $R/build/q2a_attn.o $R/build/q2a_engine.o $R/build/q2a_exact.o $R/build/q2a_format.o $R/build/q2a_whisper.o $R/build/q2a_wav.o -lpthread
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o $O/libq2a.so $O/q2a_gemm.o $R/build/q2a_attn.o $R/build/q2a_engine.o $R/build/q2a_exact.o $R/build/q2a_format.o $R/build/q2a_whisper.o $R/build/q2a_wav.o $R/build/q2a_group.o -L/opt/rocm/lib -Wl,-rpath,/opt/rocm/lib -lrccl -lpthread
 echo built $O/libq2a.so

@@ -514,7 +514,19 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     };
     typedef const __attribute__((address_space(3))) half8 * lds_h8p;
     half8 af[4][2], bf[2][2][2];
+#ifdef Q2A_DIAG_NO_READS   // timing diagnostic only (wrong results): fragments never re-read from LDS in the loop
+#define Q2A_RD_ON (p.K < 0)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int s2 = 0; s2 < 2; ++s2) af[i][s2] = (half8) ((_Float16) (lane * 0.01f + i + s2));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) (&bf[0][0][0])[i] = (half8) ((_Float16) (lane * 0.02f + i));
+#else
+#define Q2A_RD_ON true
+#endif
     auto read_a = [&](int b, int qm) {
+        if (!Q2A_RD_ON) return;
         launder();
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -522,6 +534,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             for (int s2 = 0; s2 < 2; ++s2) af[i][s2] = *(lds_h8p) (uintptr_t) (abase[b][s2] + qm * HT + i * 16 * ROWB);
     };
     auto read_b = [&](int b, int qn) {
+        if (!Q2A_RD_ON) return;
         launder();
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -562,6 +575,11 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #else
 #define Q2A_U8U() do { } while (0)
 #endif
+#ifdef Q2A_DIAG_NO_BAR   // timing diagnostic only (wrong results): no barriers inside the main loop
+#define Q2A_LOOP_BAR() do { } while (0)
+#else
+#define Q2A_LOOP_BAR() __builtin_amdgcn_s_barrier()
+#endif
 #if Q2A_GEMM_WSTAGGER
     // staggered halves: the fragment reads retire BEFORE the barrier, so an image restaged the phase after its last
     // read (A_q0) cannot overtake the other half's reads, which now run one barrier later (cdna_hip_programming.md
@@ -569,7 +587,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #define Q2A_PB(N)                                               \
     asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory");       \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          \
-    __builtin_amdgcn_s_barrier();                               \
+    Q2A_LOOP_BAR();                                             \
     asm volatile("" ::: "memory");                              \
     __builtin_amdgcn_s_setprio(1)
 #else
@@ -582,7 +600,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #define Q2A_PE()                                                \
     __builtin_amdgcn_s_setprio(0);                              \
     asm volatile("" ::: "memory");                              \
-    __builtin_amdgcn_s_barrier();                               \
+    Q2A_LOOP_BAR();                                             \
     asm volatile("" ::: "memory")
 // the four phases of one K-step in buffer B; S1..S4 = the stage statements issued in each phase
 #define Q2A_KSTEP(B, S1, S2, S3, S4, V1, V2, V3, V4)                                      \

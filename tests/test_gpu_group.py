@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 @pytest.mark.parametrize("cfg,wt,n", [("tiny", "f16", 5), ("tiny", "q4_k", 5), ("full", "q4_k", 2)])
 def test_group_of_one_through_rccl_equals_engine(make_model, make_clip, cfg, wt, n):
     path = make_model(cfg, wt)
-    clips = [make_clip(c) for c in range(n)]
+    clips = [make_clip(c, 480000) for c in range(n)]
     if n >= 5:
         clips[3] = clips[3][:12000]      # < 1 s: skipped like the reference
         clips[4] = clips[4][:200000]     # ragged length
@@ -39,7 +39,7 @@ def test_group_of_every_visible_device(make_model, make_clip):
     path = make_model("tiny", "q4_k")
     g = q2a.Group(path)
     assert g.size == torch.cuda.device_count() == q2a.lib().q2a_device_count()
-    clips = [make_clip(c) for c in range(2 * g.size + 1)]
+    clips = [make_clip(c, 480000) for c in range(2 * g.size + 1)]
     out, st = g.encode_host(clips)
     g.close()
     e = q2a.Engine(path, device=0)
@@ -58,7 +58,7 @@ def test_q2a_main_batch_over_group(make_model, make_clip, tmp_path):
     path = make_model("tiny", "f16")
     files = []
     for c in range(3):
-        pcm = make_clip(c)
+        pcm = make_clip(c, 480000)
         s16 = np.clip(np.round(pcm * 32767.0), -32768, 32767).astype(np.int16)
         f = tmp_path / f"c{c}.wav"
         with wave.open(str(f), "wb") as w:
