@@ -83,7 +83,12 @@ __device__ __forceinline__ void q2a_st(const V & v, V * ptr) {
 #ifndef Q2A_GEMM_WSTAGGER
 #define Q2A_GEMM_WSTAGGER 1
 #endif
-// 8-phase kernel with two phases of 32 MFMAs per K-step (four barrier intervals) instead of four of 16 (eight)
+// 8-phase kernel: the operand glds issued inside the MFMA segments (1) or before the reading wave's barrier (0)
+#ifndef Q2A_GEMM_GLDS_C
+#define Q2A_GEMM_GLDS_C 0
+#endif
+// 8-phase kernel with two phases of 32 MFMAs per K-step (four barrier intervals) instead of four of 16 (eight);
+// measured round 5 (diag/gpurun_r05a.sh): bit-identical, 1-3 ms per step SLOWER (fc1 / fc2), not adopted
 #ifndef Q2A_GEMM_P2
 #define Q2A_GEMM_P2 0
 #endif
@@ -541,15 +546,14 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #pragma unroll
             for (int s2 = 0; s2 < 2; ++s2) bf[qn][j][s2] = *(lds_h8p) (uintptr_t) (bbase[b][s2] + qn * HT + j * 16 * ROWB);
     };
-    auto mma = [&](int qm, int qn) {
+    auto mma_h = [&](int qm, int qn, int s2) {   // one 32-deep half of a quadrant's K-step: 8 MFMAs
 #pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[qm * 4 + i][qn * 2 + j] = mma16<BF>(bf[qn][j][s2], af[i][s2], acc[qm * 4 + i][qn * 2 + j]);
+            for (int j = 0; j < 2; ++j)
+                acc[qm * 4 + i][qn * 2 + j] = mma16<BF>(bf[qn][j][s2], af[i][s2], acc[qm * 4 + i][qn * 2 + j]);
     };
+    auto mma = [&](int qm, int qn) { mma_h(qm, qn, 0); mma_h(qm, qn, 1); };
 #ifdef Q2A_DIAG_U8_UNPACK
     // timing diagnostic (results unchanged): the VALU that biased-uint8 activation codes would add — per 8-code
     // fragment 4 v_perm_b32 (code byte | 0x64 -> fp16 1024 + u) and 4 v_pk_add_f16 (-1152) — issued as identity
@@ -585,14 +589,14 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     // read (A_q0) cannot overtake the other half's reads, which now run one barrier later (cdna_hip_programming.md
     // §5 WAR rule)
 #define Q2A_PB(N)                                               \
-    asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory");       \
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");   \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          \
     Q2A_LOOP_BAR();                                             \
     asm volatile("" ::: "memory");                              \
     __builtin_amdgcn_s_setprio(1)
 #else
 #define Q2A_PB(N)                                               \
-    asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory");       \
+    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");   \
     __builtin_amdgcn_s_barrier();                               \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          \
     __builtin_amdgcn_s_setprio(1)
@@ -603,11 +607,27 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     Q2A_LOOP_BAR();                                             \
     asm volatile("" ::: "memory")
 // the four phases of one K-step in buffer B; S1..S4 = the stage statements issued in each phase
+#if Q2A_GEMM_GLDS_C
+// the phase's glds issued by the MFMA wave between the two halves of its 16 MFMAs, instead of by the reading wave
+// before its barrier: the reading segment (fragment reads + their wait) is then the partner's only work. A stage
+// moves one barrier LATER than in the reading segment (WAR: still after both halves' last read of the slot), so every
+// counted wait drops by the size of its own phase's stage (2, or 5 where phase 2 also carries the 3 scale pieces)
+#define Q2A_SB() __builtin_amdgcn_sched_barrier(0)
+#define Q2A_KSTEPC(B, S1, S2, S3, S4, V1, V2, V3, V4)                                                     \
+    read_b(B, 0); read_a(B, 0); Q2A_PB(V1); mma_h(0, 0, 0); Q2A_SB(); S1; Q2A_SB(); mma_h(0, 0, 1); Q2A_PE(); \
+    read_b(B, 1);               Q2A_PB(V2); mma_h(0, 1, 0); Q2A_SB(); S2; Q2A_SB(); mma_h(0, 1, 1); Q2A_PE(); \
+    read_a(B, 1);               Q2A_PB(V3); mma_h(1, 1, 0); Q2A_SB(); S3; Q2A_SB(); mma_h(1, 1, 1); Q2A_PE(); \
+                                Q2A_PB(V4); mma_h(1, 0, 0); Q2A_SB(); S4; Q2A_SB(); mma_h(1, 0, 1); Q2A_PE()
+#define Q2A_KSTEP(B, S1, S2, S3, S4, V1, V2, V3, V4) Q2A_KSTEPC(B, S1, S2, S3, S4, (V1) - 2, (V2) - 2, (V3) - 2, (V4) - 2)
+#define Q2A_KSTEP_S(B, S1, S2, S3, S4, V1, V2, V3, V4) Q2A_KSTEPC(B, S1, S2, S3, S4, (V1) - 2, (V2) - 5, (V3) - 2, (V4) - 2)
+#else
 #define Q2A_KSTEP(B, S1, S2, S3, S4, V1, V2, V3, V4)                                      \
     read_b(B, 0); read_a(B, 0); S1; Q2A_PB(V1); Q2A_U8U(); mma(0, 0); Q2A_PE();           \
     read_b(B, 1);               S2; Q2A_PB(V2); mma(0, 1); Q2A_PE();                      \
     read_a(B, 1);               S3; Q2A_PB(V3); Q2A_U8U(); mma(1, 1); Q2A_PE();           \
                                 S4; Q2A_PB(V4); mma(1, 0); Q2A_PE()
+#define Q2A_KSTEP_S Q2A_KSTEP   // (phase 2 also issues the block's 3 scale pieces)
+#endif
 
 #if Q2A_GEMM_P2
     // two phases per K-step, 32 MFMAs each (one barrier interval = one SIMD's 32 MFMAs beside its partner's reads):
@@ -753,7 +773,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             block_start(std::true_type{});
             BS_T1();
             asm volatile("" ::: "memory");
-            Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
+            Q2A_KSTEP_S(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
                       stage(0, 3, kt + 2), 26, 29, 29, 29);
             Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 29, 13, 10, 10);
             Q2A_KSTEP(0, (alpha_compute(), stage(1, 1, kt + 3)), stage(0, 0, kt + 4), stage(0, 2, kt + 4), stage(0, 3, kt + 4),
@@ -764,7 +784,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
                 block_start(std::false_type{});
                 BS_T1();
                 asm volatile("" ::: "memory");
-                Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
+                Q2A_KSTEP_S(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
                           stage(0, 3, kt + 2), 10, 13, 13, 13);
                 Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 13, 13, 10, 10);
                 Q2A_KSTEP(0, (alpha_compute(), stage(1, 1, kt + 3)), stage(0, 0, kt + 4), stage(0, 2, kt + 4), stage(0, 3, kt + 4),
@@ -776,7 +796,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             block_start(std::false_type{});   // (nk >= 8: the last block is never block 0)
             BS_T1();
             asm volatile("" ::: "memory");
-            Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales_last()), stage(0, 2, kt + 2),
+            Q2A_KSTEP_S(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales_last()), stage(0, 2, kt + 2),
                       stage(0, 3, kt + 2), 10, 13, 13, 13);
             Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 13, 13, 10, 10);
             Q2A_KSTEP(0, stage(1, 1, kt + 3), ((has_next ? set_offsets(m0n, n0n) : (void) 0), stage_next(0, 0)), stage_next(0, 2),
@@ -803,7 +823,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             else block_start(std::false_type{});
             BS_T1();
             asm volatile("" ::: "memory");
-            Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
+            Q2A_KSTEP_S(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
                       stage(0, 3, kt + 2), 10, 13, 13, 13);
             Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 13, 13, 10, 10);
             // phase 9: the next block's alpha (its scales, staged in phase 2, landed by phase 7)
@@ -817,7 +837,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
         else block_start(std::false_type{});
         BS_T1();
         asm volatile("" ::: "memory");
-        Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4)), stage(0, 2, kt + 2),
+        Q2A_KSTEP_S(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4)), stage(0, 2, kt + 2),
                   stage(0, 3, kt + 2), 10, 13, 13, 13);
         Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 13, 13, 10, 10);
         Q2A_KSTEP(0, stage(1, 1, kt + 3), stage_tail(0, 0), stage_tail(0, 2), stage_tail(0, 3), 10, 10, 10, 10);
@@ -825,6 +845,11 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     }
 #endif
 #undef Q2A_KSTEP
+#undef Q2A_KSTEP_S
+#ifdef Q2A_KSTEPC
+#undef Q2A_KSTEPC
+#undef Q2A_SB
+#endif
 #undef Q2A_PB
 #undef Q2A_PE
 #undef BS_T0
@@ -884,7 +909,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     constexpr int EPI_OFF = LUT_EPI ? Q2A_GELU_C_BYTES : 0;
     // per-wave epilogue staging: V^T [64 d][WR + 4 t] fp16 (QKV), or with the lo image the hi | lo pair of [64 d][WR/2
     // + 4 t] (half the wave's rows at a time); the other epilogues keep their 32-row budget
-    constexpr int EPI_WREG = EPI == Q2A_EPI_QKV ? std::max(64 * (BM / WM + 4) * 2, 2 * 64 * (BM / WM / 2 + 4) * 2)
+    constexpr int EPI_WREG = EPI == Q2A_EPI_QKV ? (MI == 1 ? 2 * 64 * (BM / WM + 4) * 2   // (16-row waves: one pass, hi | lo)
+                                                           : std::max(64 * (BM / WM + 4) * 2, 2 * 64 * (BM / WM / 2 + 4) * 2))
                                                 : 2 * 32 * (BN / WN + 8) * 2;
     // small-tile kernels: NS operand stages (NS - 1 K-steps of loads in flight, counted vmcnt, raw barriers) within
     // ~150 KiB of LDS. Q4_K: block b+1's scales arrive by glds in 1 KiB pieces (SBP per block, one per wave on the
@@ -1621,6 +1647,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
             char * region = lds_raw + EPI_OFF + wave * EPI_WREG;
             if (!two) {
                 vt_epi(region, c0{}, cmi{}, std::integral_constant<int, WR + 4>{}, false);
+            } else if constexpr (MI == 1) {   // 16-row waves: the hi | lo pair of all rows in one pass
+                vt_epi(region, c0{}, cmi{}, std::integral_constant<int, WR + 4>{}, true);
             } else {
                 vt_epi(region, c0{}, cmh{}, std::integral_constant<int, WR / 2 + 4>{}, true);
                 vt_epi(region, cmh{}, cmh{}, std::integral_constant<int, WR / 2 + 4>{}, true);
@@ -1915,6 +1943,19 @@ hipError_t launch_cfg(const q2a_gemm_args & a, hipStream_t s) {
 #define Q2A_GEMM_STAGGER_G 2
 #endif
 
+// M-waves of the small-batch tiles (a single clip's GEMMs): 2 = 4-wave workgroups, 4 = 8 waves (16 / 32 rows per wave;
+// every wave keeps 64 columns, so the K order per output and the epilogues are those of the 4-wave form). The narrow
+// 64x128 tiles run 8 waves: a single clip's O / fc2 tiles are glds-issue-bound at one wave per SIMD; two per SIMD
+// overlap one wave's issue with the other's MFMAs — Q4_K one clip 8.35 -> 7.73 ms per encode (fc2 2.26 -> 1.78, O
+// 0.79 -> 0.68), F16 unchanged; the 128x128 tiles with 8 waves: F16 fc1 -5 %, Q4_K QKV / fc1 +18 %: kept at 4
+// (round 5, diag/gpurun_r05e.sh, profiles/r05e_small_tiles_8waves.json)
+#ifndef Q2A_GEMM_NARROW_WM
+#define Q2A_GEMM_NARROW_WM 4
+#endif
+#ifndef Q2A_GEMM_SMALL_WM
+#define Q2A_GEMM_SMALL_WM 2
+#endif
+
 // small M (one or a few clips): 64-row tiles when 128x128 tiles would leave CUs idle
 bool narrow_tiles(int M, int N) {
     return !Q2A_GEMM_NO_NARROW && (Q2A_GEMM_NARROW_ALL || (int64_t) ((M + 127) / 128) * (N / 128) < 256);
@@ -2020,8 +2061,8 @@ hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
         const bool narrow = !big && narrow_tiles(a.M, a.N) && a.ksplit <= 1 && a.ngroup != 2;
         if (blk == 0) {
             if (p8) return launch_pipe8<EPI, 0>(a, s);
-            if (narrow) return launch_cfg<64, 128, 2, 2, EPI, 0>(a, s);
-            return big ? launch_cfg<256, 256, 2, 4, EPI, 0>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 0>(a, s);
+            if (narrow) return launch_cfg<64, 128, Q2A_GEMM_NARROW_WM, 2, EPI, 0>(a, s);
+            return big ? launch_cfg<256, 256, 2, 4, EPI, 0>(a, s) : launch_cfg<128, 128, Q2A_GEMM_SMALL_WM, 2, EPI, 0>(a, s);
         }
         if constexpr (EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_CONV2 || EPI == Q2A_EPI_STORE_F) {
             // the conv GEMMs' exact accumulation: 64x128 tiles in every regime (one K order, batch invariant)
@@ -2033,19 +2074,19 @@ hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
         if (blk == 256) {
             if (!a.beta || !a.gamma) return hipErrorInvalidValue;   // the block recurrence needs beta / gamma
             if (p8) return launch_pipe8<EPI, 256>(a, s);
-            if (narrow) return launch_cfg<64, 128, 2, 2, EPI, 256>(a, s);
-            return big ? launch_cfg<128, 256, 2, 4, EPI, 256>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 256>(a, s);
+            if (narrow) return launch_cfg<64, 128, Q2A_GEMM_NARROW_WM, 2, EPI, 256>(a, s);
+            return big ? launch_cfg<128, 256, 2, 4, EPI, 256>(a, s) : launch_cfg<128, 128, Q2A_GEMM_SMALL_WM, 2, EPI, 256>(a, s);
         }
         if (blk == 32) {
-            if (narrow) return launch_cfg<64, 128, 2, 2, EPI, 32>(a, s);
-            return big ? launch_cfg<128, 256, 2, 4, EPI, 32>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 32>(a, s);
+            if (narrow) return launch_cfg<64, 128, Q2A_GEMM_NARROW_WM, 2, EPI, 32>(a, s);
+            return big ? launch_cfg<128, 256, 2, 4, EPI, 32>(a, s) : launch_cfg<128, 128, Q2A_GEMM_SMALL_WM, 2, EPI, 32>(a, s);
         }
         if constexpr (EPI == Q2A_EPI_QKV || EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_STORE_F) {
             if (blk == Q2A_BLK_BF16) {
                 constexpr int B16 = Q2A_BLK_BF16;
                 if (p8) return launch_pipe8<EPI, B16>(a, s);
-                if (narrow) return launch_cfg<64, 128, 2, 2, EPI, B16>(a, s);
-                return big ? launch_cfg<256, 256, 2, 4, EPI, B16>(a, s) : launch_cfg<128, 128, 2, 2, EPI, B16>(a, s);
+                if (narrow) return launch_cfg<64, 128, Q2A_GEMM_NARROW_WM, 2, EPI, B16>(a, s);
+                return big ? launch_cfg<256, 256, 2, 4, EPI, B16>(a, s) : launch_cfg<128, 128, Q2A_GEMM_SMALL_WM, 2, EPI, B16>(a, s);
             }
         }
         return hipErrorInvalidValue;

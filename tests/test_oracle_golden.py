@@ -132,3 +132,24 @@ def test_oracle_encoder_other_clips(make_model, make_clip, golden, clip):
     out = o.encode(o.mel_window(o.log_mel(make_clip(clip))))
     mx, l2 = rel_errors(out[g["rows_stride5"]], g[f"tiny_f16_c{clip}_rows"])
     assert mx < 2e-4 and l2 < 5e-5, (mx, l2)
+
+
+def test_compact_gelu_lookup_equals_the_full_table():
+    """The GELU lookups that use only the |x| < 10 image of ggml's fp16 table (the GEMM epilogues' LDS table, and the
+    fc1 -> fc2 quantizer with Q2A_GELU_COMPACT): for every fp16 input h the selection `x >= 10 -> x; x <= -10 -> -0
+    (+0 for -inf, ggml's x <= -10 branch); else table_c[index(h)]` is bit for bit the full table (with the quantizer's
+    -inf -> +0 entry), exhaustively over all 65 536 inputs but the NaNs, which that kernel reads from the full table."""
+    tab = np.zeros(65536, dtype=np.uint16)
+    host_lib().q2a_make_gelu_table(tab.ctypes.data_as(C.c_void_p))
+    full = tab.copy()
+    full[0xFC00] = 0
+    HALF = 0x4901
+    comp = np.concatenate([tab[:HALF], tab[0x8000:0x8000 + HALF]])
+    u = np.arange(65536, dtype=np.uint32)
+    x = u.astype(np.uint16).view(np.float16).astype(np.float32)
+    idx = np.minimum(u & 0x7FFF, HALF - 1) + np.where(u & 0x8000, HALF, 0)
+    got = comp[idx]
+    got = np.where(x >= 10, u.astype(np.uint16), got)
+    got = np.where(x <= -10, np.where(np.isneginf(x), np.uint16(0), np.uint16(0x8000)), got)
+    ok = ~np.isnan(x)
+    assert np.array_equal(got[ok], full[ok])
