@@ -621,10 +621,15 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #define Q2A_KSTEP(B, S1, S2, S3, S4, V1, V2, V3, V4) Q2A_KSTEPC(B, S1, S2, S3, S4, (V1) - 2, (V2) - 2, (V3) - 2, (V4) - 2)
 #define Q2A_KSTEP_S(B, S1, S2, S3, S4, V1, V2, V3, V4) Q2A_KSTEPC(B, S1, S2, S3, S4, (V1) - 2, (V2) - 5, (V3) - 2, (V4) - 2)
 #else
+#ifndef Q2A_DIAG_SKIP_RA   // timing diagnostic (wrong results): 1 = phase 1's A reads skipped, 3 = phase 3's
+#define Q2A_DIAG_SKIP_RA 0
+#endif
+#define Q2A_RA1(B) do { if (Q2A_DIAG_SKIP_RA != 1 || p.K < 0) read_a(B, 0); } while (0)
+#define Q2A_RA3(B) do { if (Q2A_DIAG_SKIP_RA != 3 || p.K < 0) read_a(B, 1); } while (0)
 #define Q2A_KSTEP(B, S1, S2, S3, S4, V1, V2, V3, V4)                                      \
-    read_b(B, 0); read_a(B, 0); S1; Q2A_PB(V1); Q2A_U8U(); mma(0, 0); Q2A_PE();           \
+    read_b(B, 0); Q2A_RA1(B); S1; Q2A_PB(V1); Q2A_U8U(); mma(0, 0); Q2A_PE();             \
     read_b(B, 1);               S2; Q2A_PB(V2); mma(0, 1); Q2A_PE();                      \
-    read_a(B, 1);               S3; Q2A_PB(V3); Q2A_U8U(); mma(1, 1); Q2A_PE();           \
+    Q2A_RA3(B);                 S3; Q2A_PB(V3); Q2A_U8U(); mma(1, 1); Q2A_PE();           \
                                 S4; Q2A_PB(V4); mma(1, 0); Q2A_PE()
 #define Q2A_KSTEP_S Q2A_KSTEP   // (phase 2 also issues the block's 3 scale pieces)
 #endif
