@@ -92,6 +92,14 @@ __device__ __forceinline__ void q2a_st(const V & v, V * ptr) {
 #ifndef Q2A_GEMM_P2
 #define Q2A_GEMM_P2 0
 #endif
+// 8-phase kernel with the quadrant order alternating between K-steps and the next K-step's first B_q fragments read in
+// phase 4 (which otherwise reads nothing): fragment reads per phase 8 / 4 / 8 / 4 instead of 12 / 4 / 8 / 0, six
+// phases of glds in flight instead of five ("GEMM pipeline")
+// Measured round 5 (profiles/r05h_gemm_alternating_order.json): bit-identical; F16 fc1 -1 %, Q4_K +2-4 % and the
+// residual-epilogue kernels spill at 256 VGPRs (whole step +15-25 ms); not adopted
+#ifndef Q2A_GEMM_ALT
+#define Q2A_GEMM_ALT 0
+#endif
 
 // Timing diagnostic Q2A_DIAG_STAMPS=<epi>: the 8-phase kernels of epilogue <epi> record s_memtime at fixed points of
 // every workgroup's tile (waves 0 and 4, lane 0) into g_q2a_stamps, read back by q2a_diag_stamps (diag/tile_stamps.py):
@@ -634,6 +642,29 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #define Q2A_KSTEP_S Q2A_KSTEP   // (phase 2 also issues the block's 3 scale pieces)
 #endif
 
+#if Q2A_GEMM_ALT
+    // Alternating quadrant order. The first quadrant of a K-step needs both an A and a B half of the new k-slice; in
+    // the fixed order that is phase 1's 12-read burst (8 A + 4 B fragments), the critical path of the staggered
+    // pipeline (profiles/r05g_read_burst_and_backend.json), while phase 4 reads nothing. Here the even K-step runs
+    // (0,0) (0,1) (1,1) (1,0) and the odd one (0,1) (0,0) (1,0) (1,1): the B half an odd step starts with (B_q1) is free
+    // in registers during the even step's phase 4 and vice versa (B_q0), so phase 4 reads the NEXT K-step's first B
+    // half ("PF") and every phase reads 8 / 4 / 8 / 4 fragments with the same registers. Images of K-step t are
+    // first read in phase 4 of t-1 (Bf = the prefetched B half), 1 (A_q0), 2 (Bs = the other B half), 3 (A_q1) of t;
+    // each slot of buffer t%2 is restaged for t+2 the phase after its last read: Bf in phase 1, A_q0 in 2, Bs in 3,
+    // A_q1 in 4 of step t. Every image is then first read 7 (Bf) or 6 phases after its issue and must have landed
+    // by the wait before the phase preceding that read: vmcnt(12), six stages of 2 glds in flight.
+#define Q2A_KSTEP_E(B, S1, S2, S3, S4, V1, V2, V3, V4, PF)     \
+    read_a(B, 0); S1; Q2A_PB(V1); mma(0, 0); Q2A_PE();        \
+    read_b(B, 1); S2; Q2A_PB(V2); mma(0, 1); Q2A_PE();        \
+    read_a(B, 1); S3; Q2A_PB(V3); mma(1, 1); Q2A_PE();        \
+    PF;           S4; Q2A_PB(V4); mma(1, 0); Q2A_PE()
+#define Q2A_KSTEP_O(B, S1, S2, S3, S4, V1, V2, V3, V4, PF)     \
+    read_a(B, 0); S1; Q2A_PB(V1); mma(0, 1); Q2A_PE();        \
+    read_b(B, 0); S2; Q2A_PB(V2); mma(0, 0); Q2A_PE();        \
+    read_a(B, 1); S3; Q2A_PB(V3); mma(1, 0); Q2A_PE();        \
+    PF;           S4; Q2A_PB(V4); mma(1, 1); Q2A_PE()
+#define Q2A_NOPF (void) 0
+#endif
 #if Q2A_GEMM_P2
     // two phases per K-step, 32 MFMAs each (one barrier interval = one SIMD's 32 MFMAs beside its partner's reads):
     //   phase a: B_q0, B_q1, A_q0 fragments | stage A_q1 of step t+1        | mma(0,0), mma(0,1)
@@ -647,9 +678,17 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #endif
     // prologue: the images "phases 2..8 of iteration -1" would have staged (block 0's scales before them)
     if constexpr (BLK == 256) stage_scales(0);
+#if Q2A_GEMM_ALT
+    // the stages of "K-steps -2 and -1" in their issue order; the first two (B_q0, A_q0 of step 0) and the scales land
+    stage(0, 2, 0); stage(0, 0, 0); stage(0, 3, 0); stage(0, 1, 0);
+    stage(1, 3, 1); stage(1, 0, 1); stage(1, 2, 1); stage(1, 1, 1);
+    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+#else
     stage(0, 0, 0); stage(0, 2, 0); stage(0, 3, 0); stage(0, 1, 0);
     stage(1, 0, 1); stage(1, 2, 1); stage(1, 3, 1);
-#if Q2A_GEMM_P2
+#endif
+#if Q2A_GEMM_ALT
+#elif Q2A_GEMM_P2
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // A_q0, B_q0, B_q1 of step 0 (and block 0's scales) landed
 #else
     asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
@@ -663,7 +702,119 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     auto stagger_in = [&]() { if (Q2A_GEMM_WSTAGGER && wm == 1) { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); } };
     auto stagger_out = [&]() { if (Q2A_GEMM_WSTAGGER && wm == 0) { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); } };
 
-#if Q2A_GEMM_P2
+#if Q2A_GEMM_ALT
+    // glds per wave: 2 per phase, +3 block scales in phase 2 of a block's first K-step (K0), which stay younger than
+    // the waited-for stage for six waits (counts 15) and have landed by phase 1 of K2, so the next block's alpha is
+    // computed in phase 2 of K2. Persistent form: the previous tile's S_EPI epilogue stores sit between its last stage
+    // and this tile's first one, younger than the waited-for stage for the first six waits (+16).
+    if constexpr (BLK == 0) {
+        read_b(0, 0);
+        stagger_in();
+        int kt = 0;
+        for (; kt < nk - 2; kt += 2) {
+            Q2A_KSTEP_E(0, stage(0, 2, kt + 2), stage(0, 0, kt + 2), stage(0, 3, kt + 2), stage(0, 1, kt + 2), 12, 12, 12, 12, read_b(1, 1));
+            Q2A_KSTEP_O(1, stage(1, 3, kt + 3), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 1, kt + 3), 12, 12, 12, 12, read_b(0, 0));
+        }
+        Q2A_KSTEP_E(0, stage_tail(0, 2), stage_tail(0, 0), stage_tail(0, 3), stage_tail(0, 1), 12, 12, 12, 12, read_b(1, 1));
+        Q2A_KSTEP_O(1, stage_tail(1, 3), stage_tail(1, 0), stage_tail(1, 2), stage_tail(1, 1), 12, 12, 12, 12, Q2A_NOPF);
+    } else if constexpr (PERS) {
+        static_assert(BLK == 256, "persistent 8-phase loop: Q4_K only");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        alpha_compute();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        // the first tile's B_q0 half; every later tile's is read by the previous tile's last phase 4 and carried across
+        // its epilogue in registers (reading it here instead would race the other half's phase-1 restage of that slot)
+        read_b(0, 0);
+        stagger_in();
+        for (;;) {
+            int m0n = 0, n0n = 0;
+            const bool has_next = next(m0n, n0n);
+            auto stage_next = [&](int b, int h) { stage(b, h, has_next ? b : nk - 1); };
+            int kt = 0;
+            BS_T0();
+            block_start(std::true_type{});
+            BS_T1();
+            asm volatile("" ::: "memory");
+            Q2A_KSTEP_E(0, stage(0, 2, 2), (stage(0, 0, 2), stage_scales(1)), stage(0, 3, 2), stage(0, 1, 2), 28, 31, 31, 31, read_b(1, 1));
+            Q2A_KSTEP_O(1, stage(1, 3, 3), stage(1, 0, 3), stage(1, 2, 3), stage(1, 1, 3), 31, 31, 15, 15, read_b(0, 0));
+            Q2A_KSTEP_E(0, stage(0, 2, 4), (alpha_compute(), stage(0, 0, 4)), stage(0, 3, 4), stage(0, 1, 4), 12, 12, 12, 12, read_b(1, 1));
+            Q2A_KSTEP_O(1, stage(1, 3, 5), stage(1, 0, 5), stage(1, 2, 5), stage(1, 1, 5), 12, 12, 12, 12, read_b(0, 0));
+            for (kt = 4; kt < nk - 4; kt += 4) {
+                BS_T0();
+                block_start(std::false_type{});
+                BS_T1();
+                asm volatile("" ::: "memory");
+                Q2A_KSTEP_E(0, stage(0, 2, kt + 2), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 3, kt + 2),
+                            stage(0, 1, kt + 2), 12, 15, 15, 15, read_b(1, 1));
+                Q2A_KSTEP_O(1, stage(1, 3, kt + 3), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 1, kt + 3), 15, 15, 15, 15,
+                            read_b(0, 0));
+                Q2A_KSTEP_E(0, stage(0, 2, kt + 4), (alpha_compute(), stage(0, 0, kt + 4)), stage(0, 3, kt + 4), stage(0, 1, kt + 4),
+                            12, 12, 12, 12, read_b(1, 1));
+                Q2A_KSTEP_O(1, stage(1, 3, kt + 5), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 1, kt + 5), 12, 12, 12, 12,
+                            read_b(0, 0));
+            }
+            prep_scales_last(has_next, m0n, n0n);
+            BS_T0();
+            block_start(std::false_type{});   // (nk >= 8: the last block is never block 0)
+            BS_T1();
+            asm volatile("" ::: "memory");
+            Q2A_KSTEP_E(0, stage(0, 2, kt + 2), (stage(0, 0, kt + 2), stage_scales_last()), stage(0, 3, kt + 2), stage(0, 1, kt + 2),
+                        12, 15, 15, 15, read_b(1, 1));
+            Q2A_KSTEP_O(1, stage(1, 3, kt + 3), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 1, kt + 3), 15, 15, 15, 15,
+                        read_b(0, 0));
+            // the last two K-steps stage the next tile's first two
+            Q2A_KSTEP_E(0, ((has_next ? set_offsets(m0n, n0n) : (void) 0), stage_next(0, 2)), stage_next(0, 0), stage_next(0, 3),
+                        stage_next(0, 1), 12, 12, 12, 12, read_b(1, 1));
+            Q2A_KSTEP_O(1, stage_next(1, 3), stage_next(1, 0), stage_next(1, 2), stage_next(1, 1), 12, 12, 12, 12, read_b(0, 0));
+            __builtin_amdgcn_sched_barrier(0);
+            epi(acc, m0, n0);
+            __builtin_amdgcn_sched_barrier(0);
+            if (!has_next) break;
+            m0 = m0n;
+            n0 = n0n;
+        }
+    } else {
+        static_assert(BLK == 256, "8-phase k-quant loop is Q4_K only");
+        alpha_compute();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        read_b(0, 0);
+        stagger_in();
+        int kt = 0;
+        for (; kt < nk - 4; kt += 4) {
+            BS_T0();
+            if (kt == 0) block_start(std::true_type{});
+            else block_start(std::false_type{});
+            BS_T1();
+            asm volatile("" ::: "memory");
+            Q2A_KSTEP_E(0, stage(0, 2, kt + 2), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 3, kt + 2),
+                        stage(0, 1, kt + 2), 12, 15, 15, 15, read_b(1, 1));
+            Q2A_KSTEP_O(1, stage(1, 3, kt + 3), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 1, kt + 3), 15, 15, 15, 15,
+                        read_b(0, 0));
+            Q2A_KSTEP_E(0, stage(0, 2, kt + 4), (alpha_compute(), stage(0, 0, kt + 4)), stage(0, 3, kt + 4), stage(0, 1, kt + 4),
+                        12, 12, 12, 12, read_b(1, 1));
+            Q2A_KSTEP_O(1, stage(1, 3, kt + 5), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 1, kt + 5), 12, 12, 12, 12,
+                        read_b(0, 0));
+        }
+        BS_T0();
+        if (kt == 0) block_start(std::true_type{});
+        else block_start(std::false_type{});
+        BS_T1();
+        asm volatile("" ::: "memory");
+        Q2A_KSTEP_E(0, stage(0, 2, kt + 2), (stage(0, 0, kt + 2), stage_scales(kt / 4)), stage(0, 3, kt + 2), stage(0, 1, kt + 2),
+                    12, 15, 15, 15, read_b(1, 1));
+        Q2A_KSTEP_O(1, stage(1, 3, kt + 3), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 1, kt + 3), 15, 15, 15, 15,
+                    read_b(0, 0));
+        Q2A_KSTEP_E(0, stage_tail(0, 2), stage_tail(0, 0), stage_tail(0, 3), stage_tail(0, 1), 12, 12, 12, 12, read_b(1, 1));
+        Q2A_KSTEP_O(1, stage_tail(1, 3), stage_tail(1, 0), stage_tail(1, 2), stage_tail(1, 1), 12, 12, 12, 12, Q2A_NOPF);
+    }
+#undef Q2A_KSTEP_E
+#undef Q2A_KSTEP_O
+#undef Q2A_NOPF
+#elif Q2A_GEMM_P2
     // glds stream per wave and K-step t: phase a {A_q1(t+1)} 2, phase b {A_q0, B_q0, B_q1 (t+2)} 6 (+3 block scales in
     // phase b of a block's first K-step). Steady count 8; the scale pieces raise the next three waits to 11 (they are
     // retired by phase a of the block's third K-step, whose phase b computes the next block's alpha from them).
