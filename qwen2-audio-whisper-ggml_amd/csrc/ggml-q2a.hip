@@ -454,7 +454,11 @@ __global__ void k_attn_prep(tview q, tview k, tview v, _Float16 * qh, _Float16 *
     const int d = (int) (i & 63);
     const int r = (int) (i >> 6);
     const int t = r % T, h = r / T;
-    const float qv = *(const float *) (q.base + voff(q, d, t, h, 0)) * Q2A_LOG2E;   // the attention's log2 units
+    float qv = *(const float *) (q.base + voff(q, d, t, h, 0)) * Q2A_LOG2E;   // the attention's log2 units
+    // the product rounded to f32 first, then split (as the QKV GEMM epilogue does): left to itself the compiler
+    // rounds q * log2e to fp16 in one mixed-precision op, which at an f32 value on an fp16 tie picks the other half
+    // (128 of 1.92 M Q elements of a full-size layer; diag/gpurun_r05m.sh)
+    asm volatile("" : "+v"(qv));
     const float kv = *(const float *) (k.base + voff(k, d, t, h, 0));
     const int64_t o = (int64_t) t * H * 64 + h * 64 + d;
     const _Float16 a = (_Float16) qv, b = (_Float16) kv;
@@ -579,6 +583,8 @@ struct q2a_backend_ctx {
     void * scratch = nullptr;
     _Float16 * vt_buf = nullptr;       // V^T operand of the fused attention, written at the V CONT node
     size_t vt_bytes = 0;
+    char * qkv_buf = nullptr;          // attention operands written by the fused Q|K|V GEMM (run_qkv_fused)
+    size_t qkv_bytes = 0;
     // fp16 shadows of f32 activations written by their producer (LayerNorm, fc1 GELU epilogue) for F16-weight
     // MUL_MATs that would otherwise convert them: two slots, a producer never writes the slot its own GEMM reads
     _Float16 * a16[2] = {nullptr, nullptr};
@@ -883,29 +889,23 @@ struct mm_second {         // the second GEMM of a grouped launch (same activati
     float oscale;
 };
 
-// epi: Q2A_EPI_STORE_F (bias optional), Q2A_EPI_GELU_F (bias, GELU), Q2A_EPI_RESID (bias, + resid rows); the result
-// goes to `out` (op itself, or the last node of a fused MUL_MAT -> ADD [-> GELU | ADD] chain)
-void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = nullptr, int epi = Q2A_EPI_STORE_F,
-                 const float * bias = nullptr, const float * resid = nullptr, float oscale = 0.0f,
-                 _Float16 * out16 = nullptr, const mm_second * sec = nullptr) {
-    if (!out) out = op;
-    const ggml_tensor * w = op->src[0];
-    const ggml_tensor * x = op->src[1];
-    const int K = (int) w->ne[0], N = (int) w->ne[1];
-    const int M = (int) (x->ne[1] * x->ne[2] * x->ne[3]);
-    const int blk = w->type == GGML_TYPE_Q4_K ? 256 : w->type == GGML_TYPE_F16 ? 0 : 32;
+// the activation operand of a fast MUL_MAT, in the scratch: fp16 rows (F16 weights; the producer's fp16 shadow when it
+// wrote one) or Q8_K / Q8_0 codes with their block scales (dy [K/blk][MP], and for Q8_K the bsum operand aext
+// [K/256][MP][16]); `extra` more scratch bytes follow it (returned in .extra)
+struct act_operand {
+    const q2a_half * A;
+    float * dy;
+    q2a_half * aext;
+    int MP;
+    char * extra;
+};
+act_operand activation_operand(q2a_backend_ctx * b, const ggml_tensor * x, int M, int K, int blk, size_t extra) {
     const int MP = (M + 255) / 256 * 256;
-    // scratch: A operand fp16 [M][K] | dy [K/blk][MP] | aext [K/256][MP][16]
+    // scratch: A operand fp16 [M][K] | dy [K/blk][MP] | aext [K/256][MP][16] | extra
     const size_t a_bytes = ((size_t) M * K * 2 + 255) & ~size_t(255);
     const size_t dy_bytes = blk ? ((size_t) (K / blk) * MP * 4 + 255) & ~size_t(255) : 0;
     const size_t ae_bytes = blk == 256 ? (size_t) (K / 256) * MP * 32 : 0;
-    // fp16 small-tile GEMMs (a single clip) split K like the engine's residual GEMMs (q2a_gemm_resid_ksplit: up to
-    // 4 partial [M][N] f32 planes, reduced in split order with the bias / residual / scale of the epilogue)
-    const int nsplit = sec || !(epi == Q2A_EPI_RESID || epi == Q2A_EPI_STORE_F) ? 0
-                       : blk == 0 ? q2a_gemm_resid_ksplit(M, N, K, 0) : q2a_gemm_kq_ksplit(M, N, K, blk);
-    const bool split = nsplit > 1;
-    const size_t part_bytes = split ? (size_t) nsplit * M * N * 4 : 0;
-    char * s = (char *) scratch(b, a_bytes + dy_bytes + ae_bytes + part_bytes);
+    char * s = (char *) scratch(b, a_bytes + dy_bytes + ae_bytes + extra);
     q2a_half * A = (q2a_half *) s;
     float * dy = (float *) (s + a_bytes);
     q2a_half * aext = (q2a_half *) (s + a_bytes + dy_bytes);
@@ -928,9 +928,30 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
     // the same activation (the Q, K, V projections) reuses it; an fp16 conversion overwrote it
     b->quant_src = blk ? x : nullptr;
     b->quant_blk = blk;
+    return {A, dy, aext, MP, s + a_bytes + dy_bytes + ae_bytes};
+}
+
+// epi: Q2A_EPI_STORE_F (bias optional), Q2A_EPI_GELU_F (bias, GELU), Q2A_EPI_RESID (bias, + resid rows); the result
+// goes to `out` (op itself, or the last node of a fused MUL_MAT -> ADD [-> GELU | ADD] chain)
+void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = nullptr, int epi = Q2A_EPI_STORE_F,
+                 const float * bias = nullptr, const float * resid = nullptr, float oscale = 0.0f,
+                 _Float16 * out16 = nullptr, const mm_second * sec = nullptr) {
+    if (!out) out = op;
+    const ggml_tensor * w = op->src[0];
+    const ggml_tensor * x = op->src[1];
+    const int K = (int) w->ne[0], N = (int) w->ne[1];
+    const int M = (int) (x->ne[1] * x->ne[2] * x->ne[3]);
+    const int blk = w->type == GGML_TYPE_Q4_K ? 256 : w->type == GGML_TYPE_F16 ? 0 : 32;
+    // fp16 small-tile GEMMs (a single clip) split K like the engine's residual GEMMs (q2a_gemm_resid_ksplit: up to
+    // 4 partial [M][N] f32 planes, reduced in split order with the bias / residual / scale of the epilogue)
+    const int nsplit = sec || !(epi == Q2A_EPI_RESID || epi == Q2A_EPI_STORE_F) ? 0
+                       : blk == 0 ? q2a_gemm_resid_ksplit(M, N, K, 0) : q2a_gemm_kq_ksplit(M, N, K, blk);
+    const bool split = nsplit > 1;
+    const size_t part_bytes = split ? (size_t) nsplit * M * N * 4 : 0;
+    const act_operand ao = activation_operand(b, x, M, K, blk, part_bytes);
     q2a_gemm_args a;
     memset(&a, 0, sizeof(a));
-    a.A = A; a.lda = K; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
+    a.A = ao.A; a.lda = K; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
     a.M = M; a.N = N; a.K = K; a.ldw = K;
     a.outF = (float *) out->data; a.ldo = N;
     a.bias = bias; a.store_bias = bias != nullptr; a.resid = resid; a.out_scale = oscale;
@@ -952,7 +973,7 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
         }
     }
     if (split) {
-        a.part = (float *) (s + a_bytes + dy_bytes + ae_bytes);
+        a.part = (float *) ao.extra;
         a.split_stride = (int64_t) M * N;
         a.split_store = 1;
         a.split_kq = 1;
@@ -966,13 +987,13 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
         a.W = (const q2a_half *) (base + p.off[0]);
         a.nblk = K / blk;
         a.dx = (const float *) (base + p.off[1]);
-        a.dy = dy; a.dy_ld = MP;
+        a.dy = ao.dy; a.dy_ld = ao.MP;
         if (blk == 256) {
             a.dmin = (const float *) (base + p.off[2]);
             a.wext = (const q2a_half *) (base + p.off[3]);
             a.beta = (const float *) (base + p.off[4]);
             a.gamma = (const float *) (base + p.off[5]);
-            a.aext = aext;
+            a.aext = ao.aext;
         }
     }
     Q2A_HIP(q2a_launch_gemm(a, epi, blk, b->stream));
@@ -1188,7 +1209,12 @@ _Float16 * claim_a16(q2a_backend_ctx * b, const ggml_tensor * t) {
 // vt_ready: V^T was already written into b->vt_buf at V's CONT node. merged: the CONT of permute(KQV, 0,2,1,3)
 // that follows (qwen2-whisper.cpp:2105-2107), whose [t][h*64+d] rows are exactly the fused kernel's output rows —
 // the kernel writes them there directly. Returns the number of nodes consumed.
-int run_fused_attention(q2a_backend_ctx * b, ggml_cgraph * g, int i, bool vt_ready, ggml_tensor * merged) {
+struct qkv_ops {                   // the attention operands as the fused Q|K|V GEMM wrote them (qkv_buffer layout)
+    _Float16 *qh, *ql, *kh, *kl, *vt, *vtl;
+};
+
+int run_fused_attention(q2a_backend_ctx * b, ggml_cgraph * g, int i, bool vt_ready, ggml_tensor * merged,
+                        const qkv_ops * ready = nullptr) {
     ggml_tensor * kq = ggml_graph_node(g, i);
     ggml_tensor * kqv = ggml_graph_node(g, i + 2);
     const ggml_tensor * K = kq->src[0];
@@ -1201,6 +1227,51 @@ int run_fused_attention(q2a_backend_ctx * b, ggml_cgraph * g, int i, bool vt_rea
     const bool vlo = q2a_attention_wants_vlo();
     const size_t vb1 = ((size_t) H * 64 * TP * 2 + 255) & ~size_t(255);
     const size_t vb = vlo ? 2 * vb1 : vb1;   // V^T [| V^T lo]
+#ifdef Q2A_DIAG_DUMP_ATTN   // diagnostic builds only: the first attention's operands of a process -> $Q2A_DUMP_ATTN
+    auto dump = [&](const _Float16 * qh, const _Float16 * ql, const _Float16 * kh, const _Float16 * kl, const _Float16 * vt,
+                    const _Float16 * vtl) {
+        static bool done = false;
+        const char * path = getenv("Q2A_DUMP_ATTN");
+        if (done || !path) return;
+        done = true;
+        Q2A_HIP(hipStreamSynchronize(b->stream));
+        FILE * f = fopen(path, "wb");
+        const size_t nq = (size_t) n * 2, nv = (size_t) H * 64 * TP * 2;
+        std::vector<char> h(std::max(nq, nv));
+        for (const _Float16 * x : {qh, ql, kh, kl}) { Q2A_HIP(hipMemcpy(h.data(), x, nq, hipMemcpyDeviceToHost)); fwrite(h.data(), 1, nq, f); }
+        for (const _Float16 * x : {vt, vtl}) { if (!x) continue; Q2A_HIP(hipMemcpy(h.data(), x, nv, hipMemcpyDeviceToHost)); fwrite(h.data(), 1, nv, f); }
+        fclose(f);
+    };
+    if (ready) dump(ready->qh, ready->ql, ready->kh, ready->kl, ready->vt, ready->vtl);
+    {   // the Q tensor the separate route feeds its operand pass (f32 [T][D]) -> $Q2A_DUMP_ATTN.q
+        static bool qdone = false;
+        const char * path = getenv("Q2A_DUMP_ATTN");
+        if (!ready && !qdone && path) {
+            qdone = true;
+            Q2A_HIP(hipStreamSynchronize(b->stream));
+            std::vector<float> h((size_t) n);
+            Q2A_HIP(hipMemcpy(h.data(), Q->data, (size_t) n * 4, hipMemcpyDeviceToHost));
+            FILE * f = fopen((std::string(path) + ".q").c_str(), "wb");
+            fwrite(h.data(), 4, h.size(), f);
+            fclose(f);
+        }
+    }
+#define Q2A_DUMP_PREP() dump(qh, ql, kh, kl, vt, vtl)
+#else
+#define Q2A_DUMP_PREP() do { } while (0)
+#endif
+    if (ready) {   // operands already in place (run_qkv_fused): only the kernel (and the output re-layout) runs
+        float * o = merged ? (float *) merged->data : (float *) scratch(b, (size_t) n * 4);
+        if (!merged) b->quant_src = nullptr;
+        q2a_attn_args at{(const q2a_half *) ready->qh, (const q2a_half *) ready->ql, (const q2a_half *) ready->kh,
+                         (const q2a_half *) ready->kl, (const q2a_half *) ready->vt, 1, (int) T, (int) D, (int) H, TP, nullptr, o};
+        at.vtl = ready->vtl;
+        Q2A_HIP(q2a_launch_attention(at, b->stream));
+        if (!merged)
+            hipLaunchKernelGGL(k_attn_out, grid1(n), dim3(256), 0, b->stream, (const float *) o, tv(kqv), (int) T, (int) H, n);
+        b->stats.n_attn_fused++;
+        return merged ? 5 : 3;
+    }
     char * s = (char *) scratch(b, 4 * hb + vb + (size_t) n * 4);
     b->quant_src = nullptr;   // the attention operands overwrite the scratch
     _Float16 *qh = (_Float16 *) s, *ql = (_Float16 *) (s + hb), *kh = (_Float16 *) (s + 2 * hb), *kl = (_Float16 *) (s + 3 * hb);
@@ -1215,6 +1286,8 @@ int run_fused_attention(q2a_backend_ctx * b, ggml_cgraph * g, int i, bool vt_rea
         hipLaunchKernelGGL(k_attn_prep<true>, grid1(n), dim3(256), 0, b->stream, tv(Q), tv(K), tv(V), qh, ql, kh, kl, vt,
                            vtl, (int) T, (int) H, TP, n);
     }
+    Q2A_DUMP_PREP();
+#undef Q2A_DUMP_PREP
     q2a_attn_args at{(const q2a_half *) qh, (const q2a_half *) ql, (const q2a_half *) kh, (const q2a_half *) kl,
                      (const q2a_half *) vt, 1, (int) T, (int) D, (int) H, TP, nullptr, o};
     at.vtl = vtl;
@@ -1223,6 +1296,186 @@ int run_fused_attention(q2a_backend_ctx * b, ggml_cgraph * g, int i, bool vt_rea
         hipLaunchKernelGGL(k_attn_out, grid1(n), dim3(256), 0, b->stream, (const float *) o, tv(kqv), (int) T, (int) H, n);
     b->stats.n_attn_fused++;
     return merged ? 5 : 3;
+}
+
+// ---- the Q | K | V projections as ONE GEMM whose epilogue writes the fused attention's operands (the engine's
+// Q2A_EPI_QKV: Q (+bias) * scale * log2 e and K as fp16 hi/lo pairs, V (+bias) as V^T [h][d][TP] hi (| lo)), replacing
+// two launches (K|Q grouped, V), the V^T tile pass at V's CONT and the attention's operand pass
+// (qwen2-whisper.cpp:2029-2054 projections, :2052-2089 the attention's K, Q, V views)
+struct qkv_route {
+    ggml_tensor * mm[3];            // Q, K, V MUL_MATs (same activation, same weight type and shape)
+    const ggml_tensor * bq, * bv;   // bias rows of Q and V (the reference's K has none, :2039)
+    float qscale;                   // ggml_scale after Q's bias (a power of two: KQscale = 1/8 for heads of 64)
+};
+
+// the weights as one [3N][K] operand: fp16 rows concatenated (F16), or the three packed images' sections concatenated
+// along N (every section of q2a_pack_linear's layout is row- or block-major over N, so this IS the packed image of the
+// concatenated rows). Cached with the repacks under a key spanning the three source tensors: a write to any drops it.
+packed_w get_qkv_weight(q2a_backend_ctx * b, const ggml_tensor * const w[3]) {
+    const int TAG = -64 - (int) w[0]->type;   // cache tag (not a ggml type)
+    const int N = (int) w[0]->ne[1], K = (int) w[0]->ne[0];
+    const char * lo = (const char *) w[0]->data, * hi = lo + ggml_nbytes(w[0]);
+    for (int i = 1; i < 3; ++i) {
+        lo = std::min(lo, (const char *) w[i]->data);
+        hi = std::max(hi, (const char *) w[i]->data + ggml_nbytes(w[i]));
+    }
+    q2a_device_ctx * d = dev_ctx(b->device);
+    {
+        std::lock_guard<std::mutex> lk(d->mu);
+        for (const packed_w & p : d->wcache)
+            if (p.raw == lo && p.raw_bytes == (size_t) (hi - lo) && p.type == TAG && p.N == 3 * N && p.K == K) return p;
+    }
+    packed_w p{};
+    p.raw = lo; p.raw_bytes = (size_t) (hi - lo); p.type = TAG; p.N = 3 * N; p.K = K;
+    Q2A_HIP(hipStreamSynchronize(b->stream));
+    if (w[0]->type == GGML_TYPE_F16) {
+        const size_t rb = (size_t) N * K * 2;
+        Q2A_HIP(hipMalloc(&p.dev, 3 * rb));
+        for (int i = 0; i < 3; ++i) Q2A_HIP(hipMemcpyAsync((char *) p.dev + i * rb, w[i]->data, rb, hipMemcpyDeviceToDevice, b->stream));
+    } else {
+        const int blk = w[0]->type == GGML_TYPE_Q4_K ? 256 : 32, nblk = K / blk;
+        const uint64_t bytes = q2a_pack_layout(w[0]->type, 3 * N, K, p.off);
+        if (!bytes) GGML_ABORT("ggml-q2a: cannot pack the Q|K|V weights of %s", w[0]->name);
+        Q2A_HIP(hipMalloc(&p.dev, bytes));
+        char * dst = (char *) p.dev;
+        for (int i = 0; i < 3; ++i) {
+            const packed_w s = get_packed(b, w[i]);
+            const char * src = (const char *) s.dev;
+            Q2A_HIP(hipMemcpyAsync(dst + p.off[0] + (size_t) i * N * K * 2, src + s.off[0], (size_t) N * K * 2,
+                                   hipMemcpyDeviceToDevice, b->stream));
+            // block-major sections [nblk][N] x element bytes: dx (and dmin, wext (16 halves), beta, gamma for Q4_K)
+            const int secs[5] = {1, 2, 3, 4, 5};
+            const int esz[6] = {0, 4, 4, 32, 4, 4};
+            for (int k = 0; k < (blk == 256 ? 5 : 1); ++k) {
+                const int sc = secs[k];
+                const size_t e = (size_t) esz[sc];
+                Q2A_HIP(hipMemcpy2DAsync(dst + p.off[sc] + i * N * e, 3 * N * e, src + s.off[sc], N * e, N * e, nblk,
+                                         hipMemcpyDeviceToDevice, b->stream));
+            }
+        }
+    }
+    Q2A_HIP(hipStreamSynchronize(b->stream));
+    std::lock_guard<std::mutex> lk(d->mu);
+    d->wcache.push_back(p);
+    return p;
+}
+
+// [bq | 0 | bv] as one f32 bias row (cached like the weights)
+const float * get_qkv_bias(q2a_backend_ctx * b, const ggml_tensor * bq, const ggml_tensor * bv, int N) {
+    const int TAG = -200;
+    const char * lo = std::min((const char *) bq->data, (const char *) bv->data);
+    const char * hi = std::max((const char *) bq->data + ggml_nbytes(bq), (const char *) bv->data + ggml_nbytes(bv));
+    q2a_device_ctx * d = dev_ctx(b->device);
+    {
+        std::lock_guard<std::mutex> lk(d->mu);
+        for (const packed_w & p : d->wcache)
+            if (p.raw == lo && p.raw_bytes == (size_t) (hi - lo) && p.type == TAG && p.N == 3 * N) return (const float *) p.dev;
+    }
+    packed_w p{};
+    p.raw = lo; p.raw_bytes = (size_t) (hi - lo); p.type = TAG; p.N = 3 * N; p.K = 1;
+    Q2A_HIP(hipStreamSynchronize(b->stream));
+    Q2A_HIP(hipMalloc(&p.dev, (size_t) 3 * N * 4));
+    Q2A_HIP(hipMemsetAsync(p.dev, 0, (size_t) 3 * N * 4, b->stream));
+    Q2A_HIP(hipMemcpyAsync(p.dev, bq->data, (size_t) N * 4, hipMemcpyDeviceToDevice, b->stream));
+    Q2A_HIP(hipMemcpyAsync((char *) p.dev + (size_t) 2 * N * 4, bv->data, (size_t) N * 4, hipMemcpyDeviceToDevice, b->stream));
+    Q2A_HIP(hipStreamSynchronize(b->stream));
+    std::lock_guard<std::mutex> lk(d->mu);
+    d->wcache.push_back(p);
+    return (const float *) p.dev;
+}
+
+// the operand buffer (zero-filled when it grows: V^T's columns t >= T are read as zero weights)
+char * qkv_buffer(q2a_backend_ctx * b, size_t bytes) {
+    if (bytes > b->qkv_bytes) {
+        abort_capture(b);
+        Q2A_HIP(hipStreamSynchronize(b->stream));
+        if (b->qkv_buf) Q2A_HIP(hipFree(b->qkv_buf));
+        b->qkv_buf = nullptr;
+        Q2A_HIP(hipMalloc((void **) &b->qkv_buf, bytes));
+        Q2A_HIP(hipMemsetAsync(b->qkv_buf, 0, bytes, b->stream));
+        Q2A_HIP(hipStreamSynchronize(b->stream));
+        b->qkv_bytes = bytes;
+        drop_graphs(b);
+        resume_discard(b);
+    }
+    return b->qkv_buf;
+}
+
+// V^T columns T <= t < TP of every (h, d) row -> 0 (a buffer last used with a larger T keeps finite old values there;
+// they meet P = 0 only, but a stale inf would make 0 * inf)
+__global__ void k_vt_tail_zero(_Float16 * vt, _Float16 * vtl, int rows, int T, int TP) {
+    const int w = TP - T;
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (int64_t) rows * w) return;
+    const int64_t o = (i / w) * TP + T + i % w;
+    vt[o] = (_Float16) 0.0f;
+    if (vtl) vtl[o] = (_Float16) 0.0f;
+}
+
+void run_qkv_fused(q2a_backend_ctx * b, const qkv_route & r, qkv_ops & ops) {
+    const ggml_tensor * x = r.mm[0]->src[1];
+    const int K = (int) x->ne[0], M = (int) x->ne[1], D = (int) r.mm[0]->src[0]->ne[1], H = D / 64, T = M;
+    const int TP = (T + 63) / 64 * 64;
+    const ggml_tensor * const w[3] = {r.mm[0]->src[0], r.mm[1]->src[0], r.mm[2]->src[0]};
+    const int blk = w[0]->type == GGML_TYPE_Q4_K ? 256 : w[0]->type == GGML_TYPE_F16 ? 0 : 32;
+    const packed_w pw = get_qkv_weight(b, w);
+    const float * bias = get_qkv_bias(b, r.bq, r.bv, D);
+    const bool vlo = q2a_attention_wants_vlo();
+    const size_t hb = ((size_t) T * D * 2 + 255) & ~size_t(255);
+    const size_t vb1 = ((size_t) D * TP * 2 + 255) & ~size_t(255);
+    char * ob = qkv_buffer(b, 4 * hb + (vlo ? 2 : 1) * vb1);
+    ops = {(_Float16 *) ob, (_Float16 *) (ob + hb), (_Float16 *) (ob + 2 * hb), (_Float16 *) (ob + 3 * hb),
+           (_Float16 *) (ob + 4 * hb), vlo ? (_Float16 *) (ob + 4 * hb + vb1) : nullptr};
+    const act_operand ao = activation_operand(b, x, M, K, blk, 0);
+    if (TP > T) {
+        const int64_t n = (int64_t) D * (TP - T);
+        hipLaunchKernelGGL(k_vt_tail_zero, grid1(n), dim3(256), 0, b->stream, ops.vt, ops.vtl, D, T, TP);
+    }
+    q2a_gemm_args a;
+    memset(&a, 0, sizeof(a));
+    a.A = ao.A; a.lda = K; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
+    a.M = M; a.N = 3 * D; a.K = K; a.ldw = K;
+    a.bias = bias;
+    a.qh = (q2a_half *) ops.qh; a.ql = (q2a_half *) ops.ql; a.kh = (q2a_half *) ops.kh; a.kl = (q2a_half *) ops.kl;
+    a.vt = (q2a_half *) ops.vt; a.vtl = (q2a_half *) ops.vtl;
+    a.T = T; a.D = D; a.H = H; a.TP = TP;
+    // (x + b) * s then * log2 e in the unfused path; s = 2^-k makes one multiply by s * log2 e the same rounding
+    a.qscale = r.qscale * Q2A_LOG2E;
+    a.gelu_tab = gelu_table(b->device);
+    const char * base = (const char *) pw.dev;
+    a.W = (const q2a_half *) (base + pw.off[0]);
+    if (blk) {
+        a.nblk = K / blk;
+        a.dx = (const float *) (base + pw.off[1]);
+        a.dy = ao.dy; a.dy_ld = ao.MP;
+        if (blk == 256) {
+            a.dmin = (const float *) (base + pw.off[2]);
+            a.wext = (const q2a_half *) (base + pw.off[3]);
+            a.beta = (const float *) (base + pw.off[4]);
+            a.gamma = (const float *) (base + pw.off[5]);
+            a.aext = ao.aext;
+        }
+    }
+    Q2A_HIP(q2a_launch_gemm(a, Q2A_EPI_QKV, blk, b->stream));
+#ifdef Q2A_DIAG_DUMP_ATTN   // diagnostic builds only: (acc + bias) * qscale of the same GEMM as f32 -> $Q2A_DUMP_ATTN.q
+    static bool qdone = false;
+    const char * path = getenv("Q2A_DUMP_ATTN");
+    if (!qdone && path) {
+        qdone = true;
+        float * y = nullptr;
+        Q2A_HIP(hipMalloc((void **) &y, (size_t) M * 3 * D * 4));
+        q2a_gemm_args c = a;
+        c.outF = y; c.ldo = 3 * D; c.store_bias = 1; c.out_scale = r.qscale;
+        Q2A_HIP(q2a_launch_gemm(c, Q2A_EPI_STORE_F, blk, b->stream));
+        Q2A_HIP(hipStreamSynchronize(b->stream));
+        std::vector<float> h((size_t) M * 3 * D);
+        Q2A_HIP(hipMemcpy(h.data(), y, h.size() * 4, hipMemcpyDeviceToHost));
+        FILE * f = fopen((std::string(path) + ".q").c_str(), "wb");
+        for (int m = 0; m < M; ++m) fwrite(h.data() + (size_t) m * 3 * D, 4, D, f);
+        fclose(f);
+        Q2A_HIP(hipFree(y));
+    }
+#endif
 }
 
 bool op_supported(const ggml_tensor * op) {
@@ -1371,6 +1624,89 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                 vprep[V] = j;
         }
     }
+    // Q | K | V projections feeding a fused attention through exactly the reference's views (qwen2-whisper.cpp:
+    // 2029-2089): K = PERMUTE(RESHAPE(MUL_MAT)), Q = PERMUTE(SCALE(RESHAPE(ADD(MUL_MAT, bq)))),
+    // V = CONT(PERMUTE(RESHAPE(ADD(MUL_MAT, bv)))), every link its producer's sole consumer, the three MUL_MATs on one
+    // activation with weights of one type and shape in a weights buffer: one GEMM (run_qkv_fused) then replaces
+    // them, and the attention reads its operands from it
+    static const bool no_qkv = [] { const char * v = getenv("GGML_Q2A_NO_FUSED_QKV"); return v && atoi(v); }();
+    auto match_qkv = [&](ggml_tensor * kq, ggml_tensor * kqv, qkv_route & r, std::vector<const ggml_tensor *> & absorbed) {
+        auto is = [](const ggml_tensor * t, ggml_op o) { return t && t->op == o; };
+        ggml_tensor * kp = kq->src[0];
+        if (!is(kp, GGML_OP_PERMUTE) || !sole(kp, kq)) return false;
+        ggml_tensor * kr = kp->src[0];
+        if (!is(kr, GGML_OP_RESHAPE) || !sole(kr, kp)) return false;
+        ggml_tensor * km = kr->src[0];
+        if (!is(km, GGML_OP_MUL_MAT) || !sole(km, kr)) return false;
+        ggml_tensor * qp = kq->src[1];
+        if (!is(qp, GGML_OP_PERMUTE) || !sole(qp, kq)) return false;
+        ggml_tensor * qs = qp->src[0];
+        if (!is(qs, GGML_OP_SCALE) || !sole(qs, qp)) return false;
+        ggml_tensor * qr = qs->src[0];
+        if (!is(qr, GGML_OP_RESHAPE) || !sole(qr, qs)) return false;
+        ggml_tensor * qa = qr->src[0];
+        if (!is(qa, GGML_OP_ADD) || !sole(qa, qr)) return false;
+        ggml_tensor * qm = qa->src[0];
+        if (!is(qm, GGML_OP_MUL_MAT) || !sole(qm, qa)) return false;
+        ggml_tensor * vc = kqv->src[0];
+        if (!is(vc, GGML_OP_CONT) || !sole(vc, kqv)) return false;
+        ggml_tensor * vp = vc->src[0];
+        if (!is(vp, GGML_OP_PERMUTE) || !sole(vp, vc)) return false;
+        ggml_tensor * vr = vp->src[0];
+        if (!is(vr, GGML_OP_RESHAPE) || !sole(vr, vp)) return false;
+        ggml_tensor * va = vr->src[0];
+        if (!is(va, GGML_OP_ADD) || !sole(va, vr)) return false;
+        ggml_tensor * vm = va->src[0];
+        if (!is(vm, GGML_OP_MUL_MAT) || !sole(vm, va)) return false;
+        const ggml_tensor * x = qm->src[1];
+        const ggml_tensor * wq = qm->src[0];
+        if (km->src[1] != x || vm->src[1] != x) return false;
+        for (const ggml_tensor * m : {qm, km, vm})
+            if (!mm_fast_ok(m) || m->src[0]->type != wq->type || !ggml_are_same_shape(m->src[0], wq) ||
+                !is_weight_buffer(m->src[0]) || ((uintptr_t) m->data & 15) != 0)
+                return false;
+        const int64_t D = wq->ne[1], T = x->ne[1], H = D / 64;
+        if (wq->ne[0] != D || D % 64 != 0 || x->ne[2] != 1 || x->ne[3] != 1 || T * D >= (1ll << 31)) return false;
+        if (!row_vec_f32(qa->src[1], D) || !row_vec_f32(va->src[1], D) || !is_weight_buffer(qa->src[1]) ||
+            !is_weight_buffer(va->src[1]) || !same_shape_rows(qm, qa) || !same_shape_rows(vm, va))
+            return false;
+        float sc;
+        memcpy(&sc, qs->op_params, 4);
+        int ex;
+        if (!(sc > 0.0f) || frexpf(sc, &ex) != 0.5f || !ggml_is_contiguous(qs) || qs->type != GGML_TYPE_F32) return false;
+        // element (d, t, h) of the K / Q views and (t, d, h) of V's CONT source = row t, column 64 h + d of the
+        // projection (the only layout the epilogue writes)
+        auto hd = [&](const ggml_tensor * v, const ggml_tensor * base, int64_t n0, int64_t s0, int64_t s1) {
+            return v->data == base->data && v->ne[0] == n0 && v->ne[1] == (n0 == 64 ? T : 64) && v->ne[2] == H &&
+                   (int64_t) v->nb[0] == s0 && (int64_t) v->nb[1] == s1 && (int64_t) v->nb[2] == 256;
+        };
+        if (!hd(kp, km, 64, 4, D * 4) || !hd(qp, qs, 64, 4, D * 4) || !hd(vp, va, T, D * 4, 4)) return false;
+        if (qr->data != qa->data) return false;
+        r = qkv_route{{qm, km, vm}, qa->src[1], va->src[1], sc};
+        absorbed = {qm, km, vm, qa, qs, va, vc};
+        return true;
+    };
+    std::vector<qkv_route> qkv_routes;
+    std::vector<const ggml_tensor *> qkv_route_kq;                         // [route] its attention's KQ node
+    std::unordered_map<const ggml_tensor *, int> qkv_mm;                   // Q / K / V MUL_MAT -> route
+    std::unordered_map<const ggml_tensor *, int> qkv_absorbed;             // nodes a route replaces -> route
+    std::vector<char> qkv_done;
+    std::unordered_map<const ggml_tensor *, qkv_ops> qkv_ready;            // KQ node -> operands written
+    if (!no_fuse && !no_qkv) {
+        for (int j = 0; j + 2 < nn; ++j) {
+            ggml_tensor * kqv = match_attention(g, j);
+            if (!kqv) continue;
+            qkv_route r;
+            std::vector<const ggml_tensor *> ab;
+            if (!match_qkv(ggml_graph_node(g, j), kqv, r, ab)) continue;
+            const int id = (int) qkv_routes.size();
+            qkv_routes.push_back(r);
+            qkv_route_kq.push_back(ggml_graph_node(g, j));
+            for (int k = 0; k < 3; ++k) qkv_mm[r.mm[k]] = id;
+            for (const ggml_tensor * t : ab) qkv_absorbed[t] = id;
+        }
+        qkv_done.assign(qkv_routes.size(), 0);
+    }
     // the epilogue chain that follows the fast MUL_MAT at node j (see the MUL_MAT case)
     auto chain_of = [&](int j) -> mm_chain {
         ggml_tensor * op = ggml_graph_node(g, j);
@@ -1402,6 +1738,28 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
         if (ggml_is_empty(op) || op->op == GGML_OP_NONE || op->op == GGML_OP_RESHAPE || op->op == GGML_OP_VIEW ||
             op->op == GGML_OP_PERMUTE || op->op == GGML_OP_TRANSPOSE)
             continue;
+        if (!qkv_absorbed.empty()) {
+            const auto ab = qkv_absorbed.find(op);
+            if (ab != qkv_absorbed.end()) {
+                // the first of a route's MUL_MATs in node order runs the fused GEMM; everything else it replaces is done
+                if (qkv_mm.count(op) && !qkv_done[ab->second]) {
+                    qkv_done[ab->second] = 1;
+                    b->stats.n_nodes++;
+                    qkv_ops ops;
+                    run_qkv_fused(b, qkv_routes[ab->second], ops);
+                    qkv_ready[qkv_route_kq[ab->second]] = ops;
+                    b->stats.n_mul_mat_fast += 3;
+                    b->stats.n_mm_grouped++;
+                    b->stats.n_fused += 4;   // Q bias, Q scale, V bias, V CONT
+                    const hipError_t e = hipGetLastError();
+                    if (e != hipSuccess) {
+                        Q2A_LOG_ERROR("ggml-q2a: fused Q|K|V (%s) launch failed: %s\n", op->name, hipGetErrorString(e));
+                        return GGML_STATUS_FAILED;
+                    }
+                }
+                continue;
+            }
+        }
         b->stats.n_nodes++;
         const ggml_tensor * s0 = op->src[0];
         const ggml_tensor * s1 = op->src[1];
@@ -1421,7 +1779,8 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                             merged = c;
                     }
                     const bool vt_ready = kqv->src[0] == vt_ready_for;
-                    const int used = run_fused_attention(b, g, i, vt_ready, merged);
+                    const auto rd = qkv_ready.find(op);
+                    const int used = run_fused_attention(b, g, i, vt_ready, merged, rd != qkv_ready.end() ? &rd->second : nullptr);
                     if (merged) b->stats.n_fused += 1;
                     if (vt_ready) vt_ready_for = nullptr;
                     i += used - 1;
@@ -1671,6 +2030,7 @@ void be_free(ggml_backend_t be) {
     (void) hipStreamSynchronize(b->stream);
     if (b->scratch) (void) hipFree(b->scratch);
     if (b->vt_buf) (void) hipFree(b->vt_buf);
+    if (b->qkv_buf) (void) hipFree(b->qkv_buf);
     for (int k = 0; k < 2; ++k) if (b->a16[k]) (void) hipFree(b->a16[k]);
     for (auto & e : b->graphs) if (e.exec) (void) hipGraphExecDestroy(e.exec);
     (void) hipStreamDestroy(b->stream);

@@ -506,9 +506,9 @@ int pack(const char * path, std::vector<uint8_t> & out, int act = 0, bool compac
 
 // One weight matrix on its own (the ggml-backend plugin's MUL_MAT weights): same arrays as a blob matrix,
 // laid out in one allocation whose offsets go to off[A_W..A_GAMMA] (0 = absent).
-int q2a_pack_linear(const uint8_t * raw, int wtype, int N, int K, std::vector<uint8_t> & out, uint64_t off[6]) {
+uint64_t q2a_pack_layout(int wtype, int N, int K, uint64_t off[6]) {
     const int blk = blk_of(wtype);
-    if ((wtype != Q2A_TYPE_F16 && !blk) || (blk && K % blk) || N <= 0 || K <= 0) return Q2A_ERR_UNSUPPORTED;
+    if ((wtype != Q2A_TYPE_F16 && !blk) || (blk && K % blk) || N <= 0 || K <= 0) return 0;
     uint64_t o = 0;
     auto take = [&](uint64_t bytes) { const uint64_t r = o; o += (bytes + 255) & ~uint64_t(255); return r; };
     for (int i = 0; i < A_COUNT; ++i) off[i] = 0;
@@ -520,6 +520,12 @@ int q2a_pack_linear(const uint8_t * raw, int wtype, int N, int K, std::vector<ui
         off[A_BETA] = take((uint64_t) N * (K / 256) * 4);
         off[A_GAMMA] = take((uint64_t) N * (K / 256) * 4);
     }
+    return o;
+}
+
+int q2a_pack_linear(const uint8_t * raw, int wtype, int N, int K, std::vector<uint8_t> & out, uint64_t off[6]) {
+    const uint64_t o = q2a_pack_layout(wtype, N, K, off);
+    if (!o) return Q2A_ERR_UNSUPPORTED;
     out.assign(o, 0);
     const unsigned nt = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
     std::vector<std::thread> th;
@@ -534,7 +540,8 @@ namespace {
 __global__ void k_split_hilo(const float * x, q2a_half * hi, q2a_half * lo, int64_t n, float scale) {
     const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const float v = x[i] * scale;
+    float v = x[i] * scale;
+    asm volatile("" : "+v"(v));   // rounded to f32 before the split, as the QKV epilogue (no one-step fp16 rounding)
     const _Float16 h = (_Float16) v;
     hi[i] = h;
     lo[i] = (_Float16) (v - (float) h);

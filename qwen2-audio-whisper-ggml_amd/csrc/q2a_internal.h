@@ -200,6 +200,9 @@ hipError_t q2a_launch_gelu_quant_q8k(const q2a_half * XH, int M, int K, const ui
 #ifdef __cplusplus
 #include <vector>
 int q2a_pack_linear(const uint8_t * raw, int wtype, int N, int K, std::vector<uint8_t> & out, uint64_t off[6]);
+// the section offsets of q2a_pack_linear's layout (W [N][K] fp16 | dx | dmin | wext | beta | gamma, the per-block
+// sections block-major [K/blk][N](x16 for wext)) and its total bytes (0 = unsupported type or shape)
+uint64_t q2a_pack_layout(int wtype, int N, int K, uint64_t off[6]);
 #endif
 
 // AvgPool1d(2,2) over time + final LayerNorm -> out [clips][T/2][D] f32

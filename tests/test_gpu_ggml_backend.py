@@ -68,6 +68,19 @@ def test_reference_whisper_full_on_backend_tiny(harness, make_model, make_clip, 
     assert mx <= bar["max_rel"] and l2 <= bar["rel_l2"], (mx, l2, st, bar)
 
 
+@pytest.mark.parametrize("wt", ["f16", "q4_k"])
+def test_backend_fused_qkv_equals_grouped_projections(harness, make_model, make_clip, tmp_path, wt):
+    """The Q|K|V projections as one GEMM whose epilogue writes the attention's operands (ggml-q2a.hip run_qkv_fused)
+    against the route it replaces (GGML_Q2A_NO_FUSED_QKV=1: K|Q grouped launch, V launch, V^T tile pass, operand
+    pass): the same f32 operations in the same K order, so embd_enc is bit-identical — full size, 32 layers."""
+    model, clip = make_model("full", wt), make_clip(0, 480000)
+    sep, info_s = run(harness, model, clip, tmp_path, {"GGML_Q2A_NO_FUSED_QKV": "1"})
+    fused, info_f = run(harness, model, clip, tmp_path, {})
+    assert info_f["mm_grouped"] == 32 and info_f["fused"] == info_s["fused"] + 32, (info_f, info_s)
+    assert info_f["mul_mat_fast"] == info_s["mul_mat_fast"] and info_f["attn_fused"] == 32, (info_f, info_s)
+    assert np.array_equal(fused, sep)
+
+
 def test_backend_unfused_attention_path(harness, make_model, make_clip, golden, tmp_path):
     """The generic per-node path (K.Q on the exact-f32 MFMA GEMM, SOFT_MAX with a double sum, V.P) also matches."""
     _, g = golden
@@ -122,12 +135,12 @@ def test_backend_fusions_match_per_node(harness, make_model, make_clip, tmp_path
     assert info_p["fused"] == 0 and info_p["mm_grouped"] == 0, info_p
     fused, info_f = run(harness, model, clip, tmp_path, {})
     L = 2
-    # per layer: Q bias + scale, V bias, O bias + residual, fc1 bias + GELU, fc2 bias + residual, two LayerNorm affines,
-    # the attention output CONT;
+    # per layer: Q bias + scale, V bias, V's CONT (the Q|K|V GEMM writes V^T), O bias + residual, fc1 bias + GELU,
+    # fc2 bias + residual, two LayerNorm affines, the attention output CONT;
     # plus the final LayerNorm affine
-    assert info_f["fused"] == 14 * L + 2, info_f
-    # the K and Q projections of each layer run as one grouped launch (F16 and Q4_K weights)
-    assert info_f["mm_grouped"] == (L if wt in ("f16", "q4_k") else 0), info_f
+    assert info_f["fused"] == 15 * L + 2, info_f
+    # the Q, K and V projections of each layer run as one GEMM writing the attention's operands (every weight type)
+    assert info_f["mm_grouped"] == L, info_f
     assert info_f["other"] < info_p["other"], (info_f, info_p)
     assert np.array_equal(fused, plain)
 
