@@ -585,6 +585,8 @@ struct q2a_backend_ctx {
     size_t vt_bytes = 0;
     char * qkv_buf = nullptr;          // attention operands written by the fused Q|K|V GEMM (run_qkv_fused)
     size_t qkv_bytes = 0;
+    _Float16 * pre16 = nullptr;        // fc1's fp16 pre-activation / GELU output on the way to fc2's operand (run_fc1_for_fc2)
+    size_t pre16_bytes = 0;
     // fp16 shadows of f32 activations written by their producer (LayerNorm, fc1 GELU epilogue) for F16-weight
     // MUL_MATs that would otherwise convert them: two slots, a producer never writes the slot its own GEMM reads
     _Float16 * a16[2] = {nullptr, nullptr};
@@ -899,16 +901,24 @@ struct act_operand {
     int MP;
     char * extra;
 };
-act_operand activation_operand(q2a_backend_ctx * b, const ggml_tensor * x, int M, int K, int blk, size_t extra) {
+// where an activation operand of M rows x K lives in the scratch (grown to hold it and `extra` bytes; nothing produced)
+act_operand act_slots(q2a_backend_ctx * b, int M, int K, int blk, size_t extra) {
     const int MP = (M + 255) / 256 * 256;
     // scratch: A operand fp16 [M][K] | dy [K/blk][MP] | aext [K/256][MP][16] | extra
     const size_t a_bytes = ((size_t) M * K * 2 + 255) & ~size_t(255);
     const size_t dy_bytes = blk ? ((size_t) (K / blk) * MP * 4 + 255) & ~size_t(255) : 0;
     const size_t ae_bytes = blk == 256 ? (size_t) (K / 256) * MP * 32 : 0;
     char * s = (char *) scratch(b, a_bytes + dy_bytes + ae_bytes + extra);
-    q2a_half * A = (q2a_half *) s;
-    float * dy = (float *) (s + a_bytes);
-    q2a_half * aext = (q2a_half *) (s + a_bytes + dy_bytes);
+    return {(const q2a_half *) s, (float *) (s + a_bytes), (q2a_half *) (s + a_bytes + dy_bytes), MP,
+            s + a_bytes + dy_bytes + ae_bytes};
+}
+
+act_operand activation_operand(q2a_backend_ctx * b, const ggml_tensor * x, int M, int K, int blk, size_t extra) {
+    const act_operand slots = act_slots(b, M, K, blk, extra);
+    const int MP = slots.MP;
+    q2a_half * A = (q2a_half *) slots.A;
+    float * dy = slots.dy;
+    q2a_half * aext = slots.aext;
     const _Float16 * shadow = nullptr;
     if (blk == 0)
         for (int k = 0; k < 2; ++k) if (b->a16_src[k] == x) shadow = b->a16[k];
@@ -928,7 +938,16 @@ act_operand activation_operand(q2a_backend_ctx * b, const ggml_tensor * x, int M
     // the same activation (the Q, K, V projections) reuses it; an fp16 conversion overwrote it
     b->quant_src = blk ? x : nullptr;
     b->quant_blk = blk;
-    return {A, dy, aext, MP, s + a_bytes + dy_bytes + ae_bytes};
+    return {A, dy, aext, MP, slots.extra};
+}
+
+int blk_of_type(int t) { return t == GGML_TYPE_Q4_K ? 256 : t == GGML_TYPE_F16 ? 0 : 32; }
+
+// the split-K partial planes run_mm_fast needs past the activation operand (0 = no split)
+size_t mm_part_bytes(int epi, int blk, int M, int N, int K, bool grouped) {
+    const int nsplit = grouped || !(epi == Q2A_EPI_RESID || epi == Q2A_EPI_STORE_F) ? 0
+                       : blk == 0 ? q2a_gemm_resid_ksplit(M, N, K, 0) : q2a_gemm_kq_ksplit(M, N, K, blk);
+    return nsplit > 1 ? (size_t) nsplit * M * N * 4 : 0;
 }
 
 // epi: Q2A_EPI_STORE_F (bias optional), Q2A_EPI_GELU_F (bias, GELU), Q2A_EPI_RESID (bias, + resid rows); the result
@@ -941,13 +960,11 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
     const ggml_tensor * x = op->src[1];
     const int K = (int) w->ne[0], N = (int) w->ne[1];
     const int M = (int) (x->ne[1] * x->ne[2] * x->ne[3]);
-    const int blk = w->type == GGML_TYPE_Q4_K ? 256 : w->type == GGML_TYPE_F16 ? 0 : 32;
+    const int blk = blk_of_type(w->type);
     // fp16 small-tile GEMMs (a single clip) split K like the engine's residual GEMMs (q2a_gemm_resid_ksplit: up to
     // 4 partial [M][N] f32 planes, reduced in split order with the bias / residual / scale of the epilogue)
-    const int nsplit = sec || !(epi == Q2A_EPI_RESID || epi == Q2A_EPI_STORE_F) ? 0
-                       : blk == 0 ? q2a_gemm_resid_ksplit(M, N, K, 0) : q2a_gemm_kq_ksplit(M, N, K, blk);
-    const bool split = nsplit > 1;
-    const size_t part_bytes = split ? (size_t) nsplit * M * N * 4 : 0;
+    const size_t part_bytes = mm_part_bytes(epi, blk, M, N, K, sec != nullptr);
+    const bool split = part_bytes > 0;
     const act_operand ao = activation_operand(b, x, M, K, blk, part_bytes);
     q2a_gemm_args a;
     memset(&a, 0, sizeof(a));
@@ -956,6 +973,10 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
     a.outF = (float *) out->data; a.ldo = N;
     a.bias = bias; a.store_bias = bias != nullptr; a.resid = resid; a.out_scale = oscale;
     if (epi == Q2A_EPI_GELU_F) a.outH = (q2a_half *) out16;
+    if (epi == Q2A_EPI_GELU_H || epi == Q2A_EPI_PRE_H) {   // fp16 [M][N] only (no row remap)
+        a.outH = (q2a_half *) out16;
+        a.o_rpg = M; a.o_gstride = 0; a.o_off = 0;
+    }
     if (sec) {
         a.ngroup = 2;
         a.W2 = (const q2a_half *) sec->w->data;
@@ -997,6 +1018,52 @@ void run_mm_fast(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * out = null
         }
     }
     Q2A_HIP(q2a_launch_gemm(a, epi, blk, b->stream));
+}
+
+_Float16 * claim_a16(q2a_backend_ctx * b, const ggml_tensor * t);
+
+_Float16 * pre16_buffer(q2a_backend_ctx * b, size_t bytes) {
+    if (bytes > b->pre16_bytes) {
+        abort_capture(b);
+        Q2A_HIP(hipStreamSynchronize(b->stream));
+        if (b->pre16) Q2A_HIP(hipFree(b->pre16));
+        b->pre16 = nullptr;
+        Q2A_HIP(hipMalloc((void **) &b->pre16, bytes));
+        b->pre16_bytes = bytes;
+        drop_graphs(b);
+        resume_discard(b);
+    }
+    return b->pre16;
+}
+
+// fc1 -> ADD(bias) -> GELU whose output only fc2 reads (qwen2-whisper.cpp:2136-2154): fc1's epilogue writes what fc2
+// consumes instead of the f32 GELU rows — for an F16 fc2 the fp16 GELU values (exact: ggml's GELU table is fp16), for a
+// Q4_K fc2 the fp16 pre-activation, which the engine's GELU + Q8_K kernel turns into fc2's operand, for a Q8_0 / Q4_0
+// fc2 the fp16 GELU values quantized to Q8_0. fc2 then finds its operand in place (shadow / quant_src). Same values as
+// GELU_F + conversion / quantizer (the engine's fc1 paths, q2a_engine.hip run_block).
+void run_fc1_for_fc2(q2a_backend_ctx * b, ggml_tensor * op, const mm_chain & c, const ggml_tensor * fc2) {
+    const ggml_tensor * gelu = c.out;
+    const int M = (int) (op->src[1]->ne[1] * op->src[1]->ne[2] * op->src[1]->ne[3]), F = (int) op->src[0]->ne[1];
+    const int blk2 = blk_of_type(fc2->src[0]->type);
+    if (blk2 == 0) {
+        run_mm_fast(b, op, c.out, Q2A_EPI_GELU_H, c.bias, nullptr, 0.0f, claim_a16(b, gelu));
+        return;
+    }
+    // fc2's operand slots first: a scratch growth now loses nothing (fc1's own operand is produced after it)
+    const int N2 = (int) fc2->src[0]->ne[1];
+    (void) act_slots(b, M, F, blk2, mm_part_bytes(Q2A_EPI_RESID, blk2, M, N2, F, false));
+    _Float16 * pre = pre16_buffer(b, (size_t) M * F * 2);
+    run_mm_fast(b, op, c.out, blk2 == 256 ? Q2A_EPI_PRE_H : Q2A_EPI_GELU_H, c.bias, nullptr, 0.0f, pre);
+    const act_operand d = act_slots(b, M, F, blk2, 0);
+    if (blk2 == 256) {
+        Q2A_HIP(q2a_launch_gelu_quant_q8k((const q2a_half *) pre, M, F, gelu_table(b->device), (q2a_half *) d.A, d.dy,
+                                          d.aext, d.MP, b->stream));
+    } else {
+        q2a_quant_args qa{nullptr, (const q2a_half *) pre, M, F, 2, (q2a_half *) d.A, d.dy, d.aext, d.MP};
+        Q2A_HIP(q2a_launch_quant_act(qa, b->stream));
+    }
+    b->quant_src = gelu;
+    b->quant_blk = blk2;
 }
 
 // the conv kernel duplicated into [N][2K] (w | w), cached like the repacked weights (dropped when its bytes change);
@@ -1213,8 +1280,9 @@ struct qkv_ops {                   // the attention operands as the fused Q|K|V 
     _Float16 *qh, *ql, *kh, *kl, *vt, *vtl;
 };
 
+// out16: the merged output's fp16 shadow (its only consumer an F16-weight MUL_MAT): written instead of the f32 rows
 int run_fused_attention(q2a_backend_ctx * b, ggml_cgraph * g, int i, bool vt_ready, ggml_tensor * merged,
-                        const qkv_ops * ready = nullptr) {
+                        const qkv_ops * ready = nullptr, _Float16 * out16 = nullptr) {
     ggml_tensor * kq = ggml_graph_node(g, i);
     ggml_tensor * kqv = ggml_graph_node(g, i + 2);
     const ggml_tensor * K = kq->src[0];
@@ -1266,6 +1334,7 @@ int run_fused_attention(q2a_backend_ctx * b, ggml_cgraph * g, int i, bool vt_rea
         q2a_attn_args at{(const q2a_half *) ready->qh, (const q2a_half *) ready->ql, (const q2a_half *) ready->kh,
                          (const q2a_half *) ready->kl, (const q2a_half *) ready->vt, 1, (int) T, (int) D, (int) H, TP, nullptr, o};
         at.vtl = ready->vtl;
+        if (out16 && merged) { at.outH = (q2a_half *) out16; at.outF = nullptr; }
         Q2A_HIP(q2a_launch_attention(at, b->stream));
         if (!merged)
             hipLaunchKernelGGL(k_attn_out, grid1(n), dim3(256), 0, b->stream, (const float *) o, tv(kqv), (int) T, (int) H, n);
@@ -1291,6 +1360,7 @@ int run_fused_attention(q2a_backend_ctx * b, ggml_cgraph * g, int i, bool vt_rea
     q2a_attn_args at{(const q2a_half *) qh, (const q2a_half *) ql, (const q2a_half *) kh, (const q2a_half *) kl,
                      (const q2a_half *) vt, 1, (int) T, (int) D, (int) H, TP, nullptr, o};
     at.vtl = vtl;
+    if (out16 && merged) { at.outH = (q2a_half *) out16; at.outF = nullptr; }
     Q2A_HIP(q2a_launch_attention(at, b->stream));
     if (!merged)
         hipLaunchKernelGGL(k_attn_out, grid1(n), dim3(256), 0, b->stream, (const float *) o, tv(kqv), (int) T, (int) H, n);
@@ -1401,17 +1471,6 @@ char * qkv_buffer(q2a_backend_ctx * b, size_t bytes) {
     return b->qkv_buf;
 }
 
-// V^T columns T <= t < TP of every (h, d) row -> 0 (a buffer last used with a larger T keeps finite old values there;
-// they meet P = 0 only, but a stale inf would make 0 * inf)
-__global__ void k_vt_tail_zero(_Float16 * vt, _Float16 * vtl, int rows, int T, int TP) {
-    const int w = TP - T;
-    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t) rows * w) return;
-    const int64_t o = (i / w) * TP + T + i % w;
-    vt[o] = (_Float16) 0.0f;
-    if (vtl) vtl[o] = (_Float16) 0.0f;
-}
-
 void run_qkv_fused(q2a_backend_ctx * b, const qkv_route & r, qkv_ops & ops) {
     const ggml_tensor * x = r.mm[0]->src[1];
     const int K = (int) x->ne[0], M = (int) x->ne[1], D = (int) r.mm[0]->src[0]->ne[1], H = D / 64, T = M;
@@ -1427,10 +1486,7 @@ void run_qkv_fused(q2a_backend_ctx * b, const qkv_route & r, qkv_ops & ops) {
     ops = {(_Float16 *) ob, (_Float16 *) (ob + hb), (_Float16 *) (ob + 2 * hb), (_Float16 *) (ob + 3 * hb),
            (_Float16 *) (ob + 4 * hb), vlo ? (_Float16 *) (ob + 4 * hb + vb1) : nullptr};
     const act_operand ao = activation_operand(b, x, M, K, blk, 0);
-    if (TP > T) {
-        const int64_t n = (int64_t) D * (TP - T);
-        hipLaunchKernelGGL(k_vt_tail_zero, grid1(n), dim3(256), 0, b->stream, ops.vt, ops.vtl, D, T, TP);
-    }
+    // (V^T's pad columns T <= t < TP: written as zeros by the epilogue of a one-clip launch, M == T)
     q2a_gemm_args a;
     memset(&a, 0, sizeof(a));
     a.A = ao.A; a.lda = K; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
@@ -1707,6 +1763,16 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
         }
         qkv_done.assign(qkv_routes.size(), 0);
     }
+    // the fast MUL_MAT after node `from` that reads t, when it is t's only consumer (null otherwise)
+    auto sole_mm_consumer = [&](const ggml_tensor * t, int from) -> const ggml_tensor * {
+        if (no_fuse) return nullptr;
+        for (int j = from + 1; j < nn; ++j) {
+            const ggml_tensor * n = ggml_graph_node(g, j);
+            if (n->op == GGML_OP_MUL_MAT && n->src[1] == t)
+                return sole(t, n) && mm_fast_ok(n) && !qkv_mm.count(n) && !match_attention(g, j) ? n : nullptr;
+        }
+        return nullptr;
+    };
     // the epilogue chain that follows the fast MUL_MAT at node j (see the MUL_MAT case)
     auto chain_of = [&](int j) -> mm_chain {
         ggml_tensor * op = ggml_graph_node(g, j);
@@ -1780,7 +1846,11 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                     }
                     const bool vt_ready = kqv->src[0] == vt_ready_for;
                     const auto rd = qkv_ready.find(op);
-                    const int used = run_fused_attention(b, g, i, vt_ready, merged, rd != qkv_ready.end() ? &rd->second : nullptr);
+                    // the merged rows feeding only an F16 O-projection: written as its fp16 operand directly
+                    const ggml_tensor * o_mm = merged ? sole_mm_consumer(merged, i + 4) : nullptr;
+                    _Float16 * out16 = o_mm && o_mm->src[0]->type == GGML_TYPE_F16 ? claim_a16(b, merged) : nullptr;
+                    const int used = run_fused_attention(b, g, i, vt_ready, merged, rd != qkv_ready.end() ? &rd->second : nullptr,
+                                                         out16);
                     if (merged) b->stats.n_fused += 1;
                     if (vt_ready) vt_ready_for = nullptr;
                     i += used - 1;
@@ -1814,6 +1884,15 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                         b->stats.n_mul_mat_fast += 2;
                         b->stats.n_mm_grouped++;
                         i = c2.last;
+                        break;
+                    }
+                }
+                if (c1.epi == Q2A_EPI_GELU_F && ggml_is_contiguous(c1.out)) {
+                    if (const ggml_tensor * f2 = sole_mm_consumer(c1.out, c1.last)) {
+                        run_fc1_for_fc2(b, op, c1, f2);
+                        b->stats.n_fused += c1.nfused;
+                        b->stats.n_mul_mat_fast++;
+                        i = c1.last;
                         break;
                     }
                 }
@@ -2031,6 +2110,7 @@ void be_free(ggml_backend_t be) {
     if (b->scratch) (void) hipFree(b->scratch);
     if (b->vt_buf) (void) hipFree(b->vt_buf);
     if (b->qkv_buf) (void) hipFree(b->qkv_buf);
+    if (b->pre16) (void) hipFree(b->pre16);
     for (int k = 0; k < 2; ++k) if (b->a16[k]) (void) hipFree(b->a16[k]);
     for (auto & e : b->graphs) if (e.exec) (void) hipGraphExecDestroy(e.exec);
     (void) hipStreamDestroy(b->stream);

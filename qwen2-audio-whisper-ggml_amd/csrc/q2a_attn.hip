@@ -725,9 +725,12 @@ __global__ __launch_bounds__(512, 2) void k_attn_pp(const q2a_attn_args p) {
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const int d = dt * 32 + 8 * g + 4 * hi;
-                const float v0 = o[dt][4 * g + 0] * inv, v1 = o[dt][4 * g + 1] * inv;
-                const float v2 = o[dt][4 * g + 2] * inv, v3 = o[dt][4 * g + 3] * inv;
+                float v0 = o[dt][4 * g + 0] * inv, v1 = o[dt][4 * g + 1] * inv;
+                float v2 = o[dt][4 * g + 2] * inv, v3 = o[dt][4 * g + 3] * inv;
                 if (p.outH) {
+                    // rounded to f32 first (no one-step fp16 rounding of the product): the fp16 output is the fp16 of
+                    // the f32 output, bit for bit
+                    asm volatile("" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));
                     const half4 hv = {to16<BF>(v0), to16<BF>(v1), to16<BF>(v2), to16<BF>(v3)};
                     *(half4 *) (p.outH + orow + d) = hv;
                 } else {

@@ -1787,10 +1787,14 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     #pragma unroll
                         for (int a = lane % LPR; a < NI * 4; a += LPR) {
                             const int ml = I0 * 16 + 4 * a, m = rbase + ml;
-                            if (m >= p.M) continue;
-                            const bool wrap = t0 + ml >= p.T;
-                            const int clip = clip0 + (wrap ? 1 : 0), t = t0 + ml - (wrap ? p.T : 0);
-                            const uint2 v = *(const uint2 *) (src + d * VS + 4 * a);
+                            // one clip (M == T): the tile rows T <= t < TP write V^T's pad columns as zeros (the
+                            // attention reads them as zero weights), so no caller has to clear them
+                            const bool pad = m >= p.M;
+                            if (pad && (p.M != p.T || m >= p.TP)) continue;
+                            const bool wrap = !pad && t0 + ml >= p.T;
+                            // (a pad row of a wave starting at or past T has clip0 = 1: it is clip 0's t = m)
+                            const int clip = pad ? 0 : clip0 + (wrap ? 1 : 0), t = pad ? m : t0 + ml - (wrap ? p.T : 0);
+                            const uint2 v = pad ? make_uint2(0u, 0u) : *(const uint2 *) (src + d * VS + 4 * a);
                             if (Q2A_ST && Q2A_ST_VT) q2a_st(v, (uint2 *) (vdst + (((int64_t) clip * p.H + h) * 64 + d) * p.TP + t));
                         }
                     }
