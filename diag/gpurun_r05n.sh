@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5: ggml backend fc1 -> fc2 operand route, fp16 attention output for an F16 O-projection, V^T pad columns from
+# round 5: ggml backend fused routes (Q|K|V GEMM, fc1 -> fc2 operand, fused LayerNorm operand, fp16 attention output):
 # the QKV epilogue: backend tests + whisper_full timing + kernel trace, then the whole GPU suite
 cd /root/repo
 mkdir -p gpurun_out

@@ -259,9 +259,11 @@ __global__ __launch_bounds__(256) void k_norm_row(tview a, tview d, float eps, c
         } else {
             v[k][0] = ok ? x[j] : 0.0f;
         }
+        // (a float4's four terms summed first, then into the running sum: the grouping of the engine's LayerNorm,
+        // q2a_exact.hip k_rownorm, so both give the same row bit for bit and the fused LN route below can use it)
         if (ok) {
-#pragma unroll
-            for (int q = 0; q < W; ++q) s += (double) v[k][q];
+            if (V4) s += (double) v[k][0] + (double) v[k][W > 1 ? 1 : 0] + (double) v[k][W > 2 ? 2 : 0] + (double) v[k][W > 3 ? 3 : 0];
+            else s += (double) v[k][0];
         }
     }
 #pragma unroll
@@ -271,11 +273,12 @@ __global__ __launch_bounds__(256) void k_norm_row(tview a, tview d, float eps, c
 #pragma unroll
     for (int k = 0; k < C; ++k) {
         if ((lane + 64 * k) * W < n) {
+            float c[W];
 #pragma unroll
-            for (int q = 0; q < W; ++q) {
-                const float c = v[k][q] - mean;
-                s2 += (double) (c * c);
-            }
+            for (int q = 0; q < W; ++q) c[q] = v[k][q] - mean;
+            if (V4) s2 += (double) (c[0] * c[0]) + (double) (c[W > 1 ? 1 : 0] * c[W > 1 ? 1 : 0]) +
+                          (double) (c[W > 2 ? 2 : 0] * c[W > 2 ? 2 : 0]) + (double) (c[W > 3 ? 3 : 0] * c[W > 3 ? 3 : 0]);
+            else s2 += (double) (c[0] * c[0]);
         }
     }
 #pragma unroll
@@ -1945,6 +1948,49 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                 const bool v4 = op->ne[0] % 4 == 0 && aligned16(s0) && aligned16(out);
                 const float * w = aff ? (const float *) n1->src[1]->data : nullptr;
                 const float * bb = aff ? (const float *) n2->src[1]->data : nullptr;
+                // rows read only by fast MUL_MATs of one weight class (the Q|K|V projections; fc1): the engine's fused
+                // LayerNorm writes their operand — fp16 rows, or Q8_K / Q8_0 codes and scales in the scratch —
+                // instead of the f32 rows (the same rows: k_norm_row sums like it; q2a_engine.hip run_block)
+                if (aff && v4 && eps == 1e-5f && !no_fuse && ggml_is_contiguous(s0) && ggml_is_contiguous(out) &&
+                    !(out->flags & GGML_TENSOR_FLAG_OUTPUT)) {
+                    const int D = (int) op->ne[0], M = (int) rows;
+                    int blk = -1, found = 0, last = -1;
+                    size_t extra = 0;
+                    bool ok = true;
+                    for (int j = i + 3; j < nn && ok; ++j) {
+                        const ggml_tensor * c = ggml_graph_node(g, j);
+                        bool reads = false;
+                        for (int k = 0; k < GGML_MAX_SRC; ++k) reads = reads || c->src[k] == out;
+                        if (reads) {
+                            if (c->op != GGML_OP_MUL_MAT || c->src[1] != out || c->src[0] == out || !mm_fast_ok(c) ||
+                                match_attention(g, j)) { ok = false; break; }
+                            const int cb = blk_of_type(c->src[0]->type);
+                            if (blk >= 0 && cb != blk) { ok = false; break; }
+                            blk = cb;
+                            ++found;
+                            last = j;
+                            extra = std::max(extra, mm_part_bytes(Q2A_EPI_STORE_F, cb, M, (int) c->src[0]->ne[1], D, false));
+                        } else if (found < (uses.count(out) ? uses[out] : 0) && c->op == GGML_OP_MUL_MAT && !qkv_absorbed.count(c)) {
+                            ok = false;   // another GEMM (scratch user) between the LayerNorm and its last reader
+                        }
+                        if (found == (uses.count(out) ? uses[out] : 0)) break;
+                    }
+                    if (ok && found > 0 && found == uses[out] && last > i && (blk == 0 || D % (blk == 256 ? 256 : 32) == 0)) {
+                        q2a_ln_args la{(const float *) s0->data, M, D, w, bb, blk == 0 ? 0 : blk == 256 ? 1 : 2, nullptr, nullptr, nullptr, 0};
+                        if (blk == 0) {
+                            la.outH = (q2a_half *) claim_a16(b, out);
+                        } else {
+                            const act_operand d = act_slots(b, M, D, blk, extra);
+                            la.outH = (q2a_half *) d.A; la.dy = d.dy; la.aext = d.aext; la.dy_ld = d.MP;
+                        }
+                        Q2A_HIP(q2a_launch_layernorm(la, st));
+                        if (blk) { b->quant_src = out; b->quant_blk = blk; }
+                        b->stats.n_fused += 2;
+                        b->stats.n_other++;
+                        i += 2;
+                        break;
+                    }
+                }
                 const dim3 grid((rows + 3) / 4);
                 _Float16 * yh = want16.count(out) && ggml_is_contiguous(out) ? claim_a16(b, out) : nullptr;
                 if (aff && v4) hipLaunchKernelGGL((k_norm_row<true, true>), grid, dim3(256), 0, st, tv(s0), tv(out), eps, w, bb, (int) rows, yh);
