@@ -490,8 +490,9 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
 #pragma unroll
             for (int db = 0; db < 4; ++db) {
                 const int d = 16 * db + 4 * g;
-                const f4v_t v = o[qb][db] * inv;
+                f4v_t v = o[qb][db] * inv;
                 if (p.outH) {
+                    asm volatile("" : "+v"(v));   // f32 first: the fp16 output is the fp16 of the f32 output
                     const half4 hv = {(_Float16) v[0], (_Float16) v[1], (_Float16) v[2], (_Float16) v[3]};
                     *(half4 *) (p.outH + orow + d) = hv;
                 } else {
