@@ -47,7 +47,9 @@ typedef struct {
     int n_nodes, n_mul_mat_fast, n_mul_mat_f32, n_attn_fused, n_other;
     int n_graph_replayed;
     int n_fused;
-    int n_mm_grouped;   /* launches that ran two weight MUL_MATs of the same activation together */
+    int n_mm_grouped;   /* launches that ran several weight MUL_MATs of the same activation together: a layer's Q, K,
+                           V projections as one GEMM writing the fused attention's operands (GGML_Q2A_NO_FUSED_QKV=1
+                           disables it: then K|Q as one launch and V), or K|Q alone */
     int n_mul_mat_conv; /* MUL_MAT(F32 im2col, F16 kernel) on the fp16 MFMA GEMM with hi/lo-split activations */
     int n_buffer_reallocs; /* backend lifetime: scratch / V^T / fp16-shadow reallocations (each drops every captured
                               HIP graph, whose launches hold those buffers' addresses) */
