@@ -100,6 +100,12 @@ __device__ __forceinline__ void q2a_st(const V & v, V * ptr) {
 #ifndef Q2A_GEMM_ALT
 #define Q2A_GEMM_ALT 0
 #endif
+// Measured round 5 (profiles/r05r_block_start_early_reads.json): bit-identical, neutral; off.
+// 8-phase Q4_K kernel: a block's first phase issues its fragment reads BEFORE the block start (whose scale reads, wait
+// and rescale VALU then run under the fragment reads' latency) instead of after it
+#ifndef Q2A_GEMM_BSR
+#define Q2A_GEMM_BSR 0
+#endif
 
 // Timing diagnostic Q2A_DIAG_STAMPS=<epi>: the 8-phase kernels of epilogue <epi> record s_memtime at fixed points of
 // every workgroup's tile (waves 0 and 4, lane 0) into g_q2a_stamps, read back by q2a_diag_stamps (diag/tile_stamps.py):
@@ -639,7 +645,19 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     read_b(B, 1);               S2; Q2A_PB(V2); mma(0, 1); Q2A_PE();                      \
     Q2A_RA3(B);                 S3; Q2A_PB(V3); Q2A_U8U(); mma(1, 1); Q2A_PE();           \
                                 S4; Q2A_PB(V4); mma(1, 0); Q2A_PE()
+#if Q2A_GEMM_BSR
+// a block's first K-step: phase 1's B fragments were read before the block start (Q2A_BSR; with the A fragments
+// too the 48 fragment registers beside the block start's temporaries spill ~60 VGPRs)
+#define Q2A_BSR() do { read_b(0, 0); } while (0)
+#define Q2A_KSTEP_S(B, S1, S2, S3, S4, V1, V2, V3, V4)                                    \
+                  Q2A_RA1(B);   S1; Q2A_PB(V1); Q2A_U8U(); mma(0, 0); Q2A_PE();           \
+    read_b(B, 1);               S2; Q2A_PB(V2); mma(0, 1); Q2A_PE();                      \
+    Q2A_RA3(B);                 S3; Q2A_PB(V3); Q2A_U8U(); mma(1, 1); Q2A_PE();           \
+                                S4; Q2A_PB(V4); mma(1, 0); Q2A_PE()
+#else
+#define Q2A_BSR() do { } while (0)
 #define Q2A_KSTEP_S Q2A_KSTEP   // (phase 2 also issues the block's 3 scale pieces)
+#endif
 #endif
 
 #if Q2A_GEMM_ALT
@@ -925,6 +943,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             // the next tile's first K-steps (tail stages), or a harmless re-load of this tile's last one
             auto stage_next = [&](int b, int h) { stage(b, h, has_next ? b : nk - 1); };
             int kt = 0;
+            Q2A_BSR();
             BS_T0();
             block_start(std::true_type{});
             BS_T1();
@@ -936,7 +955,8 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
                       10, 10, 10, 10);
             Q2A_KSTEP(1, stage(0, 1, kt + 4), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5), 10, 10, 10, 10);
             for (kt = 4; kt < nk - 4; kt += 4) {
-                BS_T0();
+                Q2A_BSR();
+            BS_T0();
                 block_start(std::false_type{});
                 BS_T1();
                 asm volatile("" ::: "memory");
@@ -948,6 +968,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
                 Q2A_KSTEP(1, stage(0, 1, kt + 4), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5), 10, 10, 10, 10);
             }
             prep_scales_last(has_next, m0n, n0n);
+            Q2A_BSR();
             BS_T0();
             block_start(std::false_type{});   // (nk >= 8: the last block is never block 0)
             BS_T1();
@@ -974,6 +995,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
         stagger_in();
         int kt = 0;
         for (; kt < nk - 4; kt += 4) {
+            Q2A_BSR();
             BS_T0();
             if (kt == 0) block_start(std::true_type{});
             else block_start(std::false_type{});
@@ -988,6 +1010,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             Q2A_KSTEP(1, stage(0, 1, kt + 4), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5), 10, 10, 10, 10);
         }
         // last block: its scales stay in place for the final multiply (the scale re-stage keeps the vmcnt counts)
+        Q2A_BSR();
         BS_T0();
         if (kt == 0) block_start(std::true_type{});
         else block_start(std::false_type{});
@@ -1002,6 +1025,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #endif
 #undef Q2A_KSTEP
 #undef Q2A_KSTEP_S
+#undef Q2A_BSR
 #ifdef Q2A_KSTEPC
 #undef Q2A_KSTEPC
 #undef Q2A_SB
