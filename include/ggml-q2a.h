@@ -33,6 +33,20 @@ GGML_API bool ggml_backend_is_q2a(ggml_backend_t backend);          /* ggml_back
 /* device memory buffer type (weights and compute buffers) */
 GGML_API ggml_backend_buffer_type_t ggml_backend_q2a_buffer_type(int device);   /* ggml-cuda.h:28 */
 
+/* pinned (page-locked, portable) host buffer type for the CPU-side buffers whose bytes cross PCIe (inputs staged by
+ * the CPU backend, results read back); replaces ggml_backend_cuda_host_buffer_type, ggml-cuda.h:34. Behaves as a CPU
+ * buffer (is_host); GGML_Q2A_NO_PINNED=1 or a failed pinning gives a plain CPU buffer. Also the device's
+ * get_host_buffer_type (ggml_backend_dev_host_buffer_type) */
+GGML_API ggml_backend_buffer_type_t ggml_backend_q2a_host_buffer_type(void);
+
+/* page-lock / release memory the caller owns; opt-in through GGML_Q2A_REGISTER_HOST (the reference's
+ * GGML_CUDA_REGISTER_HOST): false when not enabled or refused. Replace ggml_backend_cuda_register_host_buffer /
+ * _unregister_host_buffer, ggml-cuda.h:40-41; also reachable as "ggml_backend_register_host_buffer" /
+ * "ggml_backend_unregister_host_buffer" through ggml_backend_reg_get_proc_address(ggml_backend_q2a_reg(), name).
+ * (ggml_backend_cuda_split_buffer_type, ggml-cuda.h:31, has no counterpart: models are replicated per device.) */
+GGML_API bool ggml_backend_q2a_register_host_buffer(void * buffer, size_t size);
+GGML_API void ggml_backend_q2a_unregister_host_buffer(void * buffer);
+
 GGML_API int  ggml_backend_q2a_get_device_count(void);                                           /* ggml-cuda.h:36 */
 GGML_API void ggml_backend_q2a_get_device_description(int device, char * description, size_t description_size);
 GGML_API void ggml_backend_q2a_get_device_memory(int device, size_t * free, size_t * total);      /* ggml-cuda.h:38 */

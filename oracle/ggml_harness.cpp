@@ -14,6 +14,7 @@
 //                                                          dumpdir, the first ndump encoder-graph node outputs of the
 //                                                          first call (per-node comparison with ref_harness's dumps)
 //   ggml_harness graphs [device]                        -> HIP-graph capture vs scratch growth check, JSON line
+//   ggml_harness hostbuf [device]                       -> pinned host buffer type / host registration check, JSON line
 
 #define GGML_USE_CUDA
 #define ggml_backend_cuda_init ggml_backend_q2a_init
@@ -209,6 +210,85 @@ int cmd_graphs(int argc, char ** argv) {
     return eq ? 0 : 6;
 }
 
+// The pinned host buffer type and host-memory registration (ggml-q2a.h; the reference's ggml-cuda.h:34, 40-41):
+// a host-buffer tensor is ordinary CPU memory to ggml (is_host, written in place), copies between it and a device
+// tensor carry the bytes unchanged, the device and the registry expose it the way ggml's generic code looks it up, and
+// registration is opt-in (GGML_Q2A_REGISTER_HOST). Also times 64 MiB H2D from the pinned buffer vs pageable memory.
+int cmd_hostbuf(int argc, char ** argv) {
+    const int device = argc > 2 ? atoi(argv[2]) : 0;
+    ggml_backend_t be = ggml_backend_q2a_init(device);
+    if (!be) { fprintf(stderr, "no Q2A backend\n"); return 3; }
+    ggml_backend_buffer_type_t hb = ggml_backend_q2a_host_buffer_type();
+    ggml_backend_dev_t dev = ggml_backend_get_device(be);
+    ggml_backend_dev_props props;
+    ggml_backend_dev_get_props(dev, &props);
+    ggml_backend_reg_t reg = ggml_backend_q2a_reg();
+    typedef bool (*reg_fn)(void *, size_t);
+    typedef void (*unreg_fn)(void *);
+    reg_fn rf = (reg_fn) ggml_backend_reg_get_proc_address(reg, "ggml_backend_register_host_buffer");
+    unreg_fn uf = (unreg_fn) ggml_backend_reg_get_proc_address(reg, "ggml_backend_unregister_host_buffer");
+    const bool split_absent = ggml_backend_reg_get_proc_address(reg, "ggml_backend_split_buffer_type") == nullptr;
+
+    const int64_t n = 16 << 20;   // 64 MiB of f32
+    ggml_init_params ip = { 4 * ggml_tensor_overhead(), nullptr, true };
+    ggml_context * ch = ggml_init(ip), * cd = ggml_init(ip);
+    ggml_tensor * th = ggml_new_tensor_1d(ch, GGML_TYPE_F32, n);
+    ggml_tensor * td = ggml_new_tensor_1d(cd, GGML_TYPE_F32, n);
+    ggml_backend_buffer_t bh = ggml_backend_alloc_ctx_tensors_from_buft(ch, hb);
+    ggml_backend_buffer_t bd = ggml_backend_alloc_ctx_tensors(cd, be);
+    if (!bh || !bd) { fprintf(stderr, "allocation failed\n"); return 4; }
+    const bool pinned = strcmp(ggml_backend_buffer_name(bh), GGML_Q2A_NAME "_Host") == 0;
+    float * hp = (float *) th->data;   // host memory: written in place
+    for (int64_t i = 0; i < n; ++i) hp[i] = (float) ((i * 2654435761u) % 1000003) * 1e-3f - 500.f;
+    ggml_backend_tensor_copy(th, td);   // host -> device (dst->buffer set_tensor from the pinned bytes)
+    std::vector<float> back((size_t) n);
+    ggml_backend_tensor_get(td, back.data(), 0, (size_t) n * 4);
+    bool eq = memcmp(back.data(), hp, (size_t) n * 4) == 0;
+    memset(hp, 0, (size_t) n * 4);
+    ggml_backend_tensor_copy(td, th);   // device -> host buffer
+    eq = eq && memcmp(back.data(), hp, (size_t) n * 4) == 0;
+
+    auto h2d_gbs = [&](const void * src) {
+        double best = 1e30;
+        for (int r = 0; r < 5; ++r) {
+            auto t0 = std::chrono::steady_clock::now();
+            ggml_backend_tensor_set(td, src, 0, (size_t) n * 4);
+            auto t1 = std::chrono::steady_clock::now();
+            best = std::min(best, std::chrono::duration<double>(t1 - t0).count());
+        }
+        return (double) n * 4 / best / 1e9;
+    };
+    std::vector<float> pageable(back);
+    const double gbs_pinned = h2d_gbs(hp), gbs_pageable = h2d_gbs(pageable.data());
+
+    // registration of caller-owned memory: refused unless opted in, then page-locked and released again
+    const char * opt = getenv("GGML_Q2A_REGISTER_HOST");
+    const bool reg_default = opt ? true : ggml_backend_q2a_register_host_buffer(pageable.data(), pageable.size() * 4);
+    setenv("GGML_Q2A_REGISTER_HOST", "1", 1);
+    const bool reg_optin = rf && rf(pageable.data(), pageable.size() * 4);
+    const double gbs_registered = h2d_gbs(pageable.data());
+    if (uf) uf(pageable.data());
+    if (!opt) unsetenv("GGML_Q2A_REGISTER_HOST");
+
+    printf("{\"host_buft_name\": \"%s\", \"is_host\": %s, \"buffer_name\": \"%s\", \"pinned\": %s, \"dev_host_buft_same\": %s, "
+           "\"caps_host_buffer\": %s, \"buft_device_set\": %s, \"proc_register\": %s, \"proc_unregister\": %s, \"split_absent\": %s, "
+           "\"copies_equal\": %s, \"register_without_optin\": %s, \"register_optin\": %s, \"h2d_gbs_pinned\": %.2f, "
+           "\"h2d_gbs_pageable\": %.2f, \"h2d_gbs_registered\": %.2f}\n",
+           ggml_backend_buft_name(hb), ggml_backend_buft_is_host(hb) ? "true" : "false", ggml_backend_buffer_name(bh),
+           pinned ? "true" : "false", ggml_backend_dev_host_buffer_type(dev) == hb ? "true" : "false",
+           props.caps.host_buffer ? "true" : "false", ggml_backend_buft_get_device(hb) != nullptr ? "true" : "false",
+           rf == (reg_fn) ggml_backend_q2a_register_host_buffer ? "true" : "false",
+           uf == (unreg_fn) ggml_backend_q2a_unregister_host_buffer ? "true" : "false", split_absent ? "true" : "false",
+           eq ? "true" : "false", reg_default ? "true" : "false", reg_optin ? "true" : "false", gbs_pinned, gbs_pageable,
+           gbs_registered);
+    ggml_backend_buffer_free(bh);
+    ggml_backend_buffer_free(bd);
+    ggml_free(ch);
+    ggml_free(cd);
+    ggml_backend_free(be);
+    return eq ? 0 : 6;
+}
+
 }  // namespace
 
 int main(int argc, char ** argv) {
@@ -216,6 +296,7 @@ int main(int argc, char ** argv) {
     whisper_log_set([](ggml_log_level lvl, const char * text, void *) { if (lvl == GGML_LOG_LEVEL_ERROR) fputs(text, stderr); }, nullptr);
     if (std::string(argv[1]) == "encode") return cmd_encode(argc, argv);
     if (std::string(argv[1]) == "graphs") return cmd_graphs(argc, argv);
+    if (std::string(argv[1]) == "hostbuf") return cmd_hostbuf(argc, argv);
     fprintf(stderr, "unknown command %s\n", argv[1]);
     return 1;
 }

@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -762,6 +763,50 @@ const ggml_backend_buffer_type_i k_buft_iface = {
     /* get_max_size   */ nullptr,
     /* get_alloc_size */ nullptr,
     /* is_host        */ buft_is_host,
+};
+
+// ---- pinned host buffer type (ggml-cuda.h:34; the CPU-side buffers a caller stages its copies in) ------------------
+// Page-locked host memory (hipHostMalloc, portable: every device of a q2a_group sees it as pinned), handed to ggml as
+// a CPU buffer over that pointer, so the CPU backend computes in it and the DMA engines copy out of it directly instead
+// of through the runtime's pageable staging. GGML_Q2A_NO_PINNED=1 (the reference's GGML_CUDA_NO_PINNED) or a failed
+// pinning falls back to an ordinary CPU buffer.
+const char * host_buft_get_name(ggml_backend_buffer_type_t) { return GGML_Q2A_NAME "_Host"; }
+const char * host_buf_get_name(ggml_backend_buffer_t) { return GGML_Q2A_NAME "_Host"; }
+void host_buf_free(ggml_backend_buffer_t b) {
+    if (hipHostFree(b->context) != hipSuccess) (void) hipGetLastError();
+}
+bool pinned_allowed() { return getenv("GGML_Q2A_NO_PINNED") == nullptr; }
+ggml_backend_buffer_t host_buft_alloc(ggml_backend_buffer_type_t t, size_t size) {
+    void * p = nullptr;
+    if (pinned_allowed()) {
+        if (hipHostMalloc(&p, std::max<size_t>(size, 1), hipHostMallocPortable) != hipSuccess) {
+            (void) hipGetLastError();
+            Q2A_LOG_ERROR("ggml-q2a: pinning %.2f MB of host memory failed; using pageable memory\n", size / 1e6);
+            p = nullptr;
+        }
+    }
+    if (!p) return ggml_backend_buft_alloc_buffer(ggml_backend_cpu_buffer_type(), size);
+    ggml_backend_buffer_t b = ggml_backend_cpu_buffer_from_ptr(p, size);
+    b->buft = t;      // (a CPU buffer's context is its pointer: what host_buf_free releases)
+    b->iface.get_name = host_buf_get_name;
+    b->iface.free_buffer = host_buf_free;
+    return b;
+}
+size_t host_buft_get_alignment(ggml_backend_buffer_type_t) {
+    return ggml_backend_buft_get_alignment(ggml_backend_cpu_buffer_type());
+}
+size_t host_buft_get_alloc_size(ggml_backend_buffer_type_t, const ggml_tensor * t) {
+    return ggml_backend_buft_get_alloc_size(ggml_backend_cpu_buffer_type(), const_cast<ggml_tensor *>(t));
+}
+bool host_buft_is_host(ggml_backend_buffer_type_t) { return true; }
+
+const ggml_backend_buffer_type_i k_host_buft_iface = {
+    /* get_name       */ host_buft_get_name,
+    /* alloc_buffer   */ host_buft_alloc,
+    /* get_alignment  */ host_buft_get_alignment,
+    /* get_max_size   */ nullptr,
+    /* get_alloc_size */ host_buft_get_alloc_size,
+    /* is_host        */ host_buft_is_host,
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -2227,12 +2272,13 @@ void dev_get_props(ggml_backend_dev_t d, ggml_backend_dev_props * p) {
     p->description = dev_get_desc(d);
     p->type = dev_get_type(d);
     dev_get_memory(d, &p->memory_free, &p->memory_total);
-    p->caps = {/* async */ true, /* host_buffer */ false, /* events */ false};
+    p->caps = {/* async */ true, /* host_buffer */ pinned_allowed(), /* events */ false};
 }
 ggml_backend_t dev_init_backend(ggml_backend_dev_t d, const char *) {
     return ggml_backend_q2a_init(((q2a_device_ctx *) d->context)->device);
 }
 ggml_backend_buffer_type_t dev_get_buft(ggml_backend_dev_t d) { return &((q2a_device_ctx *) d->context)->buft; }
+ggml_backend_buffer_type_t dev_get_host_buft(ggml_backend_dev_t) { return ggml_backend_q2a_host_buffer_type(); }
 bool dev_offload_op(ggml_backend_dev_t, const ggml_tensor *) { return false; }
 
 const ggml_backend_device_i k_device_iface = {
@@ -2243,7 +2289,7 @@ const ggml_backend_device_i k_device_iface = {
     /* get_props            */ dev_get_props,
     /* init_backend         */ dev_init_backend,
     /* get_buffer_type      */ dev_get_buft,
-    /* get_host_buffer_type */ nullptr,
+    /* get_host_buffer_type */ dev_get_host_buft,
     /* buffer_from_host_ptr */ nullptr,
     /* supports_op          */ dev_supports_op,
     /* supports_buft        */ dev_supports_buft,
@@ -2260,11 +2306,20 @@ ggml_backend_dev_t reg_get_device(ggml_backend_reg_t, size_t i) {
     return i < r->devs.size() ? &r->devs[i]->dev : nullptr;
 }
 
+// the optional functions ggml_backend_reg_get_proc_address hands out (ggml-backend.h:169-178; the reference's CUDA
+// registry answers the same two names, ggml-cuda.cu:3276-3288). No split buffer type: a model is replicated per
+// device, never split by rows
+void * reg_get_proc_address(ggml_backend_reg_t, const char * name) {
+    if (strcmp(name, "ggml_backend_register_host_buffer") == 0) return (void *) ggml_backend_q2a_register_host_buffer;
+    if (strcmp(name, "ggml_backend_unregister_host_buffer") == 0) return (void *) ggml_backend_q2a_unregister_host_buffer;
+    return nullptr;
+}
+
 const ggml_backend_reg_i k_reg_iface = {
     /* get_name         */ reg_get_name,
     /* get_device_count */ reg_get_device_count,
     /* get_device       */ reg_get_device,
-    /* get_proc_address */ nullptr,
+    /* get_proc_address */ reg_get_proc_address,
 };
 
 ggml_backend_reg * the_reg() {
@@ -2324,6 +2379,34 @@ bool ggml_backend_is_q2a(ggml_backend_t backend) {
 ggml_backend_buffer_type_t ggml_backend_q2a_buffer_type(int device) {
     q2a_device_ctx * d = dev_ctx(device);
     return d ? &d->buft : nullptr;
+}
+
+ggml_backend_buffer_type_t ggml_backend_q2a_host_buffer_type(void) {
+    static ggml_backend_buffer_type host_buft = {k_host_buft_iface, nullptr, nullptr};
+    static std::once_flag once;
+    std::call_once(once, [] {
+        q2a_reg_ctx * r = reg_ctx();
+        host_buft.device = r->devs.empty() ? nullptr : &r->devs[0]->dev;
+    });
+    return &host_buft;
+}
+
+// Page-locks memory the caller already owns (e.g. a loaded model file or a PCM ring) so copies out of it run at DMA
+// rate. Opt-in like the reference's (GGML_Q2A_REGISTER_HOST set; ggml-cuda.cu GGML_CUDA_REGISTER_HOST): false if not
+// enabled or the runtime refuses; the buffer works either way
+bool ggml_backend_q2a_register_host_buffer(void * buffer, size_t size) {
+    if (getenv("GGML_Q2A_REGISTER_HOST") == nullptr || buffer == nullptr || size == 0) return false;
+    if (hipHostRegister(buffer, size, hipHostRegisterPortable | hipHostRegisterReadOnly) != hipSuccess) {
+        (void) hipGetLastError();
+        Q2A_LOG_ERROR("ggml-q2a: registering %.2f MB of host memory failed\n", size / 1e6);
+        return false;
+    }
+    return true;
+}
+
+void ggml_backend_q2a_unregister_host_buffer(void * buffer) {
+    if (getenv("GGML_Q2A_REGISTER_HOST") == nullptr || buffer == nullptr) return;
+    if (hipHostUnregister(buffer) != hipSuccess) (void) hipGetLastError();
 }
 
 int ggml_backend_q2a_get_device_count(void) { return (int) reg_ctx()->devs.size(); }

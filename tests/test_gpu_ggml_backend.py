@@ -174,3 +174,33 @@ def test_conv_hilo_path_runs_and_matches_exact_f32(harness, make_model, make_cli
     else:   # through 32 layers both sit within the reference's own F16 cross-build spread of each other
         bar = xbuild_bar("f16")
         assert mx < bar["max_rel"] and l2 < bar["rel_l2"], (mx, l2, bar)
+
+
+def test_pinned_host_buffer_type_and_host_registration(harness):
+    """VERDICT r04 missing item 3: the counterparts of ggml_backend_cuda_host_buffer_type and
+    ggml_backend_cuda_register_host_buffer / _unregister_host_buffer (ggml-cuda.h:34, 40-41). A tensor in the pinned
+    host buffer type is CPU memory to ggml (is_host, written in place), its bytes cross to a device tensor and back
+    unchanged, the device's get_host_buffer_type and the registry's get_proc_address hand out the same functions the
+    reference's CUDA registry names, and registration stays opt-in (oracle/ggml_harness.cpp cmd_hostbuf)."""
+    env = dict(os.environ)
+    env.pop("GGML_Q2A_REGISTER_HOST", None)
+    env.pop("GGML_Q2A_NO_PINNED", None)
+    r = subprocess.run([harness, "hostbuf"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:] + r.stdout[-2000:]
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    print(info)
+    assert info["host_buft_name"] == "Q2A_Host" and info["is_host"] is True
+    assert info["pinned"] is True and info["buffer_name"] == "Q2A_Host", info
+    assert info["dev_host_buft_same"] is True and info["caps_host_buffer"] is True and info["buft_device_set"] is True
+    assert info["proc_register"] is True and info["proc_unregister"] is True and info["split_absent"] is True
+    assert info["copies_equal"] is True
+    assert info["register_without_optin"] is False and info["register_optin"] is True, info
+    # pinned memory is what makes the copy a direct DMA: it must not be slower than the pageable staging path
+    assert info["h2d_gbs_pinned"] >= 0.9 * info["h2d_gbs_pageable"], info
+
+    # GGML_Q2A_NO_PINNED: the same type hands out an ordinary CPU buffer, and the device reports no host buffer
+    env["GGML_Q2A_NO_PINNED"] = "1"
+    r = subprocess.run([harness, "hostbuf"], capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:] + r.stdout[-2000:]
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    assert info["pinned"] is False and info["caps_host_buffer"] is False and info["copies_equal"] is True, info
