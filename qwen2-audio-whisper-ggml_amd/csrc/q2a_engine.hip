@@ -729,15 +729,6 @@ struct q2a_engine {
     hipStream_t stream = nullptr;
     hipStream_t pf_stream = nullptr;   // small-batch weight prefetch (prefetch_layer), created on first use
     hipEvent_t pf_ev = nullptr;
-    // partial last rounds of 8-phase GEMM tiles beside the next LayerNorm (run_block): the side stream and its
-    // fork / join events, created on first use; tail_rows = the row split of the previous layer's fc2 whose partial
-    // round may still be running (0: none). Q2A_TAIL_MODE at open (default 0: measured without gain,
-    // profiles/r05za_tail_overlap.json)
-    hipStream_t tail_stream = nullptr;
-    hipEvent_t tail_fork = nullptr, tail_join = nullptr;
-    int tail_mode = 0;   // 0 off (default: measured, no gain), 1 partial round on a top-priority side stream, 2 LayerNorm rows on a CU-masked side stream
-    bool tail_fc1 = true;   // the same for fc1 (Q4_K) beside the GELU + Q8_K quantizer (Q2A_TAIL_FC1=0: off)
-    int tail_rows = 0;
     blob_header h;
     dims d;
     int wtype = 0, blk = 0;
@@ -842,8 +833,6 @@ int engine_init(q2a_engine * e, int device) {
     HIP_TRY(hipGetDeviceCount(&n));
     if (device < 0 || device >= n) { set_err("device %d not available (%d devices)", device, n); return Q2A_ERR_HIP; }
     e->device = device;
-    if (const char * tm = getenv("Q2A_TAIL_MODE")) e->tail_mode = atoi(tm);
-    if (const char * tf = getenv("Q2A_TAIL_FC1")) e->tail_fc1 = atoi(tf) != 0;
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&e->meta_evt, hipEventDisableTiming));
@@ -1055,47 +1044,7 @@ int ln_mode(const q2a_engine * e) { return e->bf16 ? 4 : e->f32 ? 3 : e->blk == 
         }                                                                             \
     } while (0)
 
-int ensure_tail_stream(q2a_engine * e) {
-    if (e->tail_stream) return Q2A_OK;
-    // When the whole rounds end, the partial round's workgroups (a whole CU each) must get CUs before the LayerNorm's
-    // many small workgroups fill every CU — a normal-priority side stream ran the partial round after the LayerNorm.
-    // Mode 1: the partial round on a top-priority stream. Mode 2: the LayerNorm's first rows on a stream masked to 20 of
-    // every 32 CUs (12 per XCD whichever way the mask bits map to XCDs), the partial round on the main stream
-    if (e->tail_mode == 2) {
-        int dev = 0, cus = 0;
-        HIP_TRY(hipGetDevice(&dev));
-        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-        std::vector<uint32_t> mask((size_t) (cus + 31) / 32, 0u);
-        for (int i = 0; i < cus; ++i)
-            if (i % 32 < 20) mask[(size_t) i / 32] |= 1u << (i % 32);
-        HIP_TRY(hipExtStreamCreateWithCUMask(&e->tail_stream, (uint32_t) mask.size(), mask.data()));
-    } else {
-        int lo = 0, hi = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIP_TRY(hipStreamCreateWithPriority(&e->tail_stream, hipStreamNonBlocking, hi));
-    }
-    HIP_TRY(hipEventCreateWithFlags(&e->tail_fork, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&e->tail_join, hipEventDisableTiming));
-    return Q2A_OK;
-}
-
-// LayerNorm of rows [r0, r1) (every row is independent: the same bytes as one launch over all rows)
-q2a_ln_args ln_rows(q2a_ln_args a, int r0, int r1) {
-    a.X += (int64_t) r0 * a.D;
-    a.M = r1 - r0;
-    a.outH += (int64_t) r0 * a.D;
-    if (a.dy) a.dy += r0;                 // block-major [D/256][dy_ld]
-    if (a.aext) a.aext += (int64_t) r0 * 16;
-    return a;
-}
-
 // one pre-LN encoder block on X [B*T][D] (qwen2-whisper.cpp:2014-2155)
-//
-// The residual GEMMs (O, fc2) at large batches run 256x256 8-phase tiles, one per CU: 1 875 tiles at 64 clips are 7.32
-// rounds on 256 CUs, and the last 0.32 round would leave 3/4 of the chip idle for a whole tile time. Their rows are
-// split at the end of the whole rounds (q2a_gemm_round_split): the rest runs on a side stream after the whole rounds,
-// beside the row-wise LayerNorm that follows (LN2 after O in this block; LN1 of the next block after fc2), whose rows
-// outside the tail start at once. Outputs are the same bytes (the same kernels on the same rows, in another order).
 int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
     const dims & d = e->d;
     const int M = B * d.T;
@@ -1104,56 +1053,8 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         if (!e->taps[i]) return hipSuccess;
         return hipMemcpyAsync(e->taps[i], src, (size_t) M * K * e->kx * 2, hipMemcpyDeviceToDevice, s);
     };
-    // a LayerNorm right after a residual GEMM split at row `tail` (0: not split): rows [0, tail) beside the GEMM's
-    // partial round, then the rest
-    auto ln_after_tail = [&](const q2a_ln_args & ln, int tail) -> int {
-        if (tail <= 0) {
-            PLAUNCH(e, s, Q2A_PROF_LN, q2a_launch_layernorm(ln, s));
-            return Q2A_OK;
-        }
-        hipStream_t t = e->tail_stream;
-        if (e->tail_mode == 2) {   // first rows on the CU-masked stream (the partial round is queued on s)
-            HIP_TRY(hipStreamWaitEvent(t, e->tail_fork, 0));
-            PLAUNCH(e, t, Q2A_PROF_LN, q2a_launch_layernorm(ln_rows(ln, 0, tail), t));
-            HIP_TRY(hipEventRecord(e->tail_join, t));
-            PLAUNCH(e, s, Q2A_PROF_LN, q2a_launch_layernorm(ln_rows(ln, tail, M), s));
-            HIP_TRY(hipStreamWaitEvent(s, e->tail_join, 0));
-            return Q2A_OK;
-        }
-        PLAUNCH(e, s, Q2A_PROF_LN, q2a_launch_layernorm(ln_rows(ln, 0, tail), s));
-        HIP_TRY(hipStreamWaitEvent(s, e->tail_join, 0));
-        PLAUNCH(e, s, Q2A_PROF_LN, q2a_launch_layernorm(ln_rows(ln, tail, M), s));
-        return Q2A_OK;
-    };
-    // a residual GEMM: the whole rounds on s, then the partial round (mode 1: on the side stream); returns the row
-    // split (0: one launch on s)
-    auto resid_gemm = [&](const q2a_gemm_args & a, int cls, bool overlap, int & split) -> int {
-        split = 0;
-        if (overlap && e->tail_mode > 0 && (mode == 0 || mode == 1)) split = q2a_gemm_round_split(a, Q2A_EPI_RESID, e->gblk);
-        if (split > 0 && ensure_tail_stream(e) != Q2A_OK) split = 0;
-        if (split <= 0) {
-            PLAUNCH(e, s, cls, q2a_launch_gemm(a, Q2A_EPI_RESID, e->gblk, s));
-            return Q2A_OK;
-        }
-        q2a_gemm_args h = a, t = a;
-        h.M = split;
-        t.m_first = split;
-        PLAUNCH(e, s, cls, q2a_launch_gemm(h, Q2A_EPI_RESID, e->gblk, s));
-        HIP_TRY(hipEventRecord(e->tail_fork, s));
-        if (e->tail_mode == 2) {
-            PLAUNCH(e, s, cls, q2a_launch_gemm(t, Q2A_EPI_RESID, e->gblk, s));
-            return Q2A_OK;
-        }
-        HIP_TRY(hipStreamWaitEvent(e->tail_stream, e->tail_fork, 0));
-        PLAUNCH(e, e->tail_stream, cls, q2a_launch_gemm(t, Q2A_EPI_RESID, e->gblk, e->tail_stream));
-        HIP_TRY(hipEventRecord(e->tail_join, e->tail_stream));
-        return Q2A_OK;
-    };
-    int rc;
     q2a_ln_args ln{e->X, M, d.D, e->lv<const float *>(l, L_LN1W), e->lv<const float *>(l, L_LN1B), mode, e->actD, e->dyD, e->aextD, e->dy_ld};
-    rc = ln_after_tail(ln, e->tail_rows);   // the previous block's fc2 tail
-    e->tail_rows = 0;
-    if (rc) return rc;
+    PLAUNCH(e, s, Q2A_PROF_LN, q2a_launch_layernorm(ln, s));
     LAUNCH(tap(0, e->actD, d.D));
     {
         q2a_gemm_args a = gemm_base(e, l, 0, e->actD, M);
@@ -1178,16 +1079,15 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         }
     }
     LAUNCH(tap(1, e->actD, d.D));
-    int o_split = 0;
     {
         q2a_gemm_args a = gemm_base(e, l, 1, e->actD, M);
         a.bias = e->lv<const float *>(l, L_BO);
         a.outF = e->X; a.ldo = d.D;
         a.part = e->part; a.split_stride = (int64_t) M * d.D;
-        if ((rc = resid_gemm(a, Q2A_PROF_GEMM_O, true, o_split))) return rc;
+        PLAUNCH(e, s, Q2A_PROF_GEMM_O, q2a_launch_gemm(a, Q2A_EPI_RESID, e->gblk, s));
     }
     q2a_ln_args ln2{e->X, M, d.D, e->lv<const float *>(l, L_LN2W), e->lv<const float *>(l, L_LN2B), mode, e->actD, e->dyD, e->aextD, e->dy_ld};
-    if ((rc = ln_after_tail(ln2, o_split))) return rc;
+    PLAUNCH(e, s, Q2A_PROF_LN, q2a_launch_layernorm(ln2, s));
     LAUNCH(tap(2, e->actD, d.D));
     {
         q2a_gemm_args a = gemm_base(e, l, 2, e->actD, M);
@@ -1208,44 +1108,9 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
             // GELU table from LDS on the way (same codes as the GELU epilogue + quantizer below)
             q2a_half * hH = (q2a_half *) e->hF;
             a.outH = hH; a.ldo = d.F; a.o_rpg = M; a.o_gstride = 0; a.o_off = 0;
-            const uint16_t * gtab = e->g<const uint16_t *>(G_GELU);
-            // the persistent fc1's partial last round beside the GELU + quantizer of the rows already done (as for
-            // the residual GEMMs; the quantizer's one-workgroup-per-CU grid is capped to the CUs the round leaves)
-            int split = e->tail_mode > 0 && e->tail_fc1 ? q2a_gemm_round_split(a, Q2A_EPI_PRE_H, e->blk) : 0;
-            if (split > 0 && ensure_tail_stream(e) != Q2A_OK) split = 0;
-            if (split <= 0) {
-                PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_PRE_H, e->blk, s));
-                PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_gelu_quant_q8k(hH, M, d.F, gtab, e->actF, e->dyF, e->aextF, e->dy_ld, s));
-            } else {
-                q2a_gemm_args h = a, t = a;
-                h.M = split;
-                t.m_first = split;
-                int dev = 0, cus = 0;
-                HIP_TRY(hipGetDevice(&dev));
-                HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-                const int tail_grid = std::min(cus, (M - split) / 256 * (d.F / 256));
-                const int64_t off = (int64_t) split * d.F;
-                hipStream_t ts = e->tail_stream;
-                PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(h, Q2A_EPI_PRE_H, e->blk, s));
-                HIP_TRY(hipEventRecord(e->tail_fork, s));
-                if (e->tail_mode == 2) {   // quantizer's first rows on the CU-masked stream, the partial round on s
-                    HIP_TRY(hipStreamWaitEvent(ts, e->tail_fork, 0));
-                    PLAUNCH(e, ts, Q2A_PROF_QUANT, q2a_launch_gelu_quant_q8k(hH, split, d.F, gtab, e->actF, e->dyF, e->aextF,
-                                                                            e->dy_ld, ts, cus * 20 / 32));
-                    HIP_TRY(hipEventRecord(e->tail_join, ts));
-                    PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(t, Q2A_EPI_PRE_H, e->blk, s));
-                } else {                   // the partial round on the top-priority stream
-                    HIP_TRY(hipStreamWaitEvent(ts, e->tail_fork, 0));
-                    PLAUNCH(e, ts, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(t, Q2A_EPI_PRE_H, e->blk, ts));
-                    HIP_TRY(hipEventRecord(e->tail_join, ts));
-                    PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_gelu_quant_q8k(hH, split, d.F, gtab, e->actF, e->dyF, e->aextF,
-                                                                           e->dy_ld, s, cus - tail_grid));
-                    HIP_TRY(hipStreamWaitEvent(s, e->tail_join, 0));   // (the tail rows' pre-activations)
-                }
-                PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_gelu_quant_q8k(hH + off, M - split, d.F, gtab, e->actF + off,
-                                                                       e->dyF + split, e->aextF + (int64_t) split * 16, e->dy_ld, s));
-                if (e->tail_mode == 2) HIP_TRY(hipStreamWaitEvent(s, e->tail_join, 0));   // (the first rows' codes)
-            }
+            PLAUNCH(e, s, Q2A_PROF_GEMM_FC1, q2a_launch_gemm(a, Q2A_EPI_PRE_H, e->blk, s));
+            PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_gelu_quant_q8k(hH, M, d.F, e->g<const uint16_t *>(G_GELU), e->actF,
+                                                                   e->dyF, e->aextF, e->dy_ld, s));
         } else {
             // GELU output is exactly fp16-valued (LUT): keep it as fp16, then quantize for fc2
             q2a_half * hH = (q2a_half *) e->hF;
@@ -1261,10 +1126,7 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         a.bias = e->lv<const float *>(l, L_B2);
         a.outF = e->X; a.ldo = d.D;
         a.part = e->part; a.split_stride = (int64_t) M * d.D;
-        // (the last block's fc2 is read by the final pool + LayerNorm, not by a row-wise LN1: one launch)
-        int f_split = 0;
-        if ((rc = resid_gemm(a, Q2A_PROF_GEMM_FC2, l + 1 < d.L, f_split))) return rc;
-        e->tail_rows = f_split;
+        PLAUNCH(e, s, Q2A_PROF_GEMM_FC2, q2a_launch_gemm(a, Q2A_EPI_RESID, e->gblk, s));
     }
     return Q2A_OK;
 }
@@ -1395,7 +1257,6 @@ int encode_impl(q2a_engine * e, const float * pcm, int64_t stride, const int32_t
     int max_frames = 0;
     rc = prepare_meta(e, n_samples, B, offset_ms, offs, status, max_frames, stride > 0 ? stride : -1, s);   // stride 0: shared PCM
     if (rc) return rc;
-    e->tail_rows = 0;
     const bool pf = B <= Q2A_PREFETCH_MAX_B;
     if (pf && (rc = prefetch_layer(e, 0, s))) return rc;   // layer 0's weights under the front end
     rc = run_frontend(e, pcm, stride, B, max_frames, s);
@@ -1562,8 +1423,6 @@ void q2a_close(q2a_engine * e) {
     if (e->meta_evt) (void) hipEventDestroy(e->meta_evt);
     if (e->pf_stream) { (void) hipStreamSynchronize(e->pf_stream); (void) hipStreamDestroy(e->pf_stream); }
     if (e->pf_ev) (void) hipEventDestroy(e->pf_ev);
-    if (e->tail_stream) { (void) hipStreamSynchronize(e->tail_stream); (void) hipStreamDestroy(e->tail_stream); }
-    for (hipEvent_t ev : {e->tail_fork, e->tail_join}) if (ev) (void) hipEventDestroy(ev);
     if (e->stream) (void) hipStreamDestroy(e->stream);
     delete e;
 }
@@ -1809,13 +1668,8 @@ int q2a_test_block(q2a_engine * e, int layer, float * x, int n_clips, void * str
     if (rc) return rc;
     const size_t bytes = (size_t) n_clips * e->d.T * e->d.D * 4;
     HIP_TRY(hipMemcpyAsync(e->X, x, bytes, hipMemcpyDeviceToDevice, s));
-    e->tail_rows = 0;
     rc = run_block(e, layer, n_clips, s);
     if (rc) return rc;
-    if (e->tail_rows > 0 && e->tail_mode == 1) {   // fc2's partial round, still on the side stream (no LN1 here)
-        HIP_TRY(hipStreamWaitEvent(s, e->tail_join, 0));
-    }
-    e->tail_rows = 0;
     HIP_TRY(hipMemcpyAsync(x, e->X, bytes, hipMemcpyDeviceToDevice, s));
     return Q2A_OK;
 }

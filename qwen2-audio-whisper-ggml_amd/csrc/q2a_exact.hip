@@ -638,12 +638,11 @@ hipError_t q2a_launch_layernorm(const q2a_ln_args & a, hipStream_t s) {
 }
 
 hipError_t q2a_launch_gelu_quant_q8k(const q2a_half * XH, int M, int K, const uint16_t * gelu_tab, q2a_half * outH,
-                                     float * dy, q2a_half * aext, int dy_ld, hipStream_t s, int max_grid) {
+                                     float * dy, q2a_half * aext, int dy_ld, hipStream_t s) {
     if (K % 256 != 0 || M <= 0 || (int64_t) M * K >= ((int64_t) 1 << 31)) return hipErrorInvalidValue;
     int dev = 0, ncu = 256;
     (void) hipGetDevice(&dev);
     (void) hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (max_grid > 0) ncu = std::min(ncu, max_grid);
     const int64_t units = (int64_t) ((M + 15) / 16) * (K / 256);
     const unsigned grid = (unsigned) std::min<int64_t>((units + GQ_WAVES - 1) / GQ_WAVES, (int64_t) ncu);   // 144 KiB each
     hipLaunchKernelGGL(k_gelu_quant_q8k_h16, dim3(grid), dim3(GQ_THREADS), 0, s, XH, M, K / 256, gelu_tab, outH, dy, aext, dy_ld);

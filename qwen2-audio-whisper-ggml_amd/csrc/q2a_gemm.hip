@@ -2217,9 +2217,6 @@ hipError_t launch_pipe8(const q2a_gemm_args & a, hipStream_t s) {
                 return BLK == 256 ? launch_cfg<128, 256, 2, 4, EPI, BLK>(t, s) : launch_cfg<256, 256, 2, 4, EPI, BLK>(t, s);
             return launch_cfg<128, 128, 2, 2, EPI, BLK>(t, s);
         }
-        // a caller's row split (q2a_gemm_round_split: m_first at the end of the whole rounds): the partial round of a
-        // deep-K GEMM on 128x128 tiles as above, shallow K on the 8-phase tiles
-        if (Q2A_GEMM_TAIL == 1 && a.K >= 4096 && a.m_base > 0) return launch_cfg<128, 128, 2, 2, EPI, BLK>(a, s);
     }
     return launch_cfg<256, 256, 2, 4, EPI, BLK, 1>(a, s);
 }
@@ -2310,9 +2307,7 @@ int q2a_gemm_kq_ksplit(int M, int N, int K, int blk) {
 
 hipError_t q2a_launch_gemm(const q2a_gemm_args & a_in, int epi, int blk, hipStream_t s) {
     q2a_gemm_args a = a_in;
-    if (a.m_first < 0 || (a.m_first > 0 && (a.m_first >= a.M || a.m_first % 256 != 0 || a.ksplit > 1 || a.ngroup == 2)))
-        return hipErrorInvalidValue;
-    a.m_base = a.m_first;
+    a.m_base = 0;
     a.stagger_ns = Q2A_GEMM_STAGGER_NS; a.stagger_g = std::max(1, Q2A_GEMM_STAGGER_G);
     a.group_m = Q2A_GEMM_GROUP_M;
     if (a.ngroup == 2 && (epi != Q2A_EPI_STORE_F || (blk != 0 && blk != 256) || wide_tiles(a.M, a.N))) return hipErrorInvalidValue;
@@ -2337,18 +2332,6 @@ hipError_t q2a_launch_gemm(const q2a_gemm_args & a_in, int epi, int blk, hipStre
 }
 
 bool q2a_gemm_wide_tiles(int M, int N, int blk) { (void) blk; return wide_tiles(M, N); }
-
-int q2a_gemm_round_split(const q2a_gemm_args & a, int epi, int blk) {
-    if (!(epi == Q2A_EPI_RESID || epi == Q2A_EPI_PRE_H || epi == Q2A_EPI_GELU_H) || a.m_first != 0 || a.ngroup == 2) return 0;
-    if (!(pipe8_ok(a, blk) && (blk != 256 || a.beta))) return 0;
-    const int cus = cu_count();
-    const int nbn = a.N / 256, nbm = (a.M + 255) / 256;
-    const int64_t ntl = (int64_t) nbn * nbm, rem = cus > 0 ? ntl % cus : 0;
-    // (the same threshold as launch_pipe8's own deep-K split: a last round at most 5/8 full)
-    if (rem == 0 || rem * 8 > (int64_t) cus * 5) return 0;
-    const int m_main = (int) ((ntl - rem) / nbn);
-    return m_main > 0 && m_main < nbm ? m_main * 256 : 0;
-}
 
 bool q2a_gemm_pipe8(const q2a_gemm_args & a, int blk) { return pipe8_ok(a, blk) && (blk != 256 || a.beta); }
 

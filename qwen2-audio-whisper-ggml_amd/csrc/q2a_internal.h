@@ -98,8 +98,6 @@ struct q2a_gemm_args {
     int split_kq;                     // allow the small-tile split-K for k-quant / Q8_0 / Q4_0 weights (q2a_gemm_kq_ksplit)
     q2a_half * vtl;                   // Q2A_EPI_QKV: V^T lo image fp16(v - fp16(v)), same layout as vt (null = not written)
     int m_base;                       // first output row of the launch (tiles cover rows [m_base, M)); set by the launcher
-    int m_first;                      // caller: first output row to compute (0 = all of [0, M)); a GEMM split by rows
-                                      // (q2a_gemm_round_split) runs as [0, m) and [m, M) launches, same outputs bit for bit
 };
 
 // the launcher's split factor for a small-tile Q2A_EPI_RESID GEMM (0 = none): a function of K only, so every batch
@@ -115,9 +113,6 @@ constexpr int Q2A_BLK_BF16 = 1;
 // backend's conv MUL_MAT): summed this way the conv output is within rounding of the exact dot product instead of
 // carrying a 120-deep f32 accumulation chain ("the conv's own summation")
 constexpr int Q2A_BLK_EXACT = 2;
-// rows of a GEMM that fill whole rounds of 8-phase tiles (256x256, one per CU) when its last round would leave most
-// CUs idle, else 0: the caller runs rows [0, m) and then rows [m, M) (m_first = m) beside other work
-int q2a_gemm_round_split(const q2a_gemm_args & a, int epi, int blk);
 hipError_t q2a_launch_gemm(const q2a_gemm_args & a, int epi, int blk, hipStream_t s);
 // true when the launcher will use the 256-column tile configuration for this shape (Q2A_EPI_GELU_Q8K needs it)
 bool q2a_gemm_wide_tiles(int M, int N, int blk);
@@ -196,9 +191,8 @@ struct q2a_quant_args {
 hipError_t q2a_launch_quant_act(const q2a_quant_args & a, hipStream_t s);
 // GELU (ggml's fp16 table gelu_tab, 64 Ki entries, staged in LDS) of an fp16 pre-activation written by Q2A_EPI_PRE_H,
 // then Q8_K quantization — the same codes as Q2A_EPI_GELU_H + q2a_launch_quant_act(mode 1, XH). XH [M][K], K % 256 == 0.
-// The grid is one workgroup per CU (grid-stride over the rows); max_grid > 0 caps it (CUs left to other work).
 hipError_t q2a_launch_gelu_quant_q8k(const q2a_half * XH, int M, int K, const uint16_t * gelu_tab, q2a_half * outH,
-                                     float * dy, q2a_half * aext, int dy_ld, hipStream_t s, int max_grid = 0);
+                                     float * dy, q2a_half * aext, int dy_ld, hipStream_t s);
 
 // One ggml weight matrix [N][K] (raw ggml rows, host memory; F16 / Q4_K / Q8_0 / Q4_0) packed into the GEMM's
 // operand layout: fp16 W' [N][K] plus the block-major scale arrays, at byte offsets off[0..5] = W, DX, DMIN, WEXT,
