@@ -125,9 +125,6 @@ __device__ __forceinline__ float sub_half(float p, half2_t h) {
 #define Q2A_ATTN_S_SCHED 1   // sched_group_barrier interleaving (0: the compiler's own order; diagnostic builds)
 #endif
 constexpr int KS = 32;   // keys per tile
-#ifndef Q2A_ATTN_FUSE_Q8K   // 0: never write the Q8_K operand in the attention kernel (the separate quantizer runs)
-#define Q2A_ATTN_FUSE_Q8K 1
-#endif
 // fp16 remainder pair p - h (h = the truncated fp16 pair of p0, p1) in two v_fma_mix{lo,hi}_f16: the exact f32
 // difference rounded once to fp16 (RNE), written straight into the packed register
 __device__ __forceinline__ half2_t rem_pair(float p0, float p1, half2_t h) {
@@ -158,31 +155,6 @@ __device__ __forceinline__ float sum_lane32(float x) {
     const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
     return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
-__device__ __forceinline__ int min_lane16_i(int x) {
-    const auto r = __builtin_amdgcn_permlane16_swap((unsigned) x, (unsigned) x, false, false);
-    return min((int) r[0], (int) r[1]);
-}
-__device__ __forceinline__ int min_lane32_i(int x) {
-    const auto r = __builtin_amdgcn_permlane32_swap((unsigned) x, (unsigned) x, false, false);
-    return min((int) r[0], (int) r[1]);
-}
-__device__ __forceinline__ int sum_lane16_i(int x) {
-    const auto r = __builtin_amdgcn_permlane16_swap((unsigned) x, (unsigned) x, false, false);
-    return (int) r[0] + (int) r[1];
-}
-__device__ __forceinline__ int sum_lane32_i(int x) {
-    const auto r = __builtin_amdgcn_permlane32_swap((unsigned) x, (unsigned) x, false, false);
-    return (int) r[0] + (int) r[1];
-}
-
-// HG = 1: one workgroup = 128 queries of one (clip, head). HG = 4 (q2a_attention_fuses_q8k): the same workgroup runs
-// the four heads of one 256-column block of the output rows one after the other (the per-head arithmetic unchanged),
-// and after the fourth writes the O-projection's Q8_K operand of its 128 rows x 256 columns itself — each lane then
-// holds 64 of a row's 256 values (its own f32 stores of the first three heads read back, the fourth from registers),
-// the row's other three quarters in the lanes l ^ 16, l ^ 32, l ^ 48: quantize_row_q8_K_ref (ggml-quants.c:3785-3822)
-// with the block reductions as v_permlane16/32_swap pairs, the same operations as q2a_quant.h's quant_q8k_blocks, so
-// the codes, d and bsums are those of the separate quantizer pass it replaces (batch-invariance tests).
-template <int HG>
 __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
     constexpr int KROW = 128, VROW = 64;
     constexpr int KIMG = KS * KROW, VIMG = 64 * VROW;
@@ -195,14 +167,10 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
     const int nq = (T + 127) / 128, total = (int) gridDim.x;
     const int L = (int) blockIdx.x;
     const int w = (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);   // XCD-contiguous work order: the q-tiles of one (clip, head) on one XCD
-    const int ng = p.H / HG;
-    const int qt = w % nq, hg = (w / nq) % ng, clip = w / (nq * ng);
+    const int qt = w % nq, h = (w / nq) % p.H, clip = w / (nq * p.H);
     const int q0 = qt * 128 + wave * 32;
     const int64_t rowbase = (int64_t) clip * T;
     const int c16 = lane & 15, g = lane >> 4;
-#pragma unroll 1
-    for (int hh = 0; hh < HG; ++hh) {
-    const int h = hg * HG + hh;
 
     // Q fragments (B operand): query 16qb + c16, d = 32ds + 8g .. +7
     half8 qh[2][2], ql[2][2];
@@ -512,88 +480,6 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
         iter(ldsA, ldsC, ldsB, t + 2);
     }
 
-    if (HG > 1 && hh == HG - 1) {   // the group's last head: the Q8_K operand of the 256-column block
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // (this lane's own f32 stores of the first heads)
-#pragma unroll
-        for (int qb = 0; qb < 2; ++qb) {
-            const float inv = 1.0f / sum_lane32(sum_lane16(l_run[qb]));
-            const int q = q0 + 16 * qb + c16;
-            const bool ok = q < T;
-            const int64_t row = rowbase + (ok ? q : 0);
-            // x[hh2][db][r] = column 64 hh2 + 16 db + 4 g + r of the block (this lane's 64; element order = column order)
-            f4v_t x[HG][4];
-#pragma unroll
-            for (int hh2 = 0; hh2 < HG; ++hh2)
-#pragma unroll
-                for (int db = 0; db < 4; ++db) {
-                    if (hh2 == HG - 1) {
-                        x[hh2][db] = o[qb][db] * inv;
-                    } else {
-                        const float4 t4 = ok ? *(const float4 *) (p.outF + row * D + (hg * HG + hh2) * 64 + 16 * db + 4 * g)
-                                             : make_float4(0.f, 0.f, 0.f, 0.f);
-                        x[hh2][db] = f4v_t{t4.x, t4.y, t4.z, t4.w};
-                    }
-                }
-            // max |x| of the row's block and the signed value of its FIRST occurrence (lowest column)
-            float am = 0.f;
-#pragma unroll
-            for (int hh2 = 0; hh2 < HG; ++hh2)
-#pragma unroll
-                for (int db = 0; db < 4; ++db)
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) am = fmaxf(am, fabsf(x[hh2][db][r]));
-            const float amax = max_lane32(max_lane16(am));
-            int cf = 1 << 20;
-            float vf = 0.f;
-#pragma unroll
-            for (int hh2 = HG - 1; hh2 >= 0; --hh2)
-#pragma unroll
-                for (int db = 3; db >= 0; --db)
-#pragma unroll
-                    for (int r = 3; r >= 0; --r)
-                        if (fabsf(x[hh2][db][r]) == amax) { cf = 64 * hh2 + 16 * db + 4 * g + r; vf = x[hh2][db][r]; }
-            const int cmin = min_lane32_i(min_lane16_i(cf));
-            const float mx = sum_lane32(sum_lane16(cf == cmin ? vf : 0.f));   // one lane holds it
-            float dq = 1.f;   // all-zero block: see quant_q8k_block
-            int sb[2 * HG];
-#pragma unroll
-            for (int j = 0; j < 2 * HG; ++j) sb[j] = 0;
-            const float iscale = -127.f / mx;
-            q2a_half * crow = p.outQ + row * D + hg * 256 + 4 * g;
-#pragma unroll
-            for (int hh2 = 0; hh2 < HG; ++hh2)
-#pragma unroll
-                for (int db = 0; db < 4; ++db) {
-                    int qv[4] = {0, 0, 0, 0};
-                    if (amax != 0.f) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) qv[r] = min(127, (int) rintf(iscale * x[hh2][db][r]));
-                    }
-                    if (ok) *(half4 *) (crow + 64 * hh2 + 16 * db) = half4{(_Float16) (float) qv[0], (_Float16) (float) qv[1],
-                                                                          (_Float16) (float) qv[2], (_Float16) (float) qv[3]};
-                    sb[2 * hh2 + (db >> 1)] += qv[0] + qv[1] + qv[2] + qv[3];
-                }
-            if (amax != 0.f) dq = 1 / iscale;
-            // bsum32 of sub-block j (columns 32j .. 32j + 31: 8 in each of the row's four lanes); lane g stores head
-            // g's two as (hi, lo) = (floor(s / 64), s - 64 hi), the layout quant_q8k_blocks writes
-            half4 bs;
-#pragma unroll
-            for (int j = 0; j < 2 * HG; ++j) {
-                const int st = sum_lane32_i(sum_lane16_i(sb[j]));
-                const int hi2 = (st >= 0) ? (st >> 6) : -((-st + 63) >> 6);
-                const int lo2 = st - 64 * hi2;
-                if ((j >> 1) == g) {
-                    bs[2 * (j & 1)] = (_Float16) (float) hi2;
-                    bs[2 * (j & 1) + 1] = (_Float16) (float) lo2;
-                }
-            }
-            if (ok) {
-                *(half4 *) (p.qaext + ((int64_t) hg * p.q_ld + row) * 16 + 4 * g) = bs;
-                if (g == 0) p.qdy[(int64_t) hg * p.q_ld + row] = dq;
-            }
-        }
-        continue;
-    }
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
         const float l_tot = sum_lane32(sum_lane16(l_run[qb]));
@@ -615,7 +501,6 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
             }
         }
     }
-    }   // heads of the group
 }
 
 // ---- ping-pong variant (default): one 512-thread workgroup = 8 waves x 32 queries (256 queries of one (clip, head)),
@@ -863,21 +748,6 @@ bool q2a_attention_wants_vlo() { return Q2A_ATTN_VHL != 0; }
 #ifndef Q2A_ATTN_LAUNCH
 #define Q2A_ATTN_LAUNCH q2a_launch_attention
 #endif
-// Q8_K operand written by the attention kernel: reference contract, f32 output, whole 256-column blocks of four heads,
-// and enough four-head workgroups to fill the chip three deep (three per CU) — a single clip keeps one head per
-// workgroup (60 four-head workgroups would leave most CUs idle) and the separate quantizer
-bool q2a_attention_fuses_q8k(const q2a_attn_args & a) {
-    if (a.bf16 || !a.outQ || !a.outF || !a.qdy || !a.qaext || a.H % 4 != 0 || a.q_ld < a.n_clips * a.T) return false;
-    static const bool off = Q2A_ATTN_FUSE_Q8K == 0 || getenv("Q2A_NO_ATTN_Q8K") != nullptr;   // (A/B switch)
-    if (off) return false;
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) {
-        (void) hipGetLastError();
-        cus = 256;
-    }
-    return (int64_t) ((a.T + 127) / 128) * (a.H / 4) * a.n_clips >= 3 * (int64_t) cus;
-}
-
 hipError_t Q2A_ATTN_LAUNCH(const q2a_attn_args & a, hipStream_t s) {
     if (a.D != a.H * 64 || a.TP < ((a.T + KT - 1) / KT) * KT) return hipErrorInvalidValue;
     if (a.bf16) {
@@ -886,10 +756,7 @@ hipError_t Q2A_ATTN_LAUNCH(const q2a_attn_args & a, hipStream_t s) {
         hipLaunchKernelGGL(k_attn_pp<true>, dim3(((a.T + 255) / 256) * a.H * a.n_clips), dim3(512), 0, s, a);
     } else {
         if (!a.vtl) return hipErrorInvalidValue;
-        if (q2a_attention_fuses_q8k(a))
-            hipLaunchKernelGGL(k_attn_t<4>, dim3(((a.T + 127) / 128) * (a.H / 4) * a.n_clips), dim3(256), 0, s, a);
-        else
-            hipLaunchKernelGGL(k_attn_t<1>, dim3(((a.T + 127) / 128) * a.H * a.n_clips), dim3(256), 0, s, a);
+        hipLaunchKernelGGL(k_attn_t, dim3(((a.T + 127) / 128) * a.H * a.n_clips), dim3(256), 0, s, a);
     }
     return hipGetLastError();
 }

@@ -1069,14 +1069,11 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         q2a_attn_args at{e->qh, e->ql, e->kh, e->kl, e->vt, B, d.T, d.D, d.H, e->TP, nullptr, nullptr, e->bf16 ? 1 : 0};
         at.vtl = e->vtl;
         if (mode == 0 || mode == 4) at.outH = e->actD; else at.outF = e->attF;
-        if (mode == 1) {   // Q8_K of the O-projection input written by the attention itself when the batch is large
-            at.outQ = e->actD; at.qdy = e->dyD; at.qaext = e->aextD; at.q_ld = e->dy_ld;
-        }
         PLAUNCH(e, s, Q2A_PROF_ATTN, q2a_launch_attention(at, s));
         if (mode == 3) {
             const int64_t n = (int64_t) M * d.D;
             PLAUNCH(e, s, Q2A_PROF_QUANT, launch_split3(e->attF, e->actD, d.D, n, s));
-        } else if ((mode == 1 && !q2a_attention_fuses_q8k(at)) || mode == 2) {
+        } else if (mode == 1 || mode == 2) {
             q2a_quant_args qa{e->attF, nullptr, M, d.D, mode, e->actD, e->dyD, e->aextD, e->dy_ld};
             PLAUNCH(e, s, Q2A_PROF_QUANT, q2a_launch_quant_act(qa, s));
         }

@@ -127,17 +127,7 @@ struct q2a_attn_args {
     float * outF;        // [clips*T][D] f32  (quantized paths)
     int bf16;            // bf16-activation mode: qh/kh/vt and outH hold bf16, ql/kl unused, one MFMA per QK^T step
     const q2a_half * vtl;   // V^T lo image (v - fp16(v)) when q2a_attention_wants_vlo(), else unused
-    // reference contract, quantized weights: with outQ set the kernel also writes the O-projection's Q8_K operand —
-    // codes [clips*T][D] (fp16 integers), block-major d [D/256][q_ld] and bsum operand [D/256][q_ld][16] — the bytes
-    // q2a_launch_quant_act(mode 1) makes of outF (outF still receives the f32 output). Taken only when the batch fills
-    // the chip with workgroups of four heads (q2a_attention_fuses_q8k); the caller runs the quantizer otherwise
-    q2a_half * outQ;
-    float * qdy;
-    q2a_half * qaext;
-    int q_ld;
 };
-// true when q2a_launch_attention writes the Q8_K operand itself for these arguments (outQ set)
-bool q2a_attention_fuses_q8k(const q2a_attn_args & a);
 // Reference contract (bf16 == 0): qh/ql hold Q * Q2A_LOG2E (after the 1/sqrt(dh) scale), split hi/lo — the kernel
 // works in log2 units (P = exp2(S' - m')); every producer (QKV epilogue qscale, ggml backend prep, test entry) folds it.
 // bf16 contract: qh holds Q scaled by 1/sqrt(dh) only.
