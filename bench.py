@@ -218,7 +218,7 @@ def host_cpu_info() -> dict:
 
 
 # The profile set measured on the current tree; its summaries are cited ahead of older rounds' (tags do not sort
-# by date: r04y was taken after r04z; r05x is the round-5 closing set).
+# by date: r04y was taken after r04z, and r05w, not r05x, is the round-5 closing set).
 PROFILE_TAG = "r05w"
 
 
@@ -241,6 +241,113 @@ def fc1_kernel_label(wt: str, bf16: bool, M: int) -> str:
     return f"k_gemm<128,128,2,2,{epi},{blk},0>"
 
 
+# the matrix-core kernel classes (Q2A_PROF_*: QKV, attention, O, fc1, fc2), one launch per layer each
+ROOF_CLASSES = (4, 5, 7, 8, 9)
+
+
+def roof_flop_per_launch(cls: int, clips: int) -> float:
+    """Algorithmic flops of one launch of a class: 2.M.N.K for the weight GEMMs (M = 1500 x clips),
+    4.T^2.D per clip for the attention (QK^T and P.V)."""
+    M = T * clips
+    return {4: 2.0 * M * 3 * D * D, 5: 2 * 2.0 * T * T * D * clips, 7: 2.0 * M * D * D, 8: 2.0 * M * F * D,
+            9: 2.0 * M * D * F}[cls]
+
+
+def roof_label(cls: int, wt: str, bf16: bool, clips: int) -> str:
+    M = T * clips
+    if cls == 5:
+        return ("attention (k_attn_pp<true>: bf16 contract, one bf16 MFMA per product)" if bf16 else
+                "attention (k_attn_t: F32-class contract, 3 fp16 MFMA terms per product), T=1500 D=1280 H=20")
+    if cls == 8:
+        return "gemm_fc1 (%s), M=%d N=5120 K=1280" % (fc1_kernel_label(wt, bf16, M), M)
+    return {4: "gemm_qkv, M=%d N=3840 K=1280", 7: "gemm_o, M=%d N=1280 K=1280",
+            9: "gemm_fc2 (8-phase main rounds + 128x128 tail at 64 clips), M=%d N=1280 K=5120"}[cls] % M
+
+
+def committed_counter(config: str, cls: int, suffix: str, field: str):
+    """A kernel class's figure from the committed profile summaries of this workload (the PROFILE_TAG set last)."""
+    pdir = os.path.join(ROOT, "profiles")
+    if not os.path.isdir(pdir):
+        return None, None
+    files = _profile_files(f for f in os.listdir(pdir) if f.endswith(f"_{config}_{suffix}.json"))
+    if not files:
+        return None, None
+    with open(os.path.join(pdir, files[-1])) as f:
+        kern = json.load(f)["kernels"]
+    name = PROF_NAMES[cls]
+    for k, e in kern.items():
+        if (k == name or e.get("class") == name) and field in e:
+            return e[field], "profiles/" + files[-1]
+    return None, None
+
+
+def roofline_of(cls: int, timed_ms, timed_n, config: str, wt: str, bf16: bool, clips: int) -> dict:
+    """roofline object of one class: achieved = algorithmic flops per launch / its average launch time (HIP events on
+    the engine's stream over the timed region), against the dense fp16 / bf16 MFMA peak (the MFMA dtype issued, also
+    for the integer k-quant dots); traffic = HBM bytes per launch (PMC FETCH_SIZE x2 + WRITE_SIZE, separate passes)
+    and the SQ MFMA busy fraction from the committed summaries of this workload."""
+    avg_s = timed_ms[cls] / max(1, timed_n[cls]) / 1e3
+    flop = roof_flop_per_launch(cls, clips)
+    achieved = flop / avg_s / 1e12 if avg_s > 0 else 0.0
+    same_batch = clips == CONFIGS[config][1]
+    traffic, tsrc = committed_counter(config, cls, "pmc_traffic", "hbm_bytes_per_launch_corrected") if same_batch else (None, None)
+    busy, bsrc = committed_counter(config, cls, "sq_mfma", "mfma_busy_frac") if same_batch else (None, None)
+    r = {"bound": "mfma", "kernel": roof_label(cls, wt, bf16, clips), "achieved": round(achieved, 1),
+         "peak": PEAK_FP16_MFMA_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP16_MFMA_TFLOPS, 4),
+         "traffic": traffic, "traffic_unit": "bytes/launch", "traffic_source": tsrc,
+         "flop_per_launch": flop, "avg_launch_ms": round(avg_s * 1e3, 4), "launches_timed": int(timed_n[cls]),
+         "mfma_busy_frac": round(busy, 4) if busy is not None else None, "mfma_busy_source": bsrc}
+    if cls == 5 and not bf16:
+        r.update({"issued_tflops": round(3 * achieved, 1), "issued_frac": round(3 * achieved / PEAK_FP16_MFMA_TFLOPS, 4),
+                  "issued_note": "3 fp16 MFMA terms per algorithmic product (F32-class QK^T and P.V, DESIGN.md §2)"})
+    return r
+
+
+def c_group_leg(args, model_path: str, clips_per_gpu: int) -> dict:
+    """The one-process multi-GPU C ABI (q2a_group_open_with + q2a_group_encode_host) at the visible
+    device count, in a child process (this one holds its own engine; the child's failure or hang cannot take the
+    bench line with it): an engine from the model file, ONE RCCL broadcast of its device-layout weights to every other
+    visible device, then clips_per_gpu x devices clips from pageable host memory (PCIe both ways included)."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--c-group-child", "--config", args.config, "--workdir",
+           args.workdir, "--clips", str(clips_per_gpu)]
+    try:
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=dict(os.environ, Q2A_GROUP_MODEL=model_path))
+        if r.returncode != 0:
+            return {"error": f"rc {r.returncode}: " + r.stderr.strip()[-300:]}
+        return json.loads(r.stdout.strip().splitlines()[-1])
+    except Exception as ex:  # noqa: BLE001
+        return {"error": str(ex)[:300]}
+
+
+def c_group_child(args) -> None:
+    import q2a
+    model_path = os.environ["Q2A_GROUP_MODEL"]
+    t0 = time.time()
+    eng = q2a.Engine(model_path, device=0, act=q2a.ACT_BF16 if "bf16" in args.config else q2a.ACT_REFERENCE)
+    t_open = time.time() - t0
+    t0 = time.time()
+    g = q2a.Group(engine=eng)
+    t_group = time.time() - t0
+    n = g.size * args.clips
+    pcm = synth_clips(0, n)
+    clips = [pcm[c] for c in range(n)]
+    out = np.empty((n,) + g.out_shape, dtype=np.float32)
+    g.encode_host(clips, out=out)   # staging buffers and workspaces grown here
+    reps = 2
+    ts = time.perf_counter()
+    for _ in range(reps):
+        _, st = g.encode_host(clips, out=out)
+    dt = (time.perf_counter() - ts) / reps
+    assert (st == q2a.CLIP_ENCODED).all() and np.isfinite(out).all()
+    res = {"devices": g.size, "clips": n, "frames_per_s": round(n * T_MEL / dt, 1), "s_per_call": round(dt, 4),
+           "engine_open_s": round(t_open, 3), "group_open_s": round(t_group, 3), "setup": g.setup_times(),
+           "source": "q2a_group_open_with over an engine opened from the model file; q2a_group_encode_host from "
+                     "pageable host arrays (PCIe in and out included), one host thread per device"}
+    g.close()
+    eng.close()
+    print(json.dumps(res), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -253,7 +360,11 @@ def main():
                     help="skip the PCIe-inclusive and host-API legs (profiles/collect.sh: every launch is then the workload's own batch)")
     ap.add_argument("--cpu-reps", type=int, default=2)   # ~7 s of reference CPU work on 16 threads (+ legs)
     ap.add_argument("--workdir", default=os.environ.get("Q2A_BENCH_DIR", os.path.join(tempfile.gettempdir(), "q2a_bench")))
+    ap.add_argument("--no-c-group", action="store_true", help="skip the one-process multi-GPU C ABI leg (c_group)")
+    ap.add_argument("--c-group-child", action="store_true", help=argparse.SUPPRESS)
     args = ap.parse_args()
+    if args.c_group_child:
+        return c_group_child(args)
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args.gpus))
@@ -326,10 +437,11 @@ def main():
         step()
     torch.cuda.synchronize()
     lib = q2a.lib()
-    # inside the timed region HIP events bracket only the roofline kernel (fc1, Q2A_PROF_GEMM_FC1 = 8) on the
-    # engine's stream; the per-kernel breakdown comes from a separate fully-profiled pass after it
+    # inside the timed region HIP events bracket only the roofline candidates (the matrix-core classes: QKV, attention,
+    # O, fc1, fc2 = Q2A_PROF_* 4, 5, 7, 8, 9) on the engine's stream; the per-kernel breakdown of every class comes from
+    # a separate fully-profiled pass after it
     lib.q2a_profile_enable_mask.argtypes = [C.c_void_p, C.c_uint]
-    lib.q2a_profile_enable_mask(C.c_void_p(eng.h), 1 << 8)
+    lib.q2a_profile_enable_mask(C.c_void_p(eng.h), sum(1 << i for i in ROOF_CLASSES))
     prof_ms = (C.c_double * 11)()
     prof_n = (C.c_int64 * 11)()
     lib.q2a_profile_read(C.c_void_p(eng.h), prof_ms, prof_n, 11, 1)
@@ -345,7 +457,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - ts
     lib.q2a_profile_read(C.c_void_p(eng.h), prof_ms, prof_n, 11, 0)
-    fc1_ms, fc1_n = prof_ms[8], prof_n[8]
+    timed_ms, timed_n = list(prof_ms), list(prof_n)
     # breakdown pass (not timed): every kernel class bracketed by events
     brk_steps = max(1, min(args.steps, 3))
     lib.q2a_profile_enable(C.c_void_p(eng.h), 1)
@@ -412,13 +524,9 @@ def main():
 
     per_kernel = {PROF_NAMES[i]: {"ms_per_step": round(prof_ms[i] / brk_steps, 3),
                                   "launches_per_step": int(prof_n[i] // brk_steps)} for i in range(11)}
-    # dominant kernel: the fc1 weight GEMM (largest single GEMM; its own kernel instantiation in rocprof), its
-    # average launch time from the events of the timed region
-    fc1_avg_s = fc1_ms / max(1, fc1_n) / 1e3
-    fc1_flop = FLOP_FC1_PER_CLIP * clips_per_gpu
-    achieved = fc1_flop / fc1_avg_s / 1e12
     gemm_ms = prof_ms[4] + prof_ms[7] + prof_ms[8] + prof_ms[9]
     gemm_tf = FLOP_WEIGHT_GEMMS_PER_CLIP * clips_per_gpu * brk_steps / (gemm_ms / 1e3) / 1e12
+    bf16 = "bf16" in args.config
     # every matrix-core kernel class against the same fp16 MFMA peak, ALGORITHMIC flops: the
     # attention's F32-class contract issues 3 MFMA terms per product and the conv's exact accumulation 3 operand
     # parts, neither counted here
@@ -427,37 +535,28 @@ def main():
         if prof_ms[i] > 0:
             tf = fl * clips_per_gpu * brk_steps / (prof_ms[i] / 1e3) / 1e12
             per_kernel[PROF_NAMES[i]].update({"tflops": round(tf, 1), "mfma_frac": round(tf / PEAK_FP16_MFMA_TFLOPS, 4)})
-            if i == 5 and "bf16" not in args.config:
+            if i == 5 and not bf16:
                 # the MFMA work the reference contract's attention issues: S = Kh.Qh + Kl.Qh + Kh.Ql and
                 # O += Vh.Ph + Vh.Pl + Vl.Ph, three 16x16x32 products per algorithmic one
                 per_kernel[PROF_NAMES[i]].update({"issued_tflops": round(3 * tf, 1),
                                                   "issued_mfma_frac": round(3 * tf / PEAK_FP16_MFMA_TFLOPS, 4)})
 
-    # HBM traffic of the same kernel from the committed rocprofv3 PMC passes of this workload (FETCH_SIZE and
-    # WRITE_SIZE in separate passes, FETCH_SIZE x2 gfx950 correction); null when no summary matches.
-    traffic, traffic_src = None, None
-    pmc_files = _profile_files(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith(f"_{args.config}_pmc_traffic.json")) \
-        if os.path.isdir(os.path.join(ROOT, "profiles")) else []
-    if pmc_files and clips_per_gpu == CONFIGS[args.config][1]:
-        with open(os.path.join(ROOT, "profiles", pmc_files[-1])) as f:
-            k = json.load(f)["kernels"].get("gemm_fc1", {})
-        if "hbm_bytes_per_launch_corrected" in k:
-            traffic, traffic_src = k["hbm_bytes_per_launch_corrected"], "profiles/" + pmc_files[-1]
-
-    # MFMA busy fraction of the same kernel from the committed SQ counter pass (profiles/collect_sq.sh +
-    # sq_summary.py): SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs x 1024 SIMDs), rocprof's MfmaUtil
-    mfma_busy, mfma_src = None, None
-    sq_files = _profile_files(f for f in os.listdir(os.path.join(ROOT, "profiles")) if f.endswith(f"_{args.config}_sq_mfma.json")) \
-        if os.path.isdir(os.path.join(ROOT, "profiles")) else []
-    if sq_files:
-        with open(os.path.join(ROOT, "profiles", sq_files[-1])) as f:
-            for e in json.load(f)["kernels"].values():
-                if e.get("class") == "gemm_fc1" and "mfma_busy_frac" in e:
-                    mfma_busy, mfma_src = round(e["mfma_busy_frac"], 4), "profiles/" + sq_files[-1]
+    # the roofline objects: the DOMINANT kernel class (largest time per step in the breakdown pass among the matrix-core
+    # classes, each one launch per layer) and the fc1 GEMM (north_star's "Q4_K encoder matmuls"), each from its own
+    # events over the timed region
+    dominant = max(ROOF_CLASSES, key=lambda i: prof_ms[i])
+    roofline = roofline_of(dominant, timed_ms, timed_n, args.config, wt, bf16, clips_per_gpu)
+    roofline["dominant"] = True
+    roofline["share_of_step"] = round(prof_ms[dominant] / brk_steps / (elapsed / args.steps * 1e3), 4)
+    roofline_fc1 = roofline_of(8, timed_ms, timed_n, args.config, wt, bf16, clips_per_gpu)
+    roofline_fc1["all_weight_gemms_tflops"] = round(gemm_tf, 1)
 
     cpu = None
     if ws == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(model_path, wt, args.workdir, args.cpu_reps)
+    c_group = None
+    if ws == 1 and not args.no_c_group and not args.no_host_legs:
+        c_group = c_group_leg(args, model_path, clips_per_gpu)
 
     res = {
         "metric": "encoder audio-frames/sec (30 s clips) at 1/2/4/8 MI355X; MFMA util %",
@@ -479,15 +578,10 @@ def main():
                    "seq_len": T_MEL, "parallelism": f"dp{ws}"},
         "clips_per_s": round(total_clips / elapsed, 3),
         "tflops_total": round(FLOP_PER_CLIP * total_clips / elapsed / 1e12, 1),
-        "roofline": {"bound": "mfma", "kernel": "gemm_fc1 (%s), M=%d N=5120 K=1280" % (fc1_kernel_label(
-                         wt, "bf16" in args.config, T * clips_per_gpu), T * clips_per_gpu),
-                     "achieved": round(achieved, 1), "peak": PEAK_FP16_MFMA_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_FP16_MFMA_TFLOPS, 4), "traffic": traffic,
-                     "traffic_unit": "bytes/launch", "traffic_source": traffic_src,
-                     "flop_per_launch": fc1_flop, "avg_launch_ms": round(fc1_avg_s * 1e3, 4),
-                     "all_weight_gemms_tflops": round(gemm_tf, 1),
-                     "mfma_busy_frac": mfma_busy, "mfma_busy_source": mfma_src},
+        "roofline": roofline,
+        "roofline_gemm_fc1": roofline_fc1,
         "cpu_baseline": cpu,
+        "c_group": c_group,
         "pcie_inclusive_frames_per_s": round(pcie_rate, 1) if pcie_rate else None,
         "pcie_inclusive_source": f"{pcie_steps} batches from pinned host memory, H2D / D2H double-buffered on a copy stream",
         "host_api_frames_per_s": round(host_rate, 1) if host_rate else None,

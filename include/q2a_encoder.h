@@ -143,6 +143,12 @@ int q2a_device_count(void);   /* visible HIP devices (0 when none) */
  * ncclBroadcast over xGMI (RCCL communicators from ncclCommInitAll); each device expands its copy into the device
  * layout. act: Q2A_ACT_REFERENCE / Q2A_ACT_BF16. NULL on error (q2a_last_error). */
 q2a_group * q2a_group_open(const char * model_path, const int * devices, int n_devices, int act);
+/* The same over an engine that is already open (its weights, activation contract and device): base's device must be
+ * in devices[0..n_devices) (n_devices = 0: base's device first, then every other visible device). base's own
+ * device-layout weights are the root of the ONE ncclBroadcast (no second pack of the model file, no second replica on
+ * base's device: that device's group engine shares base's weights, q2a_open_shared); every other device keeps the
+ * replica it received. base must outlive the group. NULL on error (q2a_last_error). */
+q2a_group * q2a_group_open_with(q2a_engine * base, const int * devices, int n_devices);
 void q2a_group_close(q2a_group * g);
 int q2a_group_size(const q2a_group * g);
 q2a_engine * q2a_group_engine(q2a_group * g, int i);   /* the engine of the group's i-th device (owned by the group) */
@@ -155,7 +161,8 @@ int q2a_group_split(int n_clips, int n_devices, int i, int * first, int * count)
  * out_host report Q2A_CLIP_FAILED. */
 int q2a_group_encode_host(q2a_group * g, const float * const * pcm, const int32_t * n_samples, const int32_t * offsets_ms,
                           int n_clips, int offset_ms, float * out_host, int32_t * status);
-/* Start-up cost of q2a_group_open: host pack, H2D + broadcast, per-device expand (seconds), transport bytes. */
+/* Start-up cost of q2a_group_open: host pack, H2D + broadcast, per-device expand (seconds), transport bytes
+ * (q2a_group_open_with: pack 0, the broadcast, the engines' open; the device-layout bytes broadcast). */
 int q2a_group_setup_times(const q2a_group * g, double * pack_s, double * broadcast_s, double * open_s, int64_t * blob_bytes);
 
 /* ---- per-kernel timing (HIP events recorded on the launch stream around every kernel of a class) ---- */

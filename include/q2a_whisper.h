@@ -6,7 +6,9 @@
  *   whisper_init_from_file_with_params   qwen2-whisper.h:141   (-> q2a_open on params.gpu_device)
  *   whisper_full / whisper_full_with_state  :446 / :452       (mel -> window at offset_ms -> encode; embd_enc kept)
  *   whisper_full_parallel                :464   (declared but never defined by the reference; here: n_processors
- *                                                 contiguous chunks of the input, encoded as one batch)
+ *                                                 contiguous chunks of the input, encoded as one batch — spread over
+ *                                                 gpu_device and the other visible devices, at most
+ *                                                 Q2A_PARALLEL_DEVICES of them, on one replica per device)
  *   whisper_pcm_to_mel / whisper_n_len   :211 / :288
  *   whisper_encode                        :245   (encode the stored mel at `offset` frames)
  *   whisper_print_emb_enc                 :527   (first 20 values of embd_enc, " %.3f" each)
@@ -167,6 +169,10 @@ const float * whisper_get_embd_enc_from_state(struct whisper_state * state, int 
 /* whisper_full_parallel results: chunk i's embd_enc (NULL if that chunk was under 1 s and skipped) */
 int whisper_full_n_chunks(struct whisper_context * ctx);
 const float * whisper_get_embd_enc_chunk(struct whisper_context * ctx, int i_chunk);
+
+/* The engine that holds the context's weights (q2a_encoder.h), for callers that batch clips through the engine API
+ * or open a q2a_group_open_with over it without loading the model again. Owned by the context. */
+struct q2a_engine * q2a_whisper_context_engine(struct whisper_context * ctx);
 
 /* Encode every 30 s window of a long recording in one batch (windows k = 0.. at offset_ms + k*30000 until the
  * audio ends; each window normalised over the whole recording, as whisper_full at that offset would). Writes

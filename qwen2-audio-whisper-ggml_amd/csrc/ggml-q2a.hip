@@ -1474,6 +1474,23 @@ packed_w get_qkv_weight(q2a_backend_ctx * b, const ggml_tensor * const w[3]) {
     }
     Q2A_HIP(hipStreamSynchronize(b->stream));
     std::lock_guard<std::mutex> lk(d->mu);
+    // the per-tensor images of Q, K and V (upload-time or lazy repacks) are not read again while the fused route is on:
+    // released, so the expanded QKV weights are resident once (a graph that still needed one repacks it lazily; the
+    // wgen bump keeps every captured graph that holds their pointers from being replayed)
+    for (size_t j = 0; j < d->wcache.size();) {
+        const packed_w & c = d->wcache[j];
+        bool own = false;
+        for (int i = 0; i < 3; ++i)
+            own |= c.raw == (const char *) w[i]->data && c.type == w[i]->type && c.N == N && c.K == K;
+        if (own) {
+            (void) hipFree(c.dev);
+            ++d->wgen;
+            d->wcache[j] = d->wcache.back();
+            d->wcache.pop_back();
+        } else {
+            ++j;
+        }
+    }
     d->wcache.push_back(p);
     return p;
 }
@@ -1770,7 +1787,9 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                 !is_weight_buffer(m->src[0]) || ((uintptr_t) m->data & 15) != 0)
                 return false;
         const int64_t D = wq->ne[1], T = x->ne[1], H = D / 64;
-        if (wq->ne[0] != D || D % 64 != 0 || x->ne[2] != 1 || x->ne[3] != 1 || T * D >= (1ll << 31)) return false;
+        // (T % 4: the epilogue's V^T stores are 4-t groups that only zero the pad columns of a group starting at or
+        // past T, q2a_gemm.hip; any other T keeps the separate projections)
+        if (wq->ne[0] != D || D % 64 != 0 || T % 4 != 0 || x->ne[2] != 1 || x->ne[3] != 1 || T * D >= (1ll << 31)) return false;
         if (!row_vec_f32(qa->src[1], D) || !row_vec_f32(va->src[1], D) || !is_weight_buffer(qa->src[1]) ||
             !is_weight_buffer(va->src[1]) || !same_shape_rows(qm, qa) || !same_shape_rows(vm, va))
             return false;

@@ -1287,6 +1287,14 @@ const char * q2a_last_error(void) { return g_err.c_str(); }
 // (q2a_internal.h) the calling thread's q2a_last_error text, for the library's other translation units
 void q2a_internal_set_error(const char * msg) { g_err = msg ? msg : ""; }
 
+int q2a_internal_engine_blob(const q2a_engine * e, const void ** blob, int64_t * bytes, int * device) {
+    if (!e || !e->blob || e->h.compact) { set_err("engine holds no device-layout weights"); return Q2A_ERR_ARG; }
+    if (blob) *blob = e->blob;
+    if (bytes) *bytes = e->blob_size;
+    if (device) *device = e->device;
+    return Q2A_OK;
+}
+
 int64_t q2a_pack_model(const char * path, void ** host_blob) { return q2a_pack_model_ex(path, Q2A_ACT_REFERENCE, host_blob); }
 
 int64_t q2a_pack_model_ex(const char * path, int act, void ** host_blob) {

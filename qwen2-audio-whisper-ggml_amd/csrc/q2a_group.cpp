@@ -24,9 +24,14 @@
 
 extern "C" void q2a_internal_set_error(const char * msg);
 
+extern "C" int q2a_internal_engine_blob(const q2a_engine * e, const void ** blob, int64_t * bytes, int * device);
+
 struct q2a_group {
     std::vector<int> dev;
     std::vector<q2a_engine *> eng;
+    // q2a_group_open_with: the received device-layout replicas the other devices' engines run on (they do not own
+    // them), released after those engines
+    std::vector<std::pair<int, void *>> held;
     int64_t blob_bytes = 0;
     double t_pack = 0, t_bcast = 0, t_open = 0;   // seconds: host pack, H2D + RCCL broadcast, expand / engine open
 };
@@ -65,17 +70,13 @@ struct bcast_bufs {
     }
 };
 
-}  // namespace
-
-extern "C" {
-
-int q2a_device_count(void) {
+int q2a_device_count_impl() {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) { (void) hipGetLastError(); return 0; }
     return n;
 }
 
-int q2a_group_split(int n_clips, int n_devices, int i, int * first, int * count) {
+int q2a_group_split_impl(int n_clips, int n_devices, int i, int * first, int * count) {
     if (n_clips < 0 || n_devices <= 0 || i < 0 || i >= n_devices || !first || !count) {
         gerr("invalid arguments");
         return Q2A_ERR_ARG;
@@ -87,22 +88,90 @@ int q2a_group_split(int n_clips, int n_devices, int i, int * first, int * count)
     return Q2A_OK;
 }
 
-q2a_group * q2a_group_open(const char * model_path, const int * devices, int n_devices, int act) {
-    if (!model_path || n_devices < 0 || (n_devices > 0 && !devices)) { gerr("invalid arguments"); return nullptr; }
+// the device list of a group: devices[0..n) checked (in range, no repeats), or every visible device when n == 0 (with
+// `first` moved to the front when >= 0)
+bool group_devices(const int * devices, int n_devices, int first, std::vector<int> & dev) {
     int visible = 0;
     if (hipGetDeviceCount(&visible) != hipSuccess || visible <= 0) {
         (void) hipGetLastError();
         gerr("no HIP device available");
-        return nullptr;
+        return false;
     }
-    std::vector<int> dev;
-    if (n_devices == 0) for (int d = 0; d < visible; ++d) dev.push_back(d);   // every visible device
-    else dev.assign(devices, devices + n_devices);
+    dev.clear();
+    if (n_devices == 0) {
+        if (first >= 0) dev.push_back(first);
+        for (int d = 0; d < visible; ++d)
+            if (d != first) dev.push_back(d);
+    } else {
+        dev.assign(devices, devices + n_devices);
+    }
     for (size_t i = 0; i < dev.size(); ++i) {
-        if (dev[i] < 0 || dev[i] >= visible) { gerr("device %d not available (%d devices)", dev[i], visible); return nullptr; }
+        if (dev[i] < 0 || dev[i] >= visible) { gerr("device %d not available (%d devices)", dev[i], visible); return false; }
         for (size_t j = 0; j < i; ++j)
-            if (dev[j] == dev[i]) { gerr("device %d listed twice", dev[i]); return nullptr; }
+            if (dev[j] == dev[i]) { gerr("device %d listed twice", dev[i]); return false; }
     }
+    return true;
+}
+
+// ONE grouped ncclBroadcast of nb bytes from src (on dev[root]) into b.buf[i] of every other device (communicators from
+// ncclCommInitAll over dev, rank i = dev[i]); b.buf[root] must be src. Q2A_OK when every device's copy has landed.
+int broadcast(bcast_bufs & b, const std::vector<int> & dev, int root, int64_t nb) {
+    const int n = (int) dev.size();
+    b.comm.assign(n, nullptr);
+    ncclResult_t r = ncclCommInitAll(b.comm.data(), n, dev.data());
+    if (r != ncclSuccess) { gerr("ncclCommInitAll over %d devices: %s", n, ncclGetErrorString(r)); return Q2A_ERR_HIP; }
+    r = ncclGroupStart();
+    for (int i = 0; i < n && r == ncclSuccess; ++i) {
+        (void) hipSetDevice(dev[i]);
+        r = ncclBroadcast(b.buf[root], b.buf[i], (size_t) nb, ncclUint8, root, b.comm[i], b.st[i]);
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess || r2 != ncclSuccess) {
+        gerr("ncclBroadcast of the weight blob: %s", ncclGetErrorString(r != ncclSuccess ? r : r2));
+        return Q2A_ERR_HIP;
+    }
+    for (int i = 0; i < n; ++i)
+        if (hipSetDevice(dev[i]) != hipSuccess || hipStreamSynchronize(b.st[i]) != hipSuccess) {
+            gerr("device %d: broadcast did not complete", dev[i]);
+            return Q2A_ERR_HIP;
+        }
+    return Q2A_OK;
+}
+
+// one stream per device and an nb-byte receive buffer on every device but `skip` (-1: on every device)
+int alloc_bufs(bcast_bufs & b, const std::vector<int> & dev, int64_t nb, int skip) {
+    const int n = (int) dev.size();
+    b.dev = dev;
+    b.buf.assign(n, nullptr);
+    b.st.assign(n, nullptr);
+    for (int i = 0; i < n; ++i) {
+        if (hipSetDevice(dev[i]) != hipSuccess || hipStreamCreateWithFlags(&b.st[i], hipStreamNonBlocking) != hipSuccess) {
+            gerr("device %d: stream creation failed", dev[i]);
+            return Q2A_ERR_HIP;
+        }
+        if (i != skip && hipMalloc(&b.buf[i], (size_t) nb) != hipSuccess) {
+            (void) hipGetLastError();
+            gerr("device %d: %.2f GB for the weight blob", dev[i], nb / 1e9);
+            return Q2A_ERR_OOM;
+        }
+    }
+    return Q2A_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int q2a_device_count(void) { return q2a_device_count_impl(); }
+
+int q2a_group_split(int n_clips, int n_devices, int i, int * first, int * count) {
+    return q2a_group_split_impl(n_clips, n_devices, i, first, count);
+}
+
+q2a_group * q2a_group_open(const char * model_path, const int * devices, int n_devices, int act) {
+    if (!model_path || n_devices < 0 || (n_devices > 0 && !devices)) { gerr("invalid arguments"); return nullptr; }
+    std::vector<int> dev;
+    if (!group_devices(devices, n_devices, -1, dev)) return nullptr;
     const int n = (int) dev.size();
     q2a_group * g = new q2a_group();
     g->dev = dev;
@@ -116,18 +185,7 @@ q2a_group * q2a_group_open(const char * model_path, const int * devices, int n_d
     int rc = Q2A_OK;
     {
         bcast_bufs b;
-        b.dev = dev;
-        b.buf.assign(n, nullptr);
-        b.st.assign(n, nullptr);
-        for (int i = 0; i < n && rc == Q2A_OK; ++i) {
-            if (hipSetDevice(dev[i]) != hipSuccess || hipStreamCreateWithFlags(&b.st[i], hipStreamNonBlocking) != hipSuccess) {
-                gerr("device %d: stream creation failed", dev[i]);
-                rc = Q2A_ERR_HIP;
-            } else if (hipMalloc(&b.buf[i], (size_t) nb) != hipSuccess) {
-                gerr("device %d: %.2f GB for the weight blob", dev[i], nb / 1e9);
-                rc = Q2A_ERR_OOM;
-            }
-        }
+        rc = alloc_bufs(b, dev, nb, -1);
         if (rc == Q2A_OK && (hipSetDevice(dev[0]) != hipSuccess ||
                              hipMemcpy(b.buf[0], host, (size_t) nb, hipMemcpyHostToDevice) != hipSuccess)) {
             gerr("weight upload to device %d failed", dev[0]);
@@ -135,29 +193,8 @@ q2a_group * q2a_group_open(const char * model_path, const int * devices, int n_d
         }
         q2a_free_host_blob(host);
         host = nullptr;
-        if (rc == Q2A_OK) {
-            // one communicator clique over the listed devices, rank i = dev[i]; rank 0 holds the blob
-            b.comm.assign(n, nullptr);
-            ncclResult_t r = ncclCommInitAll(b.comm.data(), n, dev.data());
-            if (r != ncclSuccess) { gerr("ncclCommInitAll over %d devices: %s", n, ncclGetErrorString(r)); rc = Q2A_ERR_HIP; }
-        }
-        if (rc == Q2A_OK) {
-            ncclResult_t r = ncclGroupStart();
-            for (int i = 0; i < n && r == ncclSuccess; ++i) {
-                (void) hipSetDevice(dev[i]);
-                r = ncclBroadcast(b.buf[0], b.buf[i], (size_t) nb, ncclUint8, 0, b.comm[i], b.st[i]);
-            }
-            const ncclResult_t r2 = ncclGroupEnd();
-            if (r != ncclSuccess || r2 != ncclSuccess) {
-                gerr("ncclBroadcast of the weight blob: %s", ncclGetErrorString(r != ncclSuccess ? r : r2));
-                rc = Q2A_ERR_HIP;
-            }
-            for (int i = 0; i < n && rc == Q2A_OK; ++i)
-                if (hipSetDevice(dev[i]) != hipSuccess || hipStreamSynchronize(b.st[i]) != hipSuccess) {
-                    gerr("device %d: broadcast did not complete", dev[i]);
-                    rc = Q2A_ERR_HIP;
-                }
-        }
+        // one communicator clique over the listed devices, rank i = dev[i]; rank 0 holds the blob
+        if (rc == Q2A_OK) rc = broadcast(b, dev, 0, nb);
         g->t_bcast = now_s() - t0;
         t0 = now_s();
         // every device expands its copy into an engine-owned device layout (k_expand_rows), then the transport copy
@@ -167,6 +204,53 @@ q2a_group * q2a_group_open(const char * model_path, const int * devices, int n_d
             if (!e) { rc = Q2A_ERR_HIP; break; }
             g->eng.push_back(e);
         }
+        g->t_open = now_s() - t0;
+    }
+    if (rc != Q2A_OK) {
+        const std::string msg = q2a_last_error();
+        q2a_group_close(g);
+        q2a_internal_set_error(msg.c_str());
+        return nullptr;
+    }
+    return g;
+}
+
+q2a_group * q2a_group_open_with(q2a_engine * base, const int * devices, int n_devices) {
+    const void * src = nullptr;
+    int64_t nb = 0;
+    int bdev = -1;
+    if (!base || n_devices < 0 || (n_devices > 0 && !devices)) { gerr("invalid arguments"); return nullptr; }
+    if (q2a_internal_engine_blob(base, &src, &nb, &bdev) != Q2A_OK) return nullptr;
+    std::vector<int> dev;
+    if (!group_devices(devices, n_devices, bdev, dev)) return nullptr;
+    int root = -1;
+    for (int i = 0; i < (int) dev.size(); ++i)
+        if (dev[i] == bdev) root = i;
+    if (root < 0) { gerr("the base engine's device %d is not in the device list", bdev); return nullptr; }
+    const int n = (int) dev.size();
+    q2a_group * g = new q2a_group();
+    g->dev = dev;
+    g->blob_bytes = nb;
+    double t0 = now_s();
+    int rc = Q2A_OK;
+    {
+        bcast_bufs b;
+        rc = alloc_bufs(b, dev, nb, root);
+        if (rc == Q2A_OK) {
+            b.buf[root] = const_cast<void *>(src);   // the base engine's own replica is the broadcast's source (read only)
+            if (n > 1) rc = broadcast(b, dev, root, nb);
+        }
+        g->t_bcast = now_s() - t0;
+        t0 = now_s();
+        // the base device's engine shares base's weights (its own workspace and stream); every other device's engine
+        // runs on the replica it received, which the group keeps until close
+        for (int i = 0; i < n && rc == Q2A_OK; ++i) {
+            q2a_engine * e = i == root ? q2a_open_shared(base) : q2a_open_device_blob(b.buf[i], nb, dev[i]);
+            if (!e) { rc = Q2A_ERR_HIP; break; }
+            g->eng.push_back(e);
+            if (i != root) { g->held.emplace_back(dev[i], b.buf[i]); b.buf[i] = nullptr; }
+        }
+        b.buf[root] = nullptr;   // (never freed here: it belongs to base)
         g->t_open = now_s() - t0;
     }
     if (rc != Q2A_OK) {
@@ -227,6 +311,10 @@ int q2a_group_encode_host(q2a_group * g, const float * const * pcm, const int32_
 void q2a_group_close(q2a_group * g) {
     if (!g) return;
     for (q2a_engine * e : g->eng) q2a_close(e);
+    for (auto & h : g->held) {
+        (void) hipSetDevice(h.first);
+        (void) hipFree(h.second);
+    }
     delete g;
 }
 

@@ -9,6 +9,10 @@ typedef _Float16 q2a_half;
 
 // sets the calling thread's q2a_last_error() text (defined with the engine; used by q2a_group.cpp)
 extern "C" void q2a_internal_set_error(const char * msg);
+// an engine's device-layout weight blob (device pointer, bytes) and device ordinal (used by q2a_group.cpp to broadcast
+// an open engine's weights instead of packing the model file again)
+struct q2a_engine;
+extern "C" int q2a_internal_engine_blob(const q2a_engine * e, const void ** blob, int64_t * bytes, int * device);
 
 // Epilogue kinds of the fused weight GEMM (one template instantiation each)
 enum q2a_epi {

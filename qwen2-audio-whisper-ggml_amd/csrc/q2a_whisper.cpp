@@ -32,10 +32,9 @@ struct whisper_state {
 };
 
 struct whisper_context {
-    q2a_engine * eng = nullptr;   // owns the device weights
-    std::string path;             // model file and activation contract, for the multi-device group
-    int act = Q2A_ACT_REFERENCE;
-    q2a_group * group = nullptr;  // whisper_full_parallel on > 1 visible device (opened on first use)
+    q2a_engine * eng = nullptr;   // owns the device weights (on params.gpu_device)
+    q2a_group * group = nullptr;  // whisper_full_parallel on > 1 device (opened on first use, over eng's weights)
+    bool group_failed = false;    // a group could not be opened: the single-device path from then on
     q2a_info info{};
     int n_vocab = 0, ftype = 0;
     whisper_state * state = nullptr;
@@ -187,8 +186,6 @@ struct whisper_context * whisper_init_from_file_with_params_no_state(const char 
     if (!e) { wlog(GGML_LOG_LEVEL_ERROR, "whisper_init: %s\n", q2a_last_error()); return nullptr; }
     whisper_context * ctx = new whisper_context();
     ctx->eng = e;
-    ctx->path = path_model;
-    ctx->act = act;
     q2a_get_info(e, &ctx->info);
     ctx->n_vocab = hp[0];
     ctx->ftype = hp[10];
@@ -309,15 +306,28 @@ int whisper_full_parallel(struct whisper_context * ctx, struct whisper_full_para
     const size_t per_out = (size_t) ctx->info.n_out * ctx->info.n_audio_state;
     st->chunks.assign(per_out * n_processors, 0.0f);
     st->chunk_status.assign(n_processors, Q2A_CLIP_SKIPPED);
-    // more than one visible device: the chunks are spread over every device (q2a_group: one RCCL broadcast of the
-    // weights at first use, contiguous chunk ranges, a host thread per device); one device: one batch on the state
-    if (!ctx->group && q2a_device_count() > 1) {
-        ctx->group = q2a_group_open(ctx->path.c_str(), nullptr, 0, ctx->act);
-        if (!ctx->group) {
-            wlog(GGML_LOG_LEVEL_ERROR, "whisper_full_parallel: multi-device open failed: %s\n", q2a_last_error());
-            return -1;
+    // more than one device: the chunks are spread over the context's device (params.gpu_device, first) and the other
+    // visible devices, up to Q2A_PARALLEL_DEVICES of them (q2a_group_open_with: ONE RCCL broadcast of the context's own
+    // device-layout weights at first use, no second replica on the context's device, contiguous chunk ranges, a host
+    // thread per device). One device, Q2A_PARALLEL_DEVICES=1, or a group that cannot be opened: one batch on the state.
+    if (!ctx->group && !ctx->group_failed) {
+        const char * lim = getenv("Q2A_PARALLEL_DEVICES");
+        int ndev = q2a_device_count();
+        if (lim && atoi(lim) > 0 && atoi(lim) < ndev) ndev = atoi(lim);
+        if (ndev > 1) {
+            std::vector<int> devs;
+            devs.push_back(ctx->info.device);
+            for (int d = 0; (int) devs.size() < ndev; ++d)
+                if (d != ctx->info.device) devs.push_back(d);
+            ctx->group = q2a_group_open_with(ctx->eng, devs.data(), (int) devs.size());
+            if (ctx->group) {
+                wlog(GGML_LOG_LEVEL_INFO, "whisper_full_parallel: %d devices\n", q2a_group_size(ctx->group));
+            } else {
+                wlog(GGML_LOG_LEVEL_WARN, "whisper_full_parallel: multi-device open failed (%s): running on device %d only\n",
+                     q2a_last_error(), ctx->info.device);
+                ctx->group_failed = true;
+            }
         }
-        wlog(GGML_LOG_LEVEL_INFO, "whisper_full_parallel: %d devices\n", q2a_group_size(ctx->group));
     }
     const int64_t t0 = now_us();
     const int erc = ctx->group ? q2a_group_encode_host(ctx->group, ptr.data(), ns.data(), nullptr, n_processors, 0,
@@ -360,6 +370,8 @@ const float * whisper_get_embd_enc(struct whisper_context * ctx, int * n_out, in
     if (n_state) *n_state = ctx->info.n_audio_state;
     return ctx->state->embd.data();
 }
+
+q2a_engine * q2a_whisper_context_engine(struct whisper_context * ctx) { return ctx ? ctx->eng : nullptr; }
 
 int q2a_whisper_encode_long(struct whisper_context * ctx, const float * samples, int n_samples, int offset_ms, float * out,
                             int max_windows) {

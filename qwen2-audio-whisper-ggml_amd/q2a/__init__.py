@@ -23,7 +23,7 @@ EXPORTS = (
     "q2a_projector_open", "q2a_projector_close", "q2a_projector_get_dims", "q2a_projector_apply",
     "q2a_pack_model_compact", "q2a_blob_device_size", "q2a_expand_blob",
     "q2a_device_count", "q2a_group_open", "q2a_group_close", "q2a_group_size", "q2a_group_engine", "q2a_group_split",
-    "q2a_group_encode_host", "q2a_group_setup_times",
+    "q2a_group_encode_host", "q2a_group_setup_times", "q2a_group_open_with", "q2a_whisper_context_engine",
 )
 
 # per-clip status of the encode calls (include/q2a_encoder.h): FAILED = the host call returned an error before this
@@ -96,6 +96,8 @@ def lib() -> C.CDLL:
         if hasattr(L, "q2a_group_open"):   # round 5 (optional: earlier diagnostic builds load too)
             L.q2a_group_open.restype = vp
             L.q2a_group_open.argtypes = [C.c_char_p, i32p, C.c_int, C.c_int]
+            L.q2a_group_open_with.restype = vp
+            L.q2a_group_open_with.argtypes = [vp, i32p, C.c_int]
             L.q2a_group_close.argtypes = [vp]
             L.q2a_group_size.argtypes = [vp]
             L.q2a_group_engine.restype = vp
@@ -241,14 +243,20 @@ def group_split(n_clips: int, n_devices: int) -> list[range]:
 
 
 class Group:
-    """Several GPUs in ONE process (q2a_group_*): one RCCL broadcast of the compact weight blob at open, then clip
-    batches split into contiguous ranges, a host thread per device. devices=None: every visible device."""
+    """Several GPUs in ONE process (q2a_group_*): one RCCL broadcast of the weights at open, then clip batches split
+    into contiguous ranges, a host thread per device. devices=None: every visible device.
+    From a model file (q2a_group_open: the compact blob packed once on the host), or with engine= an open Engine
+    (q2a_group_open_with: its own device-layout weights are the broadcast's root, its device's group engine shares
+    them; the Engine must outlive the group)."""
 
-    def __init__(self, model_path: str, devices=None, act: int = ACT_REFERENCE):
+    def __init__(self, model_path: str | None = None, devices=None, act: int = ACT_REFERENCE, engine=None):
         L = lib()
         devs = np.ascontiguousarray(devices if devices is not None else [], dtype=np.int32)
-        self.h = L.q2a_group_open(model_path.encode(), devs.ctypes.data_as(C.POINTER(C.c_int32)) if len(devs) else None,
-                                  len(devs), act)
+        dptr = devs.ctypes.data_as(C.POINTER(C.c_int32)) if len(devs) else None
+        if engine is not None:
+            self.h = L.q2a_group_open_with(C.c_void_p(engine.h), dptr, len(devs))
+        else:
+            self.h = L.q2a_group_open(model_path.encode(), dptr, len(devs), act)
         if not self.h:
             raise Q2AError(L.q2a_last_error().decode())
         self.size = L.q2a_group_size(self.h)
@@ -271,6 +279,8 @@ class Group:
         st = np.full(n, -1, dtype=np.int32)
         i32p = C.POINTER(C.c_int32)
         offs = None if offsets_ms is None else np.ascontiguousarray(offsets_ms, dtype=np.int32)
+        if offs is not None and len(offs) != n:
+            raise ValueError(f"offsets_ms has {len(offs)} entries for {n} clips")
         _check(lib().q2a_group_encode_host(self.h, ptrs, ns.ctypes.data_as(i32p),
                                            offs.ctypes.data_as(i32p) if offs is not None else None, n, offset_ms,
                                            C.c_void_p(out.ctypes.data), st.ctypes.data_as(i32p)))

@@ -20,7 +20,7 @@ struct cli {
     std::string model = "models/ggml-base.en.bin";
     std::vector<std::string> files;
     int threads = 4, offset_ms = 0, duration_ms = 0, reps = 1, device = 0, processors = 1, gpus = 0;
-    bool no_prints = false, batch = false, long_audio = false, bf16 = false;
+    bool no_prints = false, batch = false, long_audio = false, bf16 = false, device_set = false;
     std::string dump;
 };
 
@@ -37,8 +37,9 @@ void usage(const char * argv0) {
             "  -la,       --long-audio     encode every 30 s window of each file in one batch\n"
             "  -oemb F,   --output-emb F   write embd_enc (f32, [windows/files][750][1280]) to F\n"
             "  -dev N,    --device N       HIP device\n"
-            "  -ng N,     --gpus N         -b: spread the batch over the first N devices (default: every visible\n"
-            "                              device; one RCCL broadcast of the weights, a host thread per device)\n"
+            "  -ng N,     --gpus N         -b: spread the batch over N devices, the -dev device first (default: every\n"
+            "                              visible device unless -dev is given; one RCCL broadcast of the loaded\n"
+            "                              weights, a host thread per device)\n"
             "  -bf16,     --bf16-act       bf16-activation contract (Q2A_ACT_BF16, BASELINE configs[4]); not the\n"
             "                              reference's numerics: see DESIGN.md\n"
             "  -np,       --no-prints      only print results\n",
@@ -57,7 +58,7 @@ bool parse(int argc, char ** argv, cli & c) {
         else if (a == "-ot" || a == "--offset-t") { if (!(v = next())) return false; c.offset_ms = atoi(v); }
         else if (a == "-d" || a == "--duration") { if (!(v = next())) return false; c.duration_ms = atoi(v); }
         else if (a == "-r" || a == "--reps") { if (!(v = next())) return false; c.reps = atoi(v); }
-        else if (a == "-dev" || a == "--device") { if (!(v = next())) return false; c.device = atoi(v); }
+        else if (a == "-dev" || a == "--device") { if (!(v = next())) return false; c.device = atoi(v); c.device_set = true; }
         else if (a == "-p" || a == "--processors") { if (!(v = next())) return false; c.processors = atoi(v); }
         else if (a == "-ng" || a == "--gpus") { if (!(v = next())) return false; c.gpus = atoi(v); }
         else if (a == "-oemb" || a == "--output-emb") { if (!(v = next())) return false; c.dump = v; }
@@ -115,20 +116,18 @@ int main(int argc, char ** argv) {
         std::vector<const float *> ptr;
         std::vector<int32_t> ns;
         for (const auto & p : pcms) { ptr.push_back(p.data()); ns.push_back((int32_t) p.size()); }
-        // more than one device: a q2a_group (contiguous clip ranges, one host thread per device); else one engine
-        const int act = c.bf16 ? Q2A_ACT_BF16 : Q2A_ACT_REFERENCE;
-        const int ndev = c.gpus > 0 ? c.gpus : q2a_device_count();
+        // more than one device: a q2a_group over the context's loaded weights (contiguous clip ranges, one host thread
+        // per device; -ng N, or every visible device when -dev was not given); else the context's own engine
+        q2a_engine * e = q2a_whisper_context_engine(ctx);
+        const int ndev = c.gpus > 0 ? c.gpus : c.device_set ? 1 : q2a_device_count();
         q2a_group * grp = nullptr;
-        q2a_engine * e = nullptr;
         if (c.gpus > 0 || ndev > 1) {   // (an explicit -ng always takes the group path, -ng 1 included)
-            std::vector<int> devs(ndev);
-            for (int i = 0; i < ndev; ++i) devs[i] = i;
-            grp = q2a_group_open(c.model.c_str(), devs.data(), ndev, act);
-            if (!grp) { fprintf(stderr, "error: %s\n", q2a_last_error()); return 3; }
+            std::vector<int> devs{c.device};
+            for (int d = 0; (int) devs.size() < ndev; ++d)
+                if (d != c.device) devs.push_back(d);
+            grp = q2a_group_open_with(e, devs.data(), ndev);
+            if (!grp) { fprintf(stderr, "error: %s\n", q2a_last_error()); whisper_free(ctx); return 3; }
             if (!c.no_prints) fprintf(stderr, "%s: batch of %zu clips over %d devices\n", __func__, ptr.size(), ndev);
-        } else {
-            e = q2a_open_ex(c.model.c_str(), c.device, act);
-            if (!e) { fprintf(stderr, "error: %s\n", q2a_last_error()); return 3; }
         }
         std::vector<float> out((size_t) ptr.size() * n_out * n_state);
         std::vector<int32_t> st(ptr.size());
@@ -145,7 +144,6 @@ int main(int argc, char ** argv) {
         }
         if (dump) fwrite(out.data(), 4, out.size(), dump);
         q2a_group_close(grp);
-        q2a_close(e);
     } else {
         whisper_full_params wp = whisper_full_default_params(WHISPER_SAMPLING_GREEDY);
         wp.n_threads = c.threads;

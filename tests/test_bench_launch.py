@@ -101,3 +101,22 @@ def test_bench_constants_and_profile_selection():
             assert kernels["gemm_fc1"]["hbm_bytes_per_launch_corrected"] > 1.24e9   # >= the algorithmic bytes
         else:
             assert any(e.get("class") == "gemm_fc1" and 0 < e["mfma_busy_frac"] < 1 for e in kernels.values())
+
+
+def test_roofline_objects_name_the_dominant_kernel():
+    """CPU-only: the line's `roofline` is built for whichever matrix-core class dominates the step (attention at the
+    default workload), with its algorithmic flops per launch, issued-term figures for the F32-class attention, and
+    its PMC traffic / SQ busy from the committed summaries of that workload; fc1 keeps its own object."""
+    sys.path.insert(0, ROOT)
+    import bench
+    ms, n = [0.0] * 11, [0] * 11
+    ms[5], n[5] = 32 * 1.75 * 3, 32 * 3          # 1.75 ms per attention launch
+    ms[8], n[8] = 32 * 1.30 * 3, 32 * 3
+    r = bench.roofline_of(5, ms, n, "q4k64", "q4_k", False, 64)
+    flop = 4.0 * 1500 * 1500 * 1280 * 64
+    assert r["flop_per_launch"] == flop and abs(r["achieved"] - flop / 1.75e-3 / 1e12) < 0.1
+    assert abs(r["issued_tflops"] - 3 * r["achieved"]) < 0.5 and "k_attn_t" in r["kernel"]
+    assert r["traffic"] and r["traffic"] > 1e9 and r["mfma_busy_frac"] and 0 < r["mfma_busy_frac"] < 1
+    f = bench.roofline_of(8, ms, n, "q4k64", "q4_k", False, 64)
+    assert f["flop_per_launch"] == 2.0 * 96000 * 5120 * 1280 and "PRE_H,256,2" in f["kernel"]
+    assert bench.roofline_of(5, ms, n, "q4k64", "q4_k", False, 2)["traffic"] is None   # other batch: no counters

@@ -75,3 +75,43 @@ def test_q2a_main_batch_over_group(make_model, make_clip, tmp_path):
                        capture_output=True)
         dumps.append(np.fromfile(d, dtype=np.uint32))
     assert dumps[0].size == 3 * 750 * 256 and np.array_equal(dumps[0], dumps[1])
+
+
+@pytest.mark.parametrize("wt", ["f16", "q4_k"])
+def test_group_open_with_engine_keeps_one_replica_per_device(make_model, make_clip, wt):
+    """q2a_group_open_with (what whisper_full_parallel and q2a_main -b run on): the open engine's own device-layout
+    weights are the broadcast's root and its device's group engine shares them, so the device holding the engine
+    grows by the group engine's workspace only — not by a second weight replica (the file-based group held
+    two) — and the group's outputs equal the engine's bit for bit."""
+    path = make_model("full", wt)
+    clips = [make_clip(c, 480000) for c in range(3)]
+    e = q2a.Engine(path, device=0)
+    ref, st_ref = e.encode_host(clips)          # the engine's own workspace exists before the measurement
+    torch.cuda.synchronize()
+    free0, _ = torch.cuda.mem_get_info(0)
+    g = q2a.Group(engine=e, devices=[0])
+    assert g.size == 1
+    t = g.setup_times()
+    assert t["blob_bytes"] == e.info.weight_bytes and t["pack_s"] == 0.0
+    out, st = g.encode_host(clips)
+    torch.cuda.synchronize()
+    free1, _ = torch.cuda.mem_get_info(0)
+    grew = free0 - free1
+    g.close()
+    e.close()
+    assert list(st) == list(st_ref)
+    assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
+    # the group engine's workspace for 3 clips is ~0.2-0.4 GB; a replica alone would be 1.40 GB (Q4_K) / 1.26 GB (F16)
+    assert grew < e.info.weight_bytes * 0.6, (grew, e.info.weight_bytes)
+
+
+def test_group_open_with_rejects_a_device_list_without_the_engine(make_model):
+    path = make_model("tiny", "f16")
+    e = q2a.Engine(path, device=0)
+    n = torch.cuda.device_count()
+    if n > 1:
+        with pytest.raises(q2a.Q2AError, match="not in the device list"):
+            q2a.Group(engine=e, devices=[1])
+    with pytest.raises(q2a.Q2AError, match="listed twice"):
+        q2a.Group(engine=e, devices=[0, 0])
+    e.close()

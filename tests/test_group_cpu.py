@@ -35,3 +35,9 @@ def test_group_open_without_device_fails_cleanly(make_model):
         q2a.Group(path)
     with pytest.raises(q2a.Q2AError):
         q2a.Group(path, devices=[0, 0])
+
+
+def test_group_open_with_needs_an_engine():
+    L = q2a.lib()
+    assert not L.q2a_group_open_with(None, None, 0)
+    assert "invalid arguments" in L.q2a_last_error().decode()
