@@ -5,9 +5,22 @@
 //                    3 k_attn_p32 (QK^T of tile t+1 interleaved with softmax t)   4 k_attn_pp32 (8-wave ping-pong)
 //                    5 k_attn_pp<false> (F32-class ping-pong, 64-key tiles)   6 / 7 k_attn with 2 / 1 QK^T terms
 //                    8 k_attn_g (64-key tiles, 32x32x16; its PHL / VHL / VDB / QK_TERMS switches)   9 k_attn_s
-// (the product's own P.V precision switches Q2A_ATTN_PHL / Q2A_ATTN_VHL apply to variant 0).
+// (round 6: the product kernel's own precision / schedule switches moved to diag/experiment_knobs_r05.patch; the
+// switches of k_attn_g below keep their product values unless a build sets them).
 #define Q2A_ATTN_LAUNCH q2a_launch_attention_product
 #include "../qwen2-audio-whisper-ggml_amd/csrc/q2a_attn.hip"
+#ifndef Q2A_ATTN_PHL
+#define Q2A_ATTN_PHL 1
+#endif
+#ifndef Q2A_ATTN_VHL
+#define Q2A_ATTN_VHL 1
+#endif
+#ifndef Q2A_ATTN_QK_TERMS
+#define Q2A_ATTN_QK_TERMS 3
+#endif
+#ifndef Q2A_ATTN_S_SCHED
+#define Q2A_ATTN_S_SCHED 1
+#endif
 
 #ifndef Q2A_ATTN_VARIANT
 #define Q2A_ATTN_VARIANT 0

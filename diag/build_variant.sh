@@ -1,5 +1,7 @@
 #!/bin/bash
-# build a diagnostic variant of libq2a.so into diag/<name>/libq2a.so with extra -D flags (A/B timing only)
+# build a diagnostic variant of libq2a.so into diag/<name>/libq2a.so with extra -D flags (A/B timing only; the
+# experiment knobs of rounds 1-5 need diag/experiment_knobs_r05.patch applied first, the Q2A_DIAG_NO_STORE / STAMPS
+# timing builds work on the product source)
 set -e
 NAME=$1; shift
 R=/root/repo/qwen2-audio-whisper-ggml_amd

@@ -80,25 +80,16 @@ __device__ __forceinline__ float max_lane32(float x) {
     return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 // P.V precision of the diagnostic k_attn_g (diag/attn_variants.hip; reference: F32 P and V, qwen2-whisper.cpp:2088-2102):
-//   Q2A_ATTN_PHL = 1: P = Ph + Pl, two fp16 halves (Ph = P truncated to fp16, Pl = the exact f32 remainder truncated
+//   PHL = 1: P = Ph + Pl, two fp16 halves (Ph = P truncated to fp16, Pl = the exact f32 remainder truncated
 //                     to fp16: 22 significant bits), two P.V MFMAs per fragment
-//   Q2A_ATTN_VHL = 1: V^T = Vh + Vl likewise (the QKV epilogue writes the lo image), one more MFMA per fragment
+//   VHL = 1: V^T = Vh + Vl likewise (the QKV epilogue writes the lo image), one more MFMA per fragment
 //                     (Vl.Ph; the Vl.Pl term is below 2^-22 relative) and a fourth LDS image per stage (two
 //                     workgroups per CU instead of three)
 // With PHL = 0 P is ONE fp16 value (truncated) and the softmax denominator is the sum of exactly those fp16 values
 // (v_dot2 of the packed pairs against 1.0): the output is an exact weighted mean of V with the fp16 weights, so P's
 // rounding does not bias the normalisation. With PHL = 1 the denominator is the f32 sum of P.
-#ifndef Q2A_ATTN_PHL
-#define Q2A_ATTN_PHL 1
-#endif
-#ifndef Q2A_ATTN_VHL
-#define Q2A_ATTN_VHL 1
-#endif
 // QK^T terms of k_attn_g (diagnostic builds only): 3 = Kh.Qh + Kl.Qh + Kh.Ql (the contract); 21 = without Kl.Qh (K as
 // fp16); 22 = without Kh.Ql (Q as fp16)
-#ifndef Q2A_ATTN_QK_TERMS
-#define Q2A_ATTN_QK_TERMS 3
-#endif
 // lazy re-basing threshold of the softmax reference point: a lane re-bases when the P of its tile (8 or 16 per lane) sum to
 // more than this (so each P <= 2^15 < 65504, inside fp16, between moves)
 constexpr float PLIM = 32768.0f;
@@ -121,9 +112,6 @@ __device__ __forceinline__ float sub_half(float p, half2_t h) {
 // re-base path, K(t)) from another, and DMAs tile t+2 into the third; one barrier per tile. The re-base path (a lane's
 // P of the tile sum past PLIM) recomputes tile t's scores from K(t), re-bases, and moves the already computed
 // S(t+1) - m' by the same shift.
-#ifndef Q2A_ATTN_S_SCHED
-#define Q2A_ATTN_S_SCHED 1   // sched_group_barrier interleaving (0: the compiler's own order; diagnostic builds)
-#endif
 constexpr int KS = 32;   // keys per tile
 // fp16 remainder pair p - h (h = the truncated fp16 pair of p0, p1) in two v_fma_mix{lo,hi}_f16: the exact f32
 // difference rounded once to fp16 (RNE), written straight into the packed register
@@ -266,56 +254,20 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
             for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-#ifdef Q2A_ATTN_DIAG_NOEXP   // timing diagnostic only (wrong results): the exponentials skipped
-                    e[qb][4 * kb + r] = fmaxf(fmaf(sv[qb][kb][r], 0.001f, 1.0f), 0.f);
-#else
                     e[qb][4 * kb + r] = __builtin_amdgcn_exp2f(sv[qb][kb][r]);
-#endif
                 }
     };
     // region A: S'^T - m' of the tile at stage st into s (initialised by the caller with the splat); with e: the
     // previous tile's P split and sums in the MFMA issue gaps
     auto qk = [&](const char * st, sc_t & s, const ex_t * e, float (&ls)[2]) {
         launder_ofs();
-#ifdef Q2A_ATTN_DIAG_F8TIME   // timing diagnostic only (wrong results): the four correction MFMAs of a (qb, kb) pair
-        // as ONE block-scaled fp8 16x16x128 MFMA on the K lo / Q lo registers (the cycles an fp8 correction form costs)
-        {
-            half8 kh2[2][2], kl2[2][2];
-#pragma unroll
-            for (int ds = 0; ds < 2; ++ds)
-#pragma unroll
-                for (int kb = 0; kb < 2; ++kb) {
-                    kh2[kb][ds] = *(const half8 *) (st + kofs[kb][ds]);
-                    kl2[kb][ds] = *(const half8 *) (st + KIMG + kofs[kb][ds]);
-                }
-            typedef int v8i_t __attribute__((ext_vector_type(8)));
-#pragma unroll
-            for (int qb = 0; qb < 2; ++qb)
-#pragma unroll
-                for (int kb = 0; kb < 2; ++kb) {
-                    s[qb][kb] = mma16(kh2[kb][0], qh[qb][0], s[qb][kb]);
-                    s[qb][kb] = mma16(kh2[kb][1], qh[qb][1], s[qb][kb]);
-                    v8i_t a8, b8;
-                    __builtin_memcpy(&a8, &kl2[kb][0], 32);
-                    __builtin_memcpy(&b8, &ql[qb][0], 32);
-                    a8 &= 0x27272727;   // finite, small e4m3 values (the bench checks its output is finite)
-                    b8 &= 0x27272727;
-                    s[qb][kb] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a8, b8, s[qb][kb], 0, 0, 0, 127, 0, 127);
-                }
-        }
-        if (false)
-#endif
 #pragma unroll
         for (int ds = 0; ds < 2; ++ds) {
             half8 kh[2], kl[2];
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb) {
                 kh[kb] = *(const half8 *) (st + kofs[kb][ds]);
-#ifdef Q2A_ATTN_DIAG_NOKL   // timing diagnostic only (wrong results): the K lo fragment reads skipped
-                kl[kb] = kh[kb];
-#else
                 kl[kb] = *(const half8 *) (st + KIMG + kofs[kb][ds]);
-#endif
             }
 #pragma unroll
             for (int qb = 0; qb < 2; ++qb)
@@ -328,7 +280,6 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
         }
         if (e) {
             split(*e, ls);
-#if Q2A_ATTN_S_SCHED
             __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
             for (int i = 0; i < 12; ++i) {
@@ -341,7 +292,6 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
             }
-#endif
         }
     };
     auto mask = [&](sc_t & sv, int t) {   // keys >= T (last tile only): key of (kb, r) in lane group g is 8g + 4kb + r
@@ -383,11 +333,7 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
 #pragma unroll
         for (int db = 0; db < 4; ++db) {
             va[db] = *(const half8 *) (st + vofs + db * 16 * VROW);
-#ifdef Q2A_ATTN_DIAG_NOVL   // timing diagnostic only (wrong results): the V^T lo fragment reads skipped
-            vl[db] = va[db];
-#else
             vl[db] = *(const half8 *) (st + VIMG + vofs + db * 16 * VROW);
-#endif
         }
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb)
@@ -404,7 +350,6 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
         asm volatile("" : "+v"(e[0][0]), "+v"(e[0][1]), "+v"(e[0][2]), "+v"(e[0][3]), "+v"(e[0][4]), "+v"(e[0][5]),
                           "+v"(e[0][6]), "+v"(e[0][7]), "+v"(e[1][0]), "+v"(e[1][1]), "+v"(e[1][2]), "+v"(e[1][3]),
                           "+v"(e[1][4]), "+v"(e[1][5]), "+v"(e[1][6]), "+v"(e[1][7]));
-#if Q2A_ATTN_S_SCHED
         __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {   // one exponential per MFMA gap (8 of the 16 cycles issue VALU)
@@ -417,7 +362,6 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
             __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
         }
         __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
-#endif
     };
 
     sc_t sn, init;
@@ -743,7 +687,7 @@ __global__ __launch_bounds__(512, 2) void k_attn_pp(const q2a_attn_args p) {
 }  // namespace
 
 // the QKV epilogue must write the V^T lo image (q2a_attn_args.vtl) for this build's reference-contract kernel
-bool q2a_attention_wants_vlo() { return Q2A_ATTN_VHL != 0; }
+bool q2a_attention_wants_vlo() { return true; }
 
 #ifndef Q2A_ATTN_LAUNCH
 #define Q2A_ATTN_LAUNCH q2a_launch_attention

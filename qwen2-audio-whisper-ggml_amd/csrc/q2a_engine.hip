@@ -47,9 +47,6 @@ void set_err(const char * fmt, ...) {
 // ------------------------------------------------------------------------------------------------
 constexpr uint32_t BLOB_MAGIC = 0x42413251u;   // "Q2AB"
 // version 3: the Q4_K gamma array holds -(dmin/dx) (stored negated); a version-2 blob (positive gamma) is refused
-#ifndef Q2A_FC1_PATH
-#define Q2A_FC1_PATH 0   // the engine's default fc1 -> fc2 operand path (below; diagnostic builds select another)
-#endif
 constexpr uint32_t BLOB_VERSION = 5;   // 4: conv1 taps against the three-part mel operand; 5: compact transport form
 constexpr int MAX_LAYERS = 64;
 constexpr size_t HEADER_BYTES = 32768;
@@ -727,8 +724,6 @@ hipError_t launch_split3(const float * x, q2a_half * y, int K, int64_t n, hipStr
 struct q2a_engine {
     int device = 0;
     hipStream_t stream = nullptr;
-    hipStream_t pf_stream = nullptr;   // small-batch weight prefetch (prefetch_layer), created on first use
-    hipEvent_t pf_ev = nullptr;
     blob_header h;
     dims d;
     int wtype = 0, blk = 0;
@@ -781,7 +776,7 @@ struct q2a_engine {
     //   0 (default) fc1 writes its fp16 pre-activation, the Q8_K quantizer applies the GELU table on the way
     //   1 GELU in the fc1 epilogue, then the fp16-input quantizer
     //   2 GELU + Q8_K quantization fused into the fc1 epilogue (8-phase tiles only)
-    int fc1_path = Q2A_FC1_PATH;
+    int fc1_path = 0;
     // q2a_test_block_taps: device buffers receiving the GEMM A operands of one block (LN1 -> QKV, attention -> O,
     // LN2 -> fc1, GELU -> fc2) as they were fed to the MFMA, for the per-layer divergence trace (NULL: off)
     void * taps[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -1213,40 +1208,6 @@ int prepare_meta(q2a_engine * e, const int32_t * n_samples, int B, int offset_ms
     return Q2A_OK;
 }
 
-// Small batches: every weight GEMM of a layer is latency-bound (a 64-row tile's 20 K-steps each wait on weight rows
-// that the first touch brings from HBM). A side stream reads the NEXT layer's blob range (its weights and scale
-// arrays, 39 MB for F16) while this layer computes, so its GEMMs find them in the Infinity Cache (256 MiB). Batches of
-// up to Q2A_PREFETCH_MAX_B clips (0 = off); no arithmetic changes (batch invariance untouched). Measured round 5
-// (diag/gpurun_r05d.sh, B <= 4): one clip 0.5 ms SLOWER — the touch competes with QKV and fc1 / fc2 / O did not get
-// faster (they are glds-issue-bound, not HBM-latency-bound): off.
-#ifndef Q2A_PREFETCH_MAX_B
-#define Q2A_PREFETCH_MAX_B 0
-#endif
-__global__ __launch_bounds__(256) void k_touch(const uint4 * __restrict__ p, int64_t n16, uint32_t * sink) {
-    uint32_t x = 0;
-    for (int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t) gridDim.x * blockDim.x) {
-        const uint4 v = p[i];
-        x ^= v.x ^ v.y ^ v.z ^ v.w;
-    }
-    if (x == 0x9E3779B9u && sink) *sink = x;   // (data-dependent, practically never: keeps the loads alive)
-}
-
-int prefetch_layer(q2a_engine * e, int l, hipStream_t s) {
-    if (!e->pf_stream) {
-        HIP_TRY(hipStreamCreateWithFlags(&e->pf_stream, hipStreamNonBlocking));
-        HIP_TRY(hipEventCreateWithFlags(&e->pf_ev, hipEventDisableTiming));
-    }
-    HIP_TRY(hipEventRecord(e->pf_ev, s));                 // after this layer's earlier work was queued
-    HIP_TRY(hipStreamWaitEvent(e->pf_stream, e->pf_ev, 0));
-    if (l < e->d.L) {
-        const uint64_t a = e->h.loff[l][L_BQKV], b = l + 1 < e->d.L ? e->h.loff[l + 1][L_BQKV] : e->h.total;
-        hipLaunchKernelGGL(k_touch, dim3(64), dim3(256), 0, e->pf_stream, (const uint4 *) (e->blob + a), (int64_t) ((b - a) / 16),
-                           (uint32_t *) nullptr);
-        HIP_TRY(hipGetLastError());
-    }
-    return Q2A_OK;
-}
-
 int encode_impl(q2a_engine * e, const float * pcm, int64_t stride, const int32_t * n_samples, int B, int offset_ms,
                 const int32_t * offs, float * out, int32_t * status, hipStream_t s) {
     if (B <= 0 || !pcm || !n_samples || !out) { set_err("invalid arguments"); return Q2A_ERR_ARG; }
@@ -1257,18 +1218,11 @@ int encode_impl(q2a_engine * e, const float * pcm, int64_t stride, const int32_t
     int max_frames = 0;
     rc = prepare_meta(e, n_samples, B, offset_ms, offs, status, max_frames, stride > 0 ? stride : -1, s);   // stride 0: shared PCM
     if (rc) return rc;
-    const bool pf = B <= Q2A_PREFETCH_MAX_B;
-    if (pf && (rc = prefetch_layer(e, 0, s))) return rc;   // layer 0's weights under the front end
     rc = run_frontend(e, pcm, stride, B, max_frames, s);
     if (rc) return rc;
     for (int l = 0; l < e->d.L; ++l) {
-        if (pf && (rc = prefetch_layer(e, l + 1, s))) return rc;
         rc = run_block(e, l, B, s);
         if (rc) return rc;
-    }
-    if (pf) {   // the side stream's last reads end before the call's work does (the blob may be freed afterwards)
-        HIP_TRY(hipEventRecord(e->pf_ev, e->pf_stream));
-        HIP_TRY(hipStreamWaitEvent(s, e->pf_ev, 0));
     }
     q2a_pool_args pa{e->X, B, e->d.T, e->d.D, e->g<const float *>(G_LNP_W), e->g<const float *>(G_LNP_B), out, e->meta + 2 * B};
     PLAUNCH(e, s, Q2A_PROF_POOL, q2a_launch_pool_ln(pa, s));
@@ -1429,8 +1383,6 @@ void q2a_close(q2a_engine * e) {
     if (e->own_blob && e->blob) (void) hipFree(e->blob);
     if (e->frange) (void) hipFree(e->frange);
     if (e->meta_evt) (void) hipEventDestroy(e->meta_evt);
-    if (e->pf_stream) { (void) hipStreamSynchronize(e->pf_stream); (void) hipStreamDestroy(e->pf_stream); }
-    if (e->pf_ev) (void) hipEventDestroy(e->pf_ev);
     if (e->stream) (void) hipStreamDestroy(e->stream);
     delete e;
 }

@@ -361,37 +361,24 @@ __global__ __launch_bounds__(256) void k_quant_q8k_h16(const q2a_half * __restri
 // iteration ahead (register prefetch cannot run ahead: vmcnt retires in order and counts the stores, and with loads
 // and stores pending the compiler waits vmcnt(0), i.e. for the previous iteration's stores). Per iteration 2 DMA +
 // 3 stores (+1 for d on the unit's last iteration).
-// Q2A_GELU_COMPACT = 1: the |x| < 10 image of the table only (75 KiB: +0..+10 | -0..-10, what the GEMM epilogues
+// Measured alternative (diag/experiment_knobs_r05.patch, Q2A_GELU_COMPACT): the |x| < 10 image of the table only (75 KiB: +0..+10 | -0..-10, what the GEMM epilogues
 // stage), ggml's two branches as selects (x >= 10 -> x; x <= -10 -> the table's own -0, +0 for -inf), NaN inputs from
 // the full table in global memory (a wave-uniform branch that real data never takes) — and 16 waves per CU instead of
 // 8 (twice the input DMA in flight) in the LDS the full 128 KiB table held. Measured round 5 (diag/gpurun_r05f.sh):
 // bit-identical, quant_act 17.26 -> 19.2 ms per step (index arithmetic + selects cost more than the DMA depth gains);
 // a timing build with conflict-free reads bounds the whole bank-conflict cost at 0.3 ms per step. Diagnostic only.
-#ifndef Q2A_GELU_COMPACT
-#define Q2A_GELU_COMPACT 0
-#endif
-constexpr int GQ_THREADS = Q2A_GELU_COMPACT ? 1024 : 512;
+constexpr int GQ_THREADS = 512;
 constexpr int GQ_WAVES = GQ_THREADS / 64;
 typedef __attribute__((address_space(3))) void * lds_vptr_t;
 __global__ __launch_bounds__(GQ_THREADS) void k_gelu_quant_q8k_h16(const q2a_half * __restrict__ X, int M, int bpr,
                                                                    const uint16_t * __restrict__ gelu_tab, q2a_half * outH,
                                                                    float * dy, q2a_half * aext, int ld) {
-#if Q2A_GELU_COMPACT
-    __shared__ __attribute__((aligned(16))) uint16_t lut[(2 * Q2A_GELU_C_HALF + 7) / 8 * 8];
-    __shared__ __attribute__((aligned(16))) char stage[GQ_WAVES][2048];
-    for (int i = threadIdx.x; i < Q2A_GELU_C_HALF; i += GQ_THREADS) {
-        lut[i] = gelu_tab[i];
-        lut[Q2A_GELU_C_HALF + i] = gelu_tab[0x8000 + i];
-    }
-    __syncthreads();
-#else
     __shared__ __attribute__((aligned(16))) uint16_t lut[65536];
     __shared__ __attribute__((aligned(16))) char stage[GQ_WAVES][2048];
     for (int i = threadIdx.x; i < 65536 / 8; i += GQ_THREADS) ((uint4 *) lut)[i] = ((const uint4 *) gelu_tab)[i];
     __syncthreads();
     if (threadIdx.x == 0) lut[0xFC00] = 0;   // -inf (x below the fp16 range) -> +0
     __syncthreads();
-#endif
     const int lane = threadIdx.x & 63, sub = lane & 15, grp = lane >> 4;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int64_t K = (int64_t) bpr * 256;
@@ -470,14 +457,7 @@ __global__ __launch_bounds__(GQ_THREADS) void k_gelu_quant_q8k_h16(const q2a_hal
             const _Float16 he = e < 8 ? h0[e] : h1[e - 8];
             uint16_t u;
             __builtin_memcpy(&u, &he, 2);
-#ifdef Q2A_DIAG_GELU_NOCONF   // timing diagnostic only (wrong results): every lane reads entry 0 (no bank conflicts)
-            u = (uint16_t) (u & 0);
-#endif
-#if Q2A_GELU_COMPACT
-            const uint32_t ix = min((uint32_t) (u & 0x7FFF), (uint32_t) (Q2A_GELU_C_HALF - 1)) + ((u & 0x8000) ? Q2A_GELU_C_HALF : 0);
-#else
             const uint32_t ix = u;
-#endif
             asm volatile("ds_read_u16 %0, %1" : "=v"(g[e]) : "v"(lut0 + ix * 2));
         }
         asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(g[0]), "+v"(g[1]), "+v"(g[2]), "+v"(g[3]), "+v"(g[4]), "+v"(g[5]), "+v"(g[6]),
@@ -489,32 +469,7 @@ __global__ __launch_bounds__(GQ_THREADS) void k_gelu_quant_q8k_h16(const q2a_hal
             _Float16 gh;
             __builtin_memcpy(&gh, &gg, 2);
             v[e] = (float) gh;
-#if Q2A_GELU_COMPACT
-            const float xf = (float) (e < 8 ? h0[e] : h1[e - 8]);   // the table's values outside |x| < 10, exactly
-            v[e] = xf >= 10.0f ? xf : xf <= -10.0f ? (xf == -__builtin_inff() ? 0.0f : -0.0f) : v[e];
-#endif
         }
-#if Q2A_GELU_COMPACT
-        {   // a NaN pre-activation: the full table's entry (real data never gets here)
-            bool nan = false;
-#pragma unroll
-            for (int e = 0; e < 16; ++e) nan |= v[e] != v[e] || (e < 8 ? h0[e] != h0[e] : h1[e - 8] != h1[e - 8]);
-            if (__builtin_amdgcn_read_exec() & __ballot(nan)) {
-#pragma unroll
-                for (int e = 0; e < 16; ++e) {
-                    const _Float16 he = e < 8 ? h0[e] : h1[e - 8];
-                    if (he != he) {
-                        uint16_t u;
-                        __builtin_memcpy(&u, &he, 2);
-                        const uint16_t gg = gelu_tab[u];
-                        _Float16 gh;
-                        __builtin_memcpy(&gh, &gg, 2);
-                        v[e] = (float) gh;
-                    }
-                }
-            }
-        }
-#endif
         const int row = r0 + grp;
         float d;
         int sb;
@@ -616,11 +571,6 @@ hipError_t q2a_launch_mel(const q2a_mel_args & a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// Q2A_QUANT_V1 (diagnostic builds only): the round-1 one-row-per-wave LN+Q8_K and fp16-input Q8_K kernels instead of
-// the 8-rows-per-workgroup / 16-block forms (identical codes)
-#ifndef Q2A_QUANT_V1
-#define Q2A_QUANT_V1 0
-#endif
 hipError_t q2a_launch_layernorm(const q2a_ln_args & a, hipStream_t s) {
     if (a.D % 4 != 0 || a.D > 2048) return hipErrorInvalidValue;
     if (a.mode == 1 && a.D % 256) return hipErrorInvalidValue;
@@ -629,7 +579,7 @@ hipError_t q2a_launch_layernorm(const q2a_ln_args & a, hipStream_t s) {
     if (a.mode == 0) hipLaunchKernelGGL((k_rownorm<0, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else if (a.mode == 3) hipLaunchKernelGGL((k_rownorm<3, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else if (a.mode == 4) hipLaunchKernelGGL((k_rownorm<4, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
-    else if (a.mode == 1 && a.D == 1280 && !Q2A_QUANT_V1)
+    else if (a.mode == 1 && a.D == 1280)
         hipLaunchKernelGGL((k_rownorm<1, true, false, 5>), dim3((a.M + 7) / 8), dim3(512), 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy,
                            a.aext, 1, a.dy_ld);
     else if (a.mode == 1) hipLaunchKernelGGL((k_rownorm<1, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
@@ -657,7 +607,7 @@ hipError_t q2a_launch_quant_act(const q2a_quant_args & a, hipStream_t s) {
     const dim3 grid((a.M * nseg + 3) / 4), blk(256);
     // view X as [M*nseg][seg]: contiguous, and the block structure (256 / 32) never straddles a segment
     const float * X = a.XH ? (const float *) a.XH : a.X;
-    if (a.mode == 1 && a.XH && !Q2A_QUANT_V1) {
+    if (a.mode == 1 && a.XH) {
         const int64_t nb = (int64_t) a.M * (a.K / 256);
         hipLaunchKernelGGL(k_quant_q8k_h16, dim3((unsigned) ((nb + 15) / 16)), dim3(256), 0, s, a.XH, nb, a.K / 256, a.outH,
                            a.dy, a.aext, a.dy_ld);

@@ -35,77 +35,28 @@ typedef __attribute__((address_space(3))) void * lds_ptr_t;
 
 // timing diagnostic Q2A_DIAG_NO_STORE (wrong results): the epilogue computes every value but its global stores
 // are predicated off by a condition the compiler cannot fold
-#ifdef Q2A_DIAG_NO_VT_STORE   // timing diagnostic: only the V^T scatter stores predicated off
-#define Q2A_ST_VT (p.K < 0)
-#else
-#define Q2A_ST_VT true
-#endif
 #ifdef Q2A_DIAG_NO_STORE
 #define Q2A_ST (p.K < 0)
 #else
 #define Q2A_ST true
 #endif
 
-// epilogue global store (Q2A_DIAG_NT_STORE: non-temporal, A/B timing of the store cache policy)
+// epilogue global store (round 1 measured non-temporal stores +22 ms/step: plain stores)
 template <class V>
 __device__ __forceinline__ void q2a_st(const V & v, V * ptr) {
-#ifdef Q2A_DIAG_NT_STORE
-    typedef unsigned u4v __attribute__((ext_vector_type(4)));
-    typedef unsigned u2v __attribute__((ext_vector_type(2)));
-    if constexpr (sizeof(V) == 16) __builtin_nontemporal_store(__builtin_bit_cast(u4v, v), (u4v *) ptr);
-    else __builtin_nontemporal_store(__builtin_bit_cast(u2v, v), (u2v *) ptr);
-#else
     *ptr = v;
-#endif
 }
 
-// fp16 outputs of the 8-phase tile through the LDS-staged row-contiguous store (diagnostic builds: 0 = register path)
-#ifndef Q2A_GEMM_STAGED_EPI
-#define Q2A_GEMM_STAGED_EPI 1
-#endif
-// fc1 (Q4_K pre-activation) on persistent 8-phase tiles whose epilogue stores retire under the next tile (0 = one tile
-// per workgroup, a diagnostic build). Round 4 (diag/gpurun_r04d.sh): fc1 1.268 ms per launch (rocprof) against 1.341
-// one-tile-per-workgroup; same-box bench A/B fc1 39.5 / 40.4 against 41.1 / 40.7 ms per step; outputs bit-identical
-// (64-clip batch-invariance tests)
-// exact-accumulation conv GEMMs (Q2A_BLK_EXACT): LDS stages and tile (0: 64x128, 1: 128x128); diagnostic A/B knobs
-#ifndef Q2A_GEMM_EXACT_NS
-#define Q2A_GEMM_EXACT_NS 2
-#endif
-#ifndef Q2A_GEMM_EXACT_TILE
-#define Q2A_GEMM_EXACT_TILE 0
-#endif
-#ifndef Q2A_GEMM_PERSIST
-#define Q2A_GEMM_PERSIST 1
-#endif
-// 8-phase kernel: waves 4-7 one barrier behind waves 0-3 (0 = lockstep halves, a diagnostic build). Round 4, same box
-// (diag/gpurun_r04b.sh): fc1 tile 98.0k -> 82.4k shader cycles (main loop 84.2k -> 68.8k), whole step 238.6 / 242.9 ->
-// 229.2 / 227.9 ms, every weight GEMM 4-7 % faster
-#ifndef Q2A_GEMM_WSTAGGER
-#define Q2A_GEMM_WSTAGGER 1
-#endif
-// 8-phase kernel: the operand glds issued inside the MFMA segments (1) or before the reading wave's barrier (0)
-#ifndef Q2A_GEMM_GLDS_C
-#define Q2A_GEMM_GLDS_C 0
-#endif
-// 8-phase kernel with two phases of 32 MFMAs per K-step (four barrier intervals) instead of four of 16 (eight);
-// measured round 5 (diag/gpurun_r05a.sh): bit-identical, 1-3 ms per step SLOWER (fc1 / fc2), not adopted
-#ifndef Q2A_GEMM_P2
-#define Q2A_GEMM_P2 0
-#endif
-// 8-phase kernel with the quadrant order alternating between K-steps and the next K-step's first B_q fragments read in
-// phase 4 (which otherwise reads nothing): fragment reads per phase 8 / 4 / 8 / 4 instead of 12 / 4 / 8 / 0, six
-// phases of glds in flight instead of five ("GEMM pipeline")
-// Measured round 5 (profiles/r05h_gemm_alternating_order.json): bit-identical; F16 fc1 -1 %, Q4_K +2-4 % and the
-// residual-epilogue kernels spill at 256 VGPRs (whole step +15-25 ms); not adopted
-#ifndef Q2A_GEMM_ALT
-#define Q2A_GEMM_ALT 0
-#endif
-// Measured round 5 (profiles/r05r_block_start_early_reads.json): bit-identical, neutral; off.
-// 8-phase Q4_K kernel: a block's first phase issues its fragment reads BEFORE the block start (whose scale reads, wait
-// and rescale VALU then run under the fragment reads' latency) instead of after it
-#ifndef Q2A_GEMM_BSR
-#define Q2A_GEMM_BSR 0
-#endif
+// Schedule decisions of the 8-phase kernel, measured (the rejected alternatives' code is in
+// diag/experiment_knobs_r05.patch; DESIGN.md §4-§5 has the numbers):
+//   * fp16 outputs (fc1 pre-activation, Q / K hi|lo) staged through LDS and stored as whole 512-B rows;
+//   * fc1 (Q4_K pre-activation) on persistent tiles whose epilogue stores retire under the next tile (round 4,
+//     diag/gpurun_r04d.sh: 1.268 against 1.341 ms per launch, outputs bit-identical);
+//   * waves 4-7 one barrier behind waves 0-3 (round 4, diag/gpurun_r04b.sh: fc1 tile 98.0k -> 82.4k cycles, every
+//     weight GEMM 4-7 % faster);
+//   * not adopted: glds issued inside the MFMA segments, two phases of 32 MFMAs per K-step (round 5, 1-3 ms per step
+//     slower), the alternating quadrant order (r05h: Q4_K +2-4 %, spills), fragment reads before the Q4_K block start
+//     (r05r: neutral); the conv GEMMs' 128x128 / more-stage exact tiles (r04m).
 
 // Timing diagnostic Q2A_DIAG_STAMPS=<epi>: the 8-phase kernels of epilogue <epi> record s_memtime at fixed points of
 // every workgroup's tile (waves 0 and 4, lane 0) into g_q2a_stamps, read back by q2a_diag_stamps (diag/tile_stamps.py):
@@ -126,7 +77,7 @@ __device__ __forceinline__ void q2a_stamp_put(int k, uint64_t v) {
 
 constexpr int BK = 64;
 constexpr int ROWB = BK * 2;   // bytes per LDS row (64 halves)
-constexpr int GROUP_M = 4;   // swept 2..32 at the batched shapes (Q2A_GEMM_GROUP_M): 4 best by ~1 %
+constexpr int GROUP_M = 4;   // swept 2..32 at the batched shapes (round 1): 4 best by ~1 %
 
 __device__ __forceinline__ float gelu_lut(float x, const uint16_t * tab) {
     // ggml_vec_gelu_f32 with GGML_GELU_FP16 (ggml.c:2556-2570)
@@ -305,9 +256,6 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     const int nk = p.K / BK;
     // image h of buffer b: h = 0 A_q0, 1 A_q1, 2 B_q0, 3 B_q1
     auto stage = [&](int b, int h, int kt) {
-#ifdef Q2A_DIAG_NO_GLDS
-        if (kt >= 2) return;   // timing diagnostic only (wrong results): main-loop operand loads skipped
-#endif
         const int k0 = kt * BK;
         char * dst = lds_raw + (b * 4 + h) * HT + wave * 8 * ROWB;
 #pragma unroll
@@ -429,9 +377,6 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
 #define BS_T1() do { } while (0)
 #endif
     auto block_start = [&](auto first) {   // first: std::true_type for block 0 (acc = 0: only the min term)
-#ifdef Q2A_DIAG_NO_RESCALE
-        return;   // timing diagnostic only (wrong results)
-#endif
         // C^T accumulators: lane holds columns n = 16j + 4(lane>>4) + r of row m = 16i + (lane&15), so alpha (per
         // row) is one scalar per row block and beta / gamma (per column) one float4 per column block
         const uint32_t s_al = sb0 + ALPHA_OFF + (wm * 128 + (lane & 15)) * 4;
@@ -461,11 +406,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
         auto minterm = [&](f4 (&s2)[4], half4 a) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-#ifdef Q2A_DIAG_NO_MINTERM   // timing diagnostic only (wrong results): the min-term operands stand in for its MFMA
-                s2[j] = f4{(float) we[j][0], (float) we[j][1], (float) a[0], (float) a[1]};
-#else
                 s2[j] = __builtin_amdgcn_mfma_f32_16x16x16f16(we[j], a, f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-#endif
             }
         };
         if constexpr (PERS) {
@@ -533,19 +474,7 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
     };
     typedef const __attribute__((address_space(3))) half8 * lds_h8p;
     half8 af[4][2], bf[2][2][2];
-#ifdef Q2A_DIAG_NO_READS   // timing diagnostic only (wrong results): fragments never re-read from LDS in the loop
-#define Q2A_RD_ON (p.K < 0)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) af[i][s2] = (half8) ((_Float16) (lane * 0.01f + i + s2));
-#pragma unroll
-    for (int i = 0; i < 8; ++i) (&bf[0][0][0])[i] = (half8) ((_Float16) (lane * 0.02f + i));
-#else
-#define Q2A_RD_ON true
-#endif
     auto read_a = [&](int b, int qm) {
-        if (!Q2A_RD_ON) return;
         launder();
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -553,7 +482,6 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             for (int s2 = 0; s2 < 2; ++s2) af[i][s2] = *(lds_h8p) (uintptr_t) (abase[b][s2] + qm * HT + i * 16 * ROWB);
     };
     auto read_b = [&](int b, int qn) {
-        if (!Q2A_RD_ON) return;
         launder();
 #pragma unroll
         for (int j = 0; j < 2; ++j)
@@ -568,356 +496,42 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
                 acc[qm * 4 + i][qn * 2 + j] = mma16<BF>(bf[qn][j][s2], af[i][s2], acc[qm * 4 + i][qn * 2 + j]);
     };
     auto mma = [&](int qm, int qn) { mma_h(qm, qn, 0); mma_h(qm, qn, 1); };
-#ifdef Q2A_DIAG_U8_UNPACK
-    // timing diagnostic (results unchanged): the VALU that biased-uint8 activation codes would add — per 8-code
-    // fragment 4 v_perm_b32 (code byte | 0x64 -> fp16 1024 + u) and 4 v_pk_add_f16 (-1152) — issued as identity
-    // operations on the fp16 fragments between the fragment reads' wait and the MFMAs that consume them
-    auto unpack_a = [&]() {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                typedef uint32_t u4v __attribute__((ext_vector_type(4)));
-                u4v u = __builtin_bit_cast(u4v, af[i][s2]);
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    uint32_t w = u[k];
-                    asm volatile("v_perm_b32 %0, %0, %0, %1" : "+v"(w) : "s"(0x03020100u));
-                    asm volatile("v_pk_add_f16 %0, %0, %1" : "+v"(w) : "s"(0x80008000u));
-                    u[k] = w;
-                }
-                af[i][s2] = __builtin_bit_cast(half8, u);
-            }
-    };
-#define Q2A_U8U() unpack_a()
-#else
-#define Q2A_U8U() do { } while (0)
-#endif
-#ifdef Q2A_DIAG_NO_BAR   // timing diagnostic only (wrong results): no barriers inside the main loop
-#define Q2A_LOOP_BAR() do { } while (0)
-#else
-#define Q2A_LOOP_BAR() __builtin_amdgcn_s_barrier()
-#endif
-#if Q2A_GEMM_WSTAGGER
     // staggered halves: the fragment reads retire BEFORE the barrier, so an image restaged the phase after its last
     // read (A_q0) cannot overtake the other half's reads, which now run one barrier later (cdna_hip_programming.md
     // §5 WAR rule)
 #define Q2A_PB(N)                                               \
     asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");   \
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          \
-    Q2A_LOOP_BAR();                                             \
+    __builtin_amdgcn_s_barrier();                               \
     asm volatile("" ::: "memory");                              \
     __builtin_amdgcn_s_setprio(1)
-#else
-#define Q2A_PB(N)                                               \
-    asm volatile("s_waitcnt vmcnt(%0)" :: "n"(N) : "memory");   \
-    __builtin_amdgcn_s_barrier();                               \
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");          \
-    __builtin_amdgcn_s_setprio(1)
-#endif
 #define Q2A_PE()                                                \
     __builtin_amdgcn_s_setprio(0);                              \
     asm volatile("" ::: "memory");                              \
-    Q2A_LOOP_BAR();                                             \
+    __builtin_amdgcn_s_barrier();                               \
     asm volatile("" ::: "memory")
 // the four phases of one K-step in buffer B; S1..S4 = the stage statements issued in each phase
-#if Q2A_GEMM_GLDS_C
-// the phase's glds issued by the MFMA wave between the two halves of its 16 MFMAs, instead of by the reading wave
-// before its barrier: the reading segment (fragment reads + their wait) is then the partner's only work. A stage
-// moves one barrier LATER than in the reading segment (WAR: still after both halves' last read of the slot), so every
-// counted wait drops by the size of its own phase's stage (2, or 5 where phase 2 also carries the 3 scale pieces)
-#define Q2A_SB() __builtin_amdgcn_sched_barrier(0)
-#define Q2A_KSTEPC(B, S1, S2, S3, S4, V1, V2, V3, V4)                                                     \
-    read_b(B, 0); read_a(B, 0); Q2A_PB(V1); mma_h(0, 0, 0); Q2A_SB(); S1; Q2A_SB(); mma_h(0, 0, 1); Q2A_PE(); \
-    read_b(B, 1);               Q2A_PB(V2); mma_h(0, 1, 0); Q2A_SB(); S2; Q2A_SB(); mma_h(0, 1, 1); Q2A_PE(); \
-    read_a(B, 1);               Q2A_PB(V3); mma_h(1, 1, 0); Q2A_SB(); S3; Q2A_SB(); mma_h(1, 1, 1); Q2A_PE(); \
-                                Q2A_PB(V4); mma_h(1, 0, 0); Q2A_SB(); S4; Q2A_SB(); mma_h(1, 0, 1); Q2A_PE()
-#define Q2A_KSTEP(B, S1, S2, S3, S4, V1, V2, V3, V4) Q2A_KSTEPC(B, S1, S2, S3, S4, (V1) - 2, (V2) - 2, (V3) - 2, (V4) - 2)
-#define Q2A_KSTEP_S(B, S1, S2, S3, S4, V1, V2, V3, V4) Q2A_KSTEPC(B, S1, S2, S3, S4, (V1) - 2, (V2) - 5, (V3) - 2, (V4) - 2)
-#else
-#ifndef Q2A_DIAG_SKIP_RA   // timing diagnostic (wrong results): 1 = phase 1's A reads skipped, 3 = phase 3's
-#define Q2A_DIAG_SKIP_RA 0
-#endif
-#define Q2A_RA1(B) do { if (Q2A_DIAG_SKIP_RA != 1 || p.K < 0) read_a(B, 0); } while (0)
-#define Q2A_RA3(B) do { if (Q2A_DIAG_SKIP_RA != 3 || p.K < 0) read_a(B, 1); } while (0)
-#define Q2A_KSTEP(B, S1, S2, S3, S4, V1, V2, V3, V4)                                      \
-    read_b(B, 0); Q2A_RA1(B); S1; Q2A_PB(V1); Q2A_U8U(); mma(0, 0); Q2A_PE();             \
-    read_b(B, 1);               S2; Q2A_PB(V2); mma(0, 1); Q2A_PE();                      \
-    Q2A_RA3(B);                 S3; Q2A_PB(V3); Q2A_U8U(); mma(1, 1); Q2A_PE();           \
+// (phase 2 of a Q4_K block's first K-step also issues the block's 3 scale pieces)
+#define Q2A_KSTEP(B, S1, S2, S3, S4, V1, V2, V3, V4)                     \
+    read_b(B, 0); read_a(B, 0); S1; Q2A_PB(V1); mma(0, 0); Q2A_PE();     \
+    read_b(B, 1);               S2; Q2A_PB(V2); mma(0, 1); Q2A_PE();     \
+    read_a(B, 1);               S3; Q2A_PB(V3); mma(1, 1); Q2A_PE();     \
                                 S4; Q2A_PB(V4); mma(1, 0); Q2A_PE()
-#if Q2A_GEMM_BSR
-// a block's first K-step: phase 1's B fragments were read before the block start (Q2A_BSR; with the A fragments
-// too the 48 fragment registers beside the block start's temporaries spill ~60 VGPRs)
-#define Q2A_BSR() do { read_b(0, 0); } while (0)
-#define Q2A_KSTEP_S(B, S1, S2, S3, S4, V1, V2, V3, V4)                                    \
-                  Q2A_RA1(B);   S1; Q2A_PB(V1); Q2A_U8U(); mma(0, 0); Q2A_PE();           \
-    read_b(B, 1);               S2; Q2A_PB(V2); mma(0, 1); Q2A_PE();                      \
-    Q2A_RA3(B);                 S3; Q2A_PB(V3); Q2A_U8U(); mma(1, 1); Q2A_PE();           \
-                                S4; Q2A_PB(V4); mma(1, 0); Q2A_PE()
-#else
-#define Q2A_BSR() do { } while (0)
-#define Q2A_KSTEP_S Q2A_KSTEP   // (phase 2 also issues the block's 3 scale pieces)
-#endif
-#endif
 
-#if Q2A_GEMM_ALT
-    // Alternating quadrant order. The first quadrant of a K-step needs both an A and a B half of the new k-slice; in
-    // the fixed order that is phase 1's 12-read burst (8 A + 4 B fragments), the critical path of the staggered
-    // pipeline (profiles/r05g_read_burst_and_backend.json), while phase 4 reads nothing. Here the even K-step runs
-    // (0,0) (0,1) (1,1) (1,0) and the odd one (0,1) (0,0) (1,0) (1,1): the B half an odd step starts with (B_q1) is free
-    // in registers during the even step's phase 4 and vice versa (B_q0), so phase 4 reads the NEXT K-step's first B
-    // half ("PF") and every phase reads 8 / 4 / 8 / 4 fragments with the same registers. Images of K-step t are
-    // first read in phase 4 of t-1 (Bf = the prefetched B half), 1 (A_q0), 2 (Bs = the other B half), 3 (A_q1) of t;
-    // each slot of buffer t%2 is restaged for t+2 the phase after its last read: Bf in phase 1, A_q0 in 2, Bs in 3,
-    // A_q1 in 4 of step t. Every image is then first read 7 (Bf) or 6 phases after its issue and must have landed
-    // by the wait before the phase preceding that read: vmcnt(12), six stages of 2 glds in flight.
-#define Q2A_KSTEP_E(B, S1, S2, S3, S4, V1, V2, V3, V4, PF)     \
-    read_a(B, 0); S1; Q2A_PB(V1); mma(0, 0); Q2A_PE();        \
-    read_b(B, 1); S2; Q2A_PB(V2); mma(0, 1); Q2A_PE();        \
-    read_a(B, 1); S3; Q2A_PB(V3); mma(1, 1); Q2A_PE();        \
-    PF;           S4; Q2A_PB(V4); mma(1, 0); Q2A_PE()
-#define Q2A_KSTEP_O(B, S1, S2, S3, S4, V1, V2, V3, V4, PF)     \
-    read_a(B, 0); S1; Q2A_PB(V1); mma(0, 1); Q2A_PE();        \
-    read_b(B, 0); S2; Q2A_PB(V2); mma(0, 0); Q2A_PE();        \
-    read_a(B, 1); S3; Q2A_PB(V3); mma(1, 0); Q2A_PE();        \
-    PF;           S4; Q2A_PB(V4); mma(1, 1); Q2A_PE()
-#define Q2A_NOPF (void) 0
-#endif
-#if Q2A_GEMM_P2
-    // two phases per K-step, 32 MFMAs each (one barrier interval = one SIMD's 32 MFMAs beside its partner's reads):
-    //   phase a: B_q0, B_q1, A_q0 fragments | stage A_q1 of step t+1        | mma(0,0), mma(0,1)
-    //   phase b: A_q1 fragments             | stage A_q0, B_q0, B_q1 of t+2 | mma(1,1), mma(1,0)
-    // With the halves one barrier apart, an image's last read (waves 4-7) ends one interval after the first half's,
-    // so A_q0 / B_q0 / B_q1 of buffer t%2 are free from phase b of step t on, A_q1 from phase a of step t+1. Every
-    // group waits one K-step (four barrier intervals): vmcnt(8) = the 2 + 6 younger glds of the last two phases.
-#define Q2A_KSTEP2(B, SA, SB, VA, VB)                                                                \
-    read_b(B, 0); read_b(B, 1); read_a(B, 0); SA; Q2A_PB(VA); mma(0, 0); mma(0, 1); Q2A_PE();      \
-    read_a(B, 1);                             SB; Q2A_PB(VB); mma(1, 1); mma(1, 0); Q2A_PE()
-#endif
     // prologue: the images "phases 2..8 of iteration -1" would have staged (block 0's scales before them)
     if constexpr (BLK == 256) stage_scales(0);
-#if Q2A_GEMM_ALT
-    // the stages of "K-steps -2 and -1" in their issue order; the first two (B_q0, A_q0 of step 0) and the scales land
-    stage(0, 2, 0); stage(0, 0, 0); stage(0, 3, 0); stage(0, 1, 0);
-    stage(1, 3, 1); stage(1, 0, 1); stage(1, 2, 1); stage(1, 1, 1);
-    asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-#else
     stage(0, 0, 0); stage(0, 2, 0); stage(0, 3, 0); stage(0, 1, 0);
     stage(1, 0, 1); stage(1, 2, 1); stage(1, 3, 1);
-#endif
-#if Q2A_GEMM_ALT
-#elif Q2A_GEMM_P2
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");   // A_q0, B_q0, B_q1 of step 0 (and block 0's scales) landed
-#else
     asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-#endif
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     // wave stagger: the M-half wm = 1 (waves 4-7, the SIMD partners of waves 0-3) runs one barrier behind, so each
     // SIMD alternates one wave's MFMA segment with its partner's fragment reads / glds issue (MI355X_MICROARCH.md,
     // "Two waves per SIMD" item 9); the other half pays the extra barrier after the loop
     Q2A_STAMP(ST, 1);
-    auto stagger_in = [&]() { if (Q2A_GEMM_WSTAGGER && wm == 1) { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); } };
-    auto stagger_out = [&]() { if (Q2A_GEMM_WSTAGGER && wm == 0) { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); } };
+    auto stagger_in = [&]() { if (wm == 1) { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); } };
+    auto stagger_out = [&]() { if (wm == 0) { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); } };
 
-#if Q2A_GEMM_ALT
-    // glds per wave: 2 per phase, +3 block scales in phase 2 of a block's first K-step (K0), which stay younger than
-    // the waited-for stage for six waits (counts 15) and have landed by phase 1 of K2, so the next block's alpha is
-    // computed in phase 2 of K2. Persistent form: the previous tile's S_EPI epilogue stores sit between its last stage
-    // and this tile's first one, younger than the waited-for stage for the first six waits (+16).
-    if constexpr (BLK == 0) {
-        read_b(0, 0);
-        stagger_in();
-        int kt = 0;
-        for (; kt < nk - 2; kt += 2) {
-            Q2A_KSTEP_E(0, stage(0, 2, kt + 2), stage(0, 0, kt + 2), stage(0, 3, kt + 2), stage(0, 1, kt + 2), 12, 12, 12, 12, read_b(1, 1));
-            Q2A_KSTEP_O(1, stage(1, 3, kt + 3), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 1, kt + 3), 12, 12, 12, 12, read_b(0, 0));
-        }
-        Q2A_KSTEP_E(0, stage_tail(0, 2), stage_tail(0, 0), stage_tail(0, 3), stage_tail(0, 1), 12, 12, 12, 12, read_b(1, 1));
-        Q2A_KSTEP_O(1, stage_tail(1, 3), stage_tail(1, 0), stage_tail(1, 2), stage_tail(1, 1), 12, 12, 12, 12, Q2A_NOPF);
-    } else if constexpr (PERS) {
-        static_assert(BLK == 256, "persistent 8-phase loop: Q4_K only");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        alpha_compute();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        // the first tile's B_q0 half; every later tile's is read by the previous tile's last phase 4 and carried across
-        // its epilogue in registers (reading it here instead would race the other half's phase-1 restage of that slot)
-        read_b(0, 0);
-        stagger_in();
-        for (;;) {
-            int m0n = 0, n0n = 0;
-            const bool has_next = next(m0n, n0n);
-            auto stage_next = [&](int b, int h) { stage(b, h, has_next ? b : nk - 1); };
-            int kt = 0;
-            BS_T0();
-            block_start(std::true_type{});
-            BS_T1();
-            asm volatile("" ::: "memory");
-            Q2A_KSTEP_E(0, stage(0, 2, 2), (stage(0, 0, 2), stage_scales(1)), stage(0, 3, 2), stage(0, 1, 2), 28, 31, 31, 31, read_b(1, 1));
-            Q2A_KSTEP_O(1, stage(1, 3, 3), stage(1, 0, 3), stage(1, 2, 3), stage(1, 1, 3), 31, 31, 15, 15, read_b(0, 0));
-            Q2A_KSTEP_E(0, stage(0, 2, 4), (alpha_compute(), stage(0, 0, 4)), stage(0, 3, 4), stage(0, 1, 4), 12, 12, 12, 12, read_b(1, 1));
-            Q2A_KSTEP_O(1, stage(1, 3, 5), stage(1, 0, 5), stage(1, 2, 5), stage(1, 1, 5), 12, 12, 12, 12, read_b(0, 0));
-            for (kt = 4; kt < nk - 4; kt += 4) {
-                BS_T0();
-                block_start(std::false_type{});
-                BS_T1();
-                asm volatile("" ::: "memory");
-                Q2A_KSTEP_E(0, stage(0, 2, kt + 2), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 3, kt + 2),
-                            stage(0, 1, kt + 2), 12, 15, 15, 15, read_b(1, 1));
-                Q2A_KSTEP_O(1, stage(1, 3, kt + 3), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 1, kt + 3), 15, 15, 15, 15,
-                            read_b(0, 0));
-                Q2A_KSTEP_E(0, stage(0, 2, kt + 4), (alpha_compute(), stage(0, 0, kt + 4)), stage(0, 3, kt + 4), stage(0, 1, kt + 4),
-                            12, 12, 12, 12, read_b(1, 1));
-                Q2A_KSTEP_O(1, stage(1, 3, kt + 5), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 1, kt + 5), 12, 12, 12, 12,
-                            read_b(0, 0));
-            }
-            prep_scales_last(has_next, m0n, n0n);
-            BS_T0();
-            block_start(std::false_type{});   // (nk >= 8: the last block is never block 0)
-            BS_T1();
-            asm volatile("" ::: "memory");
-            Q2A_KSTEP_E(0, stage(0, 2, kt + 2), (stage(0, 0, kt + 2), stage_scales_last()), stage(0, 3, kt + 2), stage(0, 1, kt + 2),
-                        12, 15, 15, 15, read_b(1, 1));
-            Q2A_KSTEP_O(1, stage(1, 3, kt + 3), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 1, kt + 3), 15, 15, 15, 15,
-                        read_b(0, 0));
-            // the last two K-steps stage the next tile's first two
-            Q2A_KSTEP_E(0, ((has_next ? set_offsets(m0n, n0n) : (void) 0), stage_next(0, 2)), stage_next(0, 0), stage_next(0, 3),
-                        stage_next(0, 1), 12, 12, 12, 12, read_b(1, 1));
-            Q2A_KSTEP_O(1, stage_next(1, 3), stage_next(1, 0), stage_next(1, 2), stage_next(1, 1), 12, 12, 12, 12, read_b(0, 0));
-            __builtin_amdgcn_sched_barrier(0);
-            epi(acc, m0, n0);
-            __builtin_amdgcn_sched_barrier(0);
-            if (!has_next) break;
-            m0 = m0n;
-            n0 = n0n;
-        }
-    } else {
-        static_assert(BLK == 256, "8-phase k-quant loop is Q4_K only");
-        alpha_compute();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        read_b(0, 0);
-        stagger_in();
-        int kt = 0;
-        for (; kt < nk - 4; kt += 4) {
-            BS_T0();
-            if (kt == 0) block_start(std::true_type{});
-            else block_start(std::false_type{});
-            BS_T1();
-            asm volatile("" ::: "memory");
-            Q2A_KSTEP_E(0, stage(0, 2, kt + 2), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 3, kt + 2),
-                        stage(0, 1, kt + 2), 12, 15, 15, 15, read_b(1, 1));
-            Q2A_KSTEP_O(1, stage(1, 3, kt + 3), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 1, kt + 3), 15, 15, 15, 15,
-                        read_b(0, 0));
-            Q2A_KSTEP_E(0, stage(0, 2, kt + 4), (alpha_compute(), stage(0, 0, kt + 4)), stage(0, 3, kt + 4), stage(0, 1, kt + 4),
-                        12, 12, 12, 12, read_b(1, 1));
-            Q2A_KSTEP_O(1, stage(1, 3, kt + 5), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 1, kt + 5), 12, 12, 12, 12,
-                        read_b(0, 0));
-        }
-        BS_T0();
-        if (kt == 0) block_start(std::true_type{});
-        else block_start(std::false_type{});
-        BS_T1();
-        asm volatile("" ::: "memory");
-        Q2A_KSTEP_E(0, stage(0, 2, kt + 2), (stage(0, 0, kt + 2), stage_scales(kt / 4)), stage(0, 3, kt + 2), stage(0, 1, kt + 2),
-                    12, 15, 15, 15, read_b(1, 1));
-        Q2A_KSTEP_O(1, stage(1, 3, kt + 3), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 1, kt + 3), 15, 15, 15, 15,
-                    read_b(0, 0));
-        Q2A_KSTEP_E(0, stage_tail(0, 2), stage_tail(0, 0), stage_tail(0, 3), stage_tail(0, 1), 12, 12, 12, 12, read_b(1, 1));
-        Q2A_KSTEP_O(1, stage_tail(1, 3), stage_tail(1, 0), stage_tail(1, 2), stage_tail(1, 1), 12, 12, 12, 12, Q2A_NOPF);
-    }
-#undef Q2A_KSTEP_E
-#undef Q2A_KSTEP_O
-#undef Q2A_NOPF
-#elif Q2A_GEMM_P2
-    // glds stream per wave and K-step t: phase a {A_q1(t+1)} 2, phase b {A_q0, B_q0, B_q1 (t+2)} 6 (+3 block scales in
-    // phase b of a block's first K-step). Steady count 8; the scale pieces raise the next three waits to 11 (they are
-    // retired by phase a of the block's third K-step, whose phase b computes the next block's alpha from them).
-    if constexpr (BLK == 0) {
-        stagger_in();
-        int kt = 0;
-        for (; kt < nk - 2; kt += 2) {
-            Q2A_KSTEP2(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage(0, 2, kt + 2), stage(0, 3, kt + 2)), 8, 8);
-            Q2A_KSTEP2(1, stage(0, 1, kt + 2), (stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3)), 8, 8);
-        }
-        Q2A_KSTEP2(0, stage(1, 1, kt + 1), (stage_tail(0, 0), stage_tail(0, 2), stage_tail(0, 3)), 8, 8);
-        Q2A_KSTEP2(1, stage_tail(0, 1), (stage_tail(1, 0), stage_tail(1, 2), stage_tail(1, 3)), 8, 8);
-    } else if constexpr (PERS) {
-        static_assert(BLK == 256, "persistent 8-phase loop: Q4_K only");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        alpha_compute();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        stagger_in();
-        for (;;) {
-            int m0n = 0, n0n = 0;
-            const bool has_next = next(m0n, n0n);
-            auto stage_next = [&](int b, int h) { stage(b, h, has_next ? b : nk - 1); };
-            int kt = 0;
-            block_start(std::true_type{});
-            asm volatile("" ::: "memory");
-            // block 0: the previous tile's S_EPI epilogue stores sit between its last phase b and this phase a
-            Q2A_KSTEP2(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage(0, 2, kt + 2), stage(0, 3, kt + 2), stage_scales(kt / 4 + 1)),
-                       24, 27);
-            Q2A_KSTEP2(1, stage(0, 1, kt + 2), (stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3)), 11, 11);
-            Q2A_KSTEP2(0, stage(1, 1, kt + 3), (alpha_compute(), stage(0, 0, kt + 4), stage(0, 2, kt + 4), stage(0, 3, kt + 4)), 8, 8);
-            Q2A_KSTEP2(1, stage(0, 1, kt + 4), (stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5)), 8, 8);
-            for (kt = 4; kt < nk - 4; kt += 4) {
-                block_start(std::false_type{});
-                asm volatile("" ::: "memory");
-                Q2A_KSTEP2(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage(0, 2, kt + 2), stage(0, 3, kt + 2), stage_scales(kt / 4 + 1)),
-                           8, 11);
-                Q2A_KSTEP2(1, stage(0, 1, kt + 2), (stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3)), 11, 11);
-                Q2A_KSTEP2(0, stage(1, 1, kt + 3), (alpha_compute(), stage(0, 0, kt + 4), stage(0, 2, kt + 4), stage(0, 3, kt + 4)), 8, 8);
-                Q2A_KSTEP2(1, stage(0, 1, kt + 4), (stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5)), 8, 8);
-            }
-            prep_scales_last(has_next, m0n, n0n);
-            block_start(std::false_type{});   // (nk >= 8: the last block is never block 0)
-            asm volatile("" ::: "memory");
-            Q2A_KSTEP2(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage(0, 2, kt + 2), stage(0, 3, kt + 2), stage_scales_last()), 8, 11);
-            Q2A_KSTEP2(1, stage(0, 1, kt + 2), (stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3)), 11, 11);
-            Q2A_KSTEP2(0, (stage(1, 1, kt + 3), (has_next ? set_offsets(m0n, n0n) : (void) 0)),
-                       (stage_next(0, 0), stage_next(0, 2), stage_next(0, 3)), 8, 8);
-            Q2A_KSTEP2(1, stage_next(0, 1), (stage_next(1, 0), stage_next(1, 2), stage_next(1, 3)), 8, 8);
-            __builtin_amdgcn_sched_barrier(0);
-            epi(acc, m0, n0);
-            __builtin_amdgcn_sched_barrier(0);
-            if (!has_next) break;
-            m0 = m0n;
-            n0 = n0n;
-        }
-    } else {
-        static_assert(BLK == 256, "8-phase k-quant loop is Q4_K only");
-        alpha_compute();
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        stagger_in();
-        int kt = 0;
-        for (; kt < nk - 4; kt += 4) {
-            if (kt == 0) block_start(std::true_type{});
-            else block_start(std::false_type{});
-            asm volatile("" ::: "memory");
-            Q2A_KSTEP2(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage(0, 2, kt + 2), stage(0, 3, kt + 2), stage_scales(kt / 4 + 1)),
-                       8, 11);
-            Q2A_KSTEP2(1, stage(0, 1, kt + 2), (stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3)), 11, 11);
-            Q2A_KSTEP2(0, stage(1, 1, kt + 3), (alpha_compute(), stage(0, 0, kt + 4), stage(0, 2, kt + 4), stage(0, 3, kt + 4)), 8, 8);
-            Q2A_KSTEP2(1, stage(0, 1, kt + 4), (stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5)), 8, 8);
-        }
-        if (kt == 0) block_start(std::true_type{});
-        else block_start(std::false_type{});
-        asm volatile("" ::: "memory");
-        Q2A_KSTEP2(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage(0, 2, kt + 2), stage(0, 3, kt + 2), stage_scales(kt / 4)), 8, 11);
-        Q2A_KSTEP2(1, stage(0, 1, kt + 2), (stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3)), 11, 11);
-        Q2A_KSTEP2(0, stage(1, 1, kt + 3), (stage_tail(0, 0), stage_tail(0, 2), stage_tail(0, 3)), 8, 8);
-        Q2A_KSTEP2(1, stage_tail(0, 1), (stage_tail(1, 0), stage_tail(1, 2), stage_tail(1, 3)), 8, 8);
-    }
-#undef Q2A_KSTEP2
-#else
     if constexpr (BLK == 0) {
         stagger_in();
         int kt = 0;
@@ -943,24 +557,22 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             // the next tile's first K-steps (tail stages), or a harmless re-load of this tile's last one
             auto stage_next = [&](int b, int h) { stage(b, h, has_next ? b : nk - 1); };
             int kt = 0;
-            Q2A_BSR();
             BS_T0();
             block_start(std::true_type{});
             BS_T1();
             asm volatile("" ::: "memory");
-            Q2A_KSTEP_S(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
+            Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
                       stage(0, 3, kt + 2), 26, 29, 29, 29);
             Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 29, 13, 10, 10);
             Q2A_KSTEP(0, (alpha_compute(), stage(1, 1, kt + 3)), stage(0, 0, kt + 4), stage(0, 2, kt + 4), stage(0, 3, kt + 4),
                       10, 10, 10, 10);
             Q2A_KSTEP(1, stage(0, 1, kt + 4), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5), 10, 10, 10, 10);
             for (kt = 4; kt < nk - 4; kt += 4) {
-                Q2A_BSR();
             BS_T0();
                 block_start(std::false_type{});
                 BS_T1();
                 asm volatile("" ::: "memory");
-                Q2A_KSTEP_S(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
+                Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
                           stage(0, 3, kt + 2), 10, 13, 13, 13);
                 Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 13, 13, 10, 10);
                 Q2A_KSTEP(0, (alpha_compute(), stage(1, 1, kt + 3)), stage(0, 0, kt + 4), stage(0, 2, kt + 4), stage(0, 3, kt + 4),
@@ -968,12 +580,11 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
                 Q2A_KSTEP(1, stage(0, 1, kt + 4), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5), 10, 10, 10, 10);
             }
             prep_scales_last(has_next, m0n, n0n);
-            Q2A_BSR();
             BS_T0();
             block_start(std::false_type{});   // (nk >= 8: the last block is never block 0)
             BS_T1();
             asm volatile("" ::: "memory");
-            Q2A_KSTEP_S(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales_last()), stage(0, 2, kt + 2),
+            Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales_last()), stage(0, 2, kt + 2),
                       stage(0, 3, kt + 2), 10, 13, 13, 13);
             Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 13, 13, 10, 10);
             Q2A_KSTEP(0, stage(1, 1, kt + 3), ((has_next ? set_offsets(m0n, n0n) : (void) 0), stage_next(0, 0)), stage_next(0, 2),
@@ -995,13 +606,12 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
         stagger_in();
         int kt = 0;
         for (; kt < nk - 4; kt += 4) {
-            Q2A_BSR();
             BS_T0();
             if (kt == 0) block_start(std::true_type{});
             else block_start(std::false_type{});
             BS_T1();
             asm volatile("" ::: "memory");
-            Q2A_KSTEP_S(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
+            Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
                       stage(0, 3, kt + 2), 10, 13, 13, 13);
             Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 13, 13, 10, 10);
             // phase 9: the next block's alpha (its scales, staged in phase 2, landed by phase 7)
@@ -1010,26 +620,18 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             Q2A_KSTEP(1, stage(0, 1, kt + 4), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5), 10, 10, 10, 10);
         }
         // last block: its scales stay in place for the final multiply (the scale re-stage keeps the vmcnt counts)
-        Q2A_BSR();
         BS_T0();
         if (kt == 0) block_start(std::true_type{});
         else block_start(std::false_type{});
         BS_T1();
         asm volatile("" ::: "memory");
-        Q2A_KSTEP_S(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4)), stage(0, 2, kt + 2),
+        Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4)), stage(0, 2, kt + 2),
                   stage(0, 3, kt + 2), 10, 13, 13, 13);
         Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 13, 13, 10, 10);
         Q2A_KSTEP(0, stage(1, 1, kt + 3), stage_tail(0, 0), stage_tail(0, 2), stage_tail(0, 3), 10, 10, 10, 10);
         Q2A_KSTEP(1, stage_tail(0, 1), stage_tail(1, 0), stage_tail(1, 2), stage_tail(1, 3), 10, 10, 10, 10);
     }
-#endif
 #undef Q2A_KSTEP
-#undef Q2A_KSTEP_S
-#undef Q2A_BSR
-#ifdef Q2A_KSTEPC
-#undef Q2A_KSTEPC
-#undef Q2A_SB
-#endif
 #undef Q2A_PB
 #undef Q2A_PE
 #undef BS_T0
@@ -1111,7 +713,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     constexpr int NS_MAX = BLK == 256 ? 6 - SP : 5;
     // deep pipelines only on the narrow 64-row tiles (grids under one workgroup per CU); the 128-row tiles keep two
     // stages so two workgroups share a CU (their grids have several tiles per CU)
-    constexpr int NS = EX ? Q2A_GEMM_EXACT_NS : PIPE || BLK == 32 || BM > 64 ? 2 : (NS_FIT >= NS_MAX ? NS_MAX : NS_FIT >= 2 ? NS_FIT : 2);
+    constexpr int NS = EX ? 2 : PIPE || BLK == 32 || BM > 64 ? 2 : (NS_FIT >= NS_MAX ? NS_MAX : NS_FIT >= 2 ? NS_FIT : 2);
     static_assert(PIPE || BLK != 256 || SP + NS <= 6, "Q4_K scale prefetch distance");
     static_assert(NBUF == 2 || (NS == 2 && SP <= 3), "single Q4_K scale buffer: pieces on steps 4b+1 .. 4b+3");
     constexpr int LDS_MAIN = PIPE == 2 ? SBUF_OFF + SBUF_BYTES + 512 : PIPE ? (BLK ? SBUF_OFF + SBUF_BYTES : 2 * OPB) : NS * OPB + SCALE_LDS;
@@ -1124,12 +726,6 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     const int wm = wave / WN, wn = wave % WN;
 
     // XCD-contiguous bijective remap, then grouped rasterisation (GROUP_M M-tiles per N column)
-    if (PIPE && p.stagger_ns > 0 && blockIdx.x < 256) {
-        // desynchronise the CUs' tile rounds: CU group (blockIdx/8) % G of the first round starts group * ns / G later
-        const uint64_t dt = (uint64_t) (((blockIdx.x >> 3) % p.stagger_g) * (p.stagger_ns / p.stagger_g)) / 10;
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (__builtin_amdgcn_s_memrealtime() - t0 < dt) __builtin_amdgcn_s_sleep(8);
-    }
     constexpr bool GROUPABLE = !PIPE && !BF && !EX && (BLK == 0 || BLK == 256) && EPI == Q2A_EPI_STORE_F;
     const int ngrp = (GROUPABLE && p.ngroup == 2) ? 2 : 1;
     const int ksplit = (!PIPE && !EX && (BLK == 0 || BLK == 32) && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_STORE_F) &&
@@ -1145,7 +741,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
         }
     }
     const int ks = wgid_all / ntl, wgid = wgid_all - ks * ntl;   // K-split index, tile index
-    const int GM = p.group_m > 0 ? p.group_m : GROUP_M;
+    constexpr int GM = GROUP_M;
     const int gsize = GM * nbn, g = wgid / gsize, gr = wgid % gsize;
     const int gm = min(GM, nbm - g * GM);
     const int tm = g * GM + gr % gm, tn = gr / gm;
@@ -1647,17 +1243,6 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
         return;
     }
 
-#ifdef Q2A_DIAG_NO_EPI
-    {   // timing diagnostic only (wrong results): keep the accumulators live, skip the epilogue
-        float t = 0.f;
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-            for (int j = 0; j < NJ; ++j) t += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
-        if (t == 1234.5f && p.outF) p.outF[0] = t;
-        return;
-    }
-#endif
     // ---- epilogue. The accumulators are C^T tiles (the MFMAs take W as A and the activations as B): lane holds the
     // 4 CONSECUTIVE output columns n = 16j + 4q + r (q = lane>>4) of ONE row m = 16i + (lane&15), so results go to
     // memory straight from registers: f32 outputs as one float4 per (i, j); fp16 outputs as 16 B after one lane
@@ -1702,7 +1287,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
         return odd ? make_uint4(recv.x, recv.y, ub.x, ub.y) : make_uint4(ua.x, ua.y, recv.x, recv.y);
     };
     const int pcol = 16 * (q & 1) + 8 * (q >> 1);    // column of this lane's 16-B piece within a 32-column pair
-    if (Q2A_GEMM_STAGED_EPI && PIPE == 1 && (EPI == Q2A_EPI_PRE_H || (EPI == Q2A_EPI_QKV && part < 2))) {
+    if (PIPE == 1 && (EPI == Q2A_EPI_PRE_H || (EPI == Q2A_EPI_QKV && part < 2))) {
       if constexpr (PIPE == 1 && (EPI == Q2A_EPI_PRE_H || EPI == Q2A_EPI_QKV)) {
         // fp16 outputs of the 8-phase tile (fc1's pre-activation; Q / K hi and lo), staged through LDS so every store
         // instruction writes two WHOLE 512-B output rows: all 8 waves write the tile [256 rows][256 cols] into the idle
@@ -1819,7 +1404,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                             // (a pad row of a wave starting at or past T has clip0 = 1: it is clip 0's t = m)
                             const int clip = pad ? 0 : clip0 + (wrap ? 1 : 0), t = pad ? m : t0 + ml - (wrap ? p.T : 0);
                             const uint2 v = pad ? make_uint2(0u, 0u) : *(const uint2 *) (src + d * VS + 4 * a);
-                            if (Q2A_ST && Q2A_ST_VT) q2a_st(v, (uint2 *) (vdst + (((int64_t) clip * p.H + h) * 64 + d) * p.TP + t));
+                            if (Q2A_ST) q2a_st(v, (uint2 *) (vdst + (((int64_t) clip * p.H + h) * 64 + d) * p.TP + t));
                         }
                     }
                 }
@@ -2101,31 +1686,8 @@ hipError_t launch_cfg(const q2a_gemm_args & a, hipStream_t s) {
     return hipGetLastError();
 }
 
-// Tile-regime selection is fixed at compile time (every regime sums K in the same order, so these change speed, not
-// results). Diagnostic builds (diag/build_variant.sh) may override: Q2A_GEMM_NO_NARROW / Q2A_GEMM_NARROW_ALL (64-row
-// tiles never / for every small-M GEMM), Q2A_GEMM_TILE (1 force 256-wide, 2 force 128-wide), Q2A_GEMM_PIPE (0 = no
-// 8-phase kernel), Q2A_GEMM_GROUP_M (rasterisation group), Q2A_GEMM_STAGGER_NS / _G (first-round CU stagger).
-#ifndef Q2A_GEMM_NO_NARROW
-#define Q2A_GEMM_NO_NARROW 0
-#endif
-#ifndef Q2A_GEMM_NARROW_ALL
-#define Q2A_GEMM_NARROW_ALL 0
-#endif
-#ifndef Q2A_GEMM_TILE
-#define Q2A_GEMM_TILE 0
-#endif
-#ifndef Q2A_GEMM_PIPE
-#define Q2A_GEMM_PIPE 1
-#endif
-#ifndef Q2A_GEMM_GROUP_M
-#define Q2A_GEMM_GROUP_M 0
-#endif
-#ifndef Q2A_GEMM_STAGGER_NS
-#define Q2A_GEMM_STAGGER_NS 0
-#endif
-#ifndef Q2A_GEMM_STAGGER_G
-#define Q2A_GEMM_STAGGER_G 2
-#endif
+// Tile regimes (every regime sums K in the same order, so they change speed, not results). The rejected tile / raster /
+// stagger / tail alternatives measured in rounds 1-5 are recorded in DESIGN.md and diag/experiment_knobs_r05.patch.
 
 // M-waves of the small-batch tiles (a single clip's GEMMs): 2 = 4-wave workgroups, 4 = 8 waves (16 / 32 rows per wave;
 // every wave keeps 64 columns, so the K order per output and the epilogues are those of the 4-wave form). The narrow
@@ -2133,35 +1695,17 @@ hipError_t launch_cfg(const q2a_gemm_args & a, hipStream_t s) {
 // overlap one wave's issue with the other's MFMAs — Q4_K one clip 8.35 -> 7.73 ms per encode (fc2 2.26 -> 1.78, O
 // 0.79 -> 0.68), F16 unchanged; the 128x128 tiles with 8 waves: F16 fc1 -5 %, Q4_K QKV / fc1 +18 %: kept at 4
 // (round 5, diag/gpurun_r05e.sh, profiles/r05e_small_tiles_8waves.json)
-#ifndef Q2A_GEMM_NARROW_WM
-#define Q2A_GEMM_NARROW_WM 4
-#endif
-#ifndef Q2A_GEMM_SMALL_WM
-#define Q2A_GEMM_SMALL_WM 2
-#endif
 
 // small M (one or a few clips): 64-row tiles when 128x128 tiles would leave CUs idle
 bool narrow_tiles(int M, int N) {
-    return !Q2A_GEMM_NO_NARROW && (Q2A_GEMM_NARROW_ALL || (int64_t) ((M + 127) / 128) * (N / 128) < 256);
+    return (int64_t) ((M + 127) / 128) * (N / 128) < 256;
 }
 
 bool wide_tiles(int M, int N) {
     // big M: 256-wide tiles on 8 waves (k-quant variants keep 128 rows: the per-block accumulators double the
     // register footprint); small M (a single clip): 128x128 on 4 waves so the grid still covers the 256 CUs
-    bool big = (int64_t) ((M + 255) / 256) * (N / 256) >= 512 && N % 256 == 0;
-    if (Q2A_GEMM_TILE == 1 && N % 256 == 0) big = true;
-    if (Q2A_GEMM_TILE == 2) big = false;
-    return big;
+    return (int64_t) ((M + 255) / 256) * (N / 256) >= 512 && N % 256 == 0;
 }
-
-bool pipe8_enabled() { return Q2A_GEMM_PIPE != 0; }
-
-// Q2A_GEMM_TAIL (compile time): 1 = partial last round of an 8-phase grid on 128x128 tiles (product), 0 = off,
-// 2 = on the two-stage 128x256 (Q4_K) / 256x256 tiles (diagnostic), 3 = on the 64x128 deep-pipeline tiles at every K
-// (diagnostic)
-#ifndef Q2A_GEMM_TAIL
-#define Q2A_GEMM_TAIL 1
-#endif
 
 // compute units of the current device, cached per device ordinal
 int cu_count() {
@@ -2187,7 +1731,7 @@ int cu_count() {
 // than the second launch and the 128x128 tiles' lower rate.
 template <int EPI, int BLK>
 hipError_t launch_pipe8(const q2a_gemm_args & a, hipStream_t s) {
-    if constexpr (Q2A_GEMM_PERSIST && EPI == Q2A_EPI_PRE_H && BLK == 256) {
+    if constexpr (EPI == Q2A_EPI_PRE_H && BLK == 256) {
         // persistent tiles (k_gemm PIPE = 2): whole 256-row tiles only, at least two Q4_K blocks
         const int cus = cu_count();
         const int ntl = (a.N / 256) * ((a.M - a.m_base) / 256);
@@ -2198,23 +1742,19 @@ hipError_t launch_pipe8(const q2a_gemm_args & a, hipStream_t s) {
             return hipGetLastError();
         }
     }
-    constexpr bool TAILABLE = Q2A_GEMM_TAIL && (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_PRE_H || EPI == Q2A_EPI_GELU_H);
+    constexpr bool TAILABLE = (EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_PRE_H || EPI == Q2A_EPI_GELU_H);
     if constexpr (TAILABLE) {
         const int cus = cu_count();
         const int nbn = a.N / 256, nbm = (a.M - a.m_base + 255) / 256;
         const int64_t ntl = (int64_t) nbn * nbm, rem = cus > 0 ? ntl % cus : 0;
         const int m_main = (int) ((ntl - rem) / nbn);   // whole M-tiles inside the full rounds
-        if ((Q2A_GEMM_TAIL == 3 || a.K >= 4096) && a.m_base == 0 && rem > 0 && rem * 8 <= (int64_t) cus * 5 && m_main > 0 && m_main < nbm) {
+        if (a.K >= 4096 && a.m_base == 0 && rem > 0 && rem * 8 <= (int64_t) cus * 5 && m_main > 0 && m_main < nbm) {
             q2a_gemm_args h = a;
             h.M = m_main * 256;
             const hipError_t err = launch_cfg<256, 256, 2, 4, EPI, BLK, 1>(h, s);
             if (err != hipSuccess) return err;
             q2a_gemm_args t = a;
             t.m_base = m_main * 256;
-            if constexpr (Q2A_GEMM_TAIL == 3)   // diagnostic: the deep-pipeline 64x128 tiles, every K
-                return launch_cfg<64, 128, 2, 2, EPI, BLK>(t, s);
-            if constexpr (Q2A_GEMM_TAIL == 2)   // diagnostic: the two-stage wide tiles (one workgroup per CU)
-                return BLK == 256 ? launch_cfg<128, 256, 2, 4, EPI, BLK>(t, s) : launch_cfg<256, 256, 2, 4, EPI, BLK>(t, s);
             return launch_cfg<128, 128, 2, 2, EPI, BLK>(t, s);
         }
     }
@@ -2223,7 +1763,7 @@ hipError_t launch_pipe8(const q2a_gemm_args & a, hipStream_t s) {
 
 // the 8-phase kernels: 256x256 tiles, 32-bit operand offsets, K-steps in pairs (fp16) or whole Q4_K blocks
 bool pipe8_ok(const q2a_gemm_args & a, int blk) {
-    if (!pipe8_enabled() || !wide_tiles(a.M, a.N)) return false;
+    if (!wide_tiles(a.M, a.N)) return false;
     const int64_t last = (int64_t) ((a.M - 1) / a.a_rpg) * a.a_gstride + (int64_t) ((a.M - 1) % a.a_rpg) * a.a_step;
     if ((last + 1) * a.lda >= (1ll << 32) || (int64_t) a.N * a.ldw >= (1ll << 32)) return false;
     if (blk == 0 || blk == Q2A_BLK_BF16) return (a.K / BK) % 2 == 0;
@@ -2245,32 +1785,29 @@ hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
         const bool narrow = !big && narrow_tiles(a.M, a.N) && a.ksplit <= 1 && a.ngroup != 2;
         if (blk == 0) {
             if (p8) return launch_pipe8<EPI, 0>(a, s);
-            if (narrow) return launch_cfg<64, 128, Q2A_GEMM_NARROW_WM, 2, EPI, 0>(a, s);
-            return big ? launch_cfg<256, 256, 2, 4, EPI, 0>(a, s) : launch_cfg<128, 128, Q2A_GEMM_SMALL_WM, 2, EPI, 0>(a, s);
+            if (narrow) return launch_cfg<64, 128, 4, 2, EPI, 0>(a, s);
+            return big ? launch_cfg<256, 256, 2, 4, EPI, 0>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 0>(a, s);
         }
         if constexpr (EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_CONV2 || EPI == Q2A_EPI_STORE_F) {
             // the conv GEMMs' exact accumulation: 64x128 tiles in every regime (one K order, batch invariant)
-            if (blk == Q2A_BLK_EXACT) {
-                if (Q2A_GEMM_EXACT_TILE) return launch_cfg<128, 128, 2, 2, EPI, Q2A_BLK_EXACT>(a, s);
-                return launch_cfg<64, 128, 2, 2, EPI, Q2A_BLK_EXACT>(a, s);
-            }
+            if (blk == Q2A_BLK_EXACT) return launch_cfg<64, 128, 2, 2, EPI, Q2A_BLK_EXACT>(a, s);
         }
         if (blk == 256) {
             if (!a.beta || !a.gamma) return hipErrorInvalidValue;   // the block recurrence needs beta / gamma
             if (p8) return launch_pipe8<EPI, 256>(a, s);
-            if (narrow) return launch_cfg<64, 128, Q2A_GEMM_NARROW_WM, 2, EPI, 256>(a, s);
-            return big ? launch_cfg<128, 256, 2, 4, EPI, 256>(a, s) : launch_cfg<128, 128, Q2A_GEMM_SMALL_WM, 2, EPI, 256>(a, s);
+            if (narrow) return launch_cfg<64, 128, 4, 2, EPI, 256>(a, s);
+            return big ? launch_cfg<128, 256, 2, 4, EPI, 256>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 256>(a, s);
         }
         if (blk == 32) {
-            if (narrow) return launch_cfg<64, 128, Q2A_GEMM_NARROW_WM, 2, EPI, 32>(a, s);
-            return big ? launch_cfg<128, 256, 2, 4, EPI, 32>(a, s) : launch_cfg<128, 128, Q2A_GEMM_SMALL_WM, 2, EPI, 32>(a, s);
+            if (narrow) return launch_cfg<64, 128, 4, 2, EPI, 32>(a, s);
+            return big ? launch_cfg<128, 256, 2, 4, EPI, 32>(a, s) : launch_cfg<128, 128, 2, 2, EPI, 32>(a, s);
         }
         if constexpr (EPI == Q2A_EPI_QKV || EPI == Q2A_EPI_RESID || EPI == Q2A_EPI_GELU_H || EPI == Q2A_EPI_STORE_F) {
             if (blk == Q2A_BLK_BF16) {
                 constexpr int B16 = Q2A_BLK_BF16;
                 if (p8) return launch_pipe8<EPI, B16>(a, s);
-                if (narrow) return launch_cfg<64, 128, Q2A_GEMM_NARROW_WM, 2, EPI, B16>(a, s);
-                return big ? launch_cfg<256, 256, 2, 4, EPI, B16>(a, s) : launch_cfg<128, 128, Q2A_GEMM_SMALL_WM, 2, EPI, B16>(a, s);
+                if (narrow) return launch_cfg<64, 128, 4, 2, EPI, B16>(a, s);
+                return big ? launch_cfg<256, 256, 2, 4, EPI, B16>(a, s) : launch_cfg<128, 128, 2, 2, EPI, B16>(a, s);
             }
         }
         return hipErrorInvalidValue;
@@ -2279,14 +1816,11 @@ hipError_t launch_epi(const q2a_gemm_args & a, int blk, hipStream_t s) {
 
 }  // namespace
 
-// Split-K of the small-tile residual GEMMs: compiled out of the product library (diagnostic builds only:
-// -DQ2A_GEMM_SPLITK=1). Partial sums combined across splits change the fp32 summation order, so a clip's output would
+// Split-K of the small-tile residual GEMMs: off in the product library (round 1's single-clip form, kept for the
+// q2a_test_* entry points' ksplit argument). Partial sums combined across splits change the fp32 summation order, so a clip's output would
 // depend on whether its batch took the small-tile or the 8-phase regime; without it every regime sums K identically
 // (batch invariance).
-#ifndef Q2A_GEMM_SPLITK
-#define Q2A_GEMM_SPLITK 0
-#endif
-static bool splitk_on() { return Q2A_GEMM_SPLITK != 0; }
+static bool splitk_on() { return false; }
 
 int q2a_gemm_resid_ksplit(int M, int N, int K, int blk) {
     if (!splitk_on() || !(blk == 0 || blk == Q2A_BLK_BF16) || wide_tiles(M, N) || N % 128) return 0;
@@ -2308,8 +1842,6 @@ int q2a_gemm_kq_ksplit(int M, int N, int K, int blk) {
 hipError_t q2a_launch_gemm(const q2a_gemm_args & a_in, int epi, int blk, hipStream_t s) {
     q2a_gemm_args a = a_in;
     a.m_base = 0;
-    a.stagger_ns = Q2A_GEMM_STAGGER_NS; a.stagger_g = std::max(1, Q2A_GEMM_STAGGER_G);
-    a.group_m = Q2A_GEMM_GROUP_M;
     if (a.ngroup == 2 && (epi != Q2A_EPI_STORE_F || (blk != 0 && blk != 256) || wide_tiles(a.M, a.N))) return hipErrorInvalidValue;
     if (a.ngroup == 2 && blk == 256 && (!a.dx2 || !a.beta2 || !a.gamma2 || !a.wext2)) return hipErrorInvalidValue;
     if (!(epi == Q2A_EPI_RESID || (epi == Q2A_EPI_STORE_F && a.split_store)) || !a.part || a.ldo != a.N || a.ngroup == 2)

@@ -77,8 +77,6 @@ struct q2a_gemm_args {
     int ksplit;
     float * part;
     int64_t split_stride;
-    int group_m;                      // rasterisation group (M-tiles per N column); 0 = default (Q2A_GEMM_GROUP_M)
-    int stagger_ns, stagger_g;        // diagnostic (Q2A_GEMM_STAGGER_NS/_G): first-round phase offsets per CU group
     int dy_ld;                        // row stride of dy/aext (M rounded up to 256)
     // ggml-backend fusions (ggml-q2a.hip): MUL_MAT -> ADD(bias) [-> ADD(residual)] on the f32 epilogues
     const float * resid;              // Q2A_EPI_RESID: residual rows [M][ldo] (null = outF itself, in place)
