@@ -29,6 +29,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -566,6 +567,7 @@ struct q2a_device_ctx {
     std::mutex mu;
     std::vector<packed_w> wcache;
     uint64_t wgen = 0;                 // bumped whenever a packed weight is evicted (captured graphs hold its pointer)
+    std::atomic<int> n_captured{0};    // HIP graphs instantiated by the backends of this device so far
     uint16_t * gelu_tab = nullptr;     // device copy of the 64 Ki-entry fp16 GELU table (lazy)
 };
 
@@ -1475,8 +1477,9 @@ packed_w get_qkv_weight(q2a_backend_ctx * b, const ggml_tensor * const w[3]) {
     Q2A_HIP(hipStreamSynchronize(b->stream));
     std::lock_guard<std::mutex> lk(d->mu);
     // the per-tensor images of Q, K and V (upload-time or lazy repacks) are not read again while the fused route is on:
-    // released, so the expanded QKV weights are resident once (a graph that still needed one repacks it lazily; the
-    // wgen bump keeps every captured graph that holds their pointers from being replayed)
+    // released, so the expanded QKV weights are resident once (a graph that still needed one repacks it lazily; once any
+    // graph has been captured on the device, the wgen bump keeps those that may hold their pointers from being replayed —
+    // before that, nothing holds them and the capture schedule stays as it was)
     for (size_t j = 0; j < d->wcache.size();) {
         const packed_w & c = d->wcache[j];
         bool own = false;
@@ -1484,7 +1487,7 @@ packed_w get_qkv_weight(q2a_backend_ctx * b, const ggml_tensor * const w[3]) {
             own |= c.raw == (const char *) w[i]->data && c.type == w[i]->type && c.N == N && c.K == K;
         if (own) {
             (void) hipFree(c.dev);
-            ++d->wgen;
+            if (d->n_captured.load() > 0) ++d->wgen;
             d->wcache[j] = d->wcache.back();
             d->wcache.pop_back();
         } else {
@@ -2194,6 +2197,7 @@ ggml_status graph_compute(ggml_backend_t backend, ggml_cgraph * g) {
                 (void) hipGraphDestroy(graph);
                 c->exec = exec;
                 c->stats = b->stats;
+                ++d->n_captured;
                 if (hipGraphLaunch(exec, b->stream) == hipSuccess) return GGML_STATUS_SUCCESS;
                 (void) hipGraphExecDestroy(exec);
                 c->exec = nullptr;

@@ -808,9 +808,17 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                          "+v"(b4[1]), "+v"(b4[2]), "+v"(b4[3]), "+v"(yc[0]), "+v"(yc[1]), "+v"(yc[2]), "+v"(yc[3]),
                          "+v"(yc[4]), "+v"(yc[5]), "+v"(yc[6]), "+v"(yc[7]));
             typedef _Float16 h4p __attribute__((ext_vector_type(4)));
+            // whole 128-B output lines per store: a 16-row block's wave columns (64 fp16 = one line per row) leave as two
+            // stores of 8 rows x 8 lanes x 16 B instead of two of 16 rows x 64 B. Register moves only (VALU, no LDS):
+            //   1. v_permlane16_swap pairs lanes q, q^1 (rows of 16 lanes): lane (q, l) then holds 16 B of row l for
+            //      each column-tile pair jp, chunk c = 2 (q & 1) + (q >> 1) (+ 4 jp) of the row's eight 16-B chunks;
+            //   2. DPP row_ror:8 pairs lanes l, l ^ 8: the lower half keeps chunk c of its row and takes chunk c + 4 of
+            //      row l + 8 (store B), the upper half the other way round (store A) — every row's 8 chunks in one store
+            const int hi8 = l16 >> 3;
+            const int colw = tn0 + wn * 64 + pcol + 32 * hi8;
 #pragma unroll
             for (int i = 0; i < 8; ++i) {
-                q2a_half * orow = p.outH + (int64_t) (tm0 + wm * 128 + i * 16 + l16) * p.ldo + tn0 + wn * 64 + pcol;
+                uint32_t hv[2][4];   // (scalars, not uint4: a lane-varying select of a uint4 array element went to scratch)
 #pragma unroll
                 for (int jp = 0; jp < 2; ++jp) {
                     h4p ha, hb;
@@ -825,14 +833,25 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                     uint2 ua, ub;
                     __builtin_memcpy(&ua, &ha, 8);
                     __builtin_memcpy(&ub, &hb, 8);
-                    const bool odd = q & 1;
-                    const uint2 send = odd ? ua : ub;
-                    uint2 recv;
-                    recv.x = __shfl_xor(send.x, 16, 64);
-                    recv.y = __shfl_xor(send.y, 16, 64);
-                    const uint4 hv = odd ? make_uint4(recv.x, recv.y, ub.x, ub.y) : make_uint4(ua.x, ua.y, recv.x, recv.y);
-                    if (Q2A_ST) q2a_st(hv, (uint4 *) (orow + 32 * jp));
+                    // odd rows of ua <-> even rows of ub: (ua, ub) is then this lane's 8 consecutive columns
+                    const auto rx = __builtin_amdgcn_permlane16_swap(ua.x, ub.x, false, false);
+                    const auto ry = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
+                    hv[jp][0] = rx[0]; hv[jp][1] = ry[0]; hv[jp][2] = rx[1]; hv[jp][3] = ry[1];
                 }
+                // lanes l < 8 send their jp = 1 piece to lane l + 8, lanes l >= 8 their jp = 0 piece to lane l - 8
+                uint32_t sa4[4], sb4[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t snd = hi8 ? hv[0][k] : hv[1][k];
+                    const uint32_t rcv = (uint32_t) __builtin_amdgcn_mov_dpp((int) snd, 0x128, 0xF, 0xF, false);   // row_ror:8
+                    sa4[k] = hi8 ? rcv : hv[0][k];   // rows 16 i + (l & 7): chunk c (l < 8) / c + 4 (l >= 8)
+                    sb4[k] = hi8 ? hv[1][k] : rcv;   // rows 16 i + 8 + (l & 7)
+                }
+                const uint4 sa = make_uint4(sa4[0], sa4[1], sa4[2], sa4[3]);
+                const uint4 sb = make_uint4(sb4[0], sb4[1], sb4[2], sb4[3]);
+                q2a_half * o0 = p.outH + (int64_t) (tm0 + wm * 128 + i * 16 + (l16 & 7)) * p.ldo + colw;
+                if (Q2A_ST) q2a_st(sa, (uint4 *) o0);
+                if (Q2A_ST) q2a_st(sb, (uint4 *) (o0 + 8 * p.ldo));
             }
             // (no reset: the next tile's block-0 start writes every accumulator, kq_first2)
         };
