@@ -437,13 +437,20 @@ def main():
         step()
     torch.cuda.synchronize()
     lib = q2a.lib()
-    # inside the timed region HIP events bracket only the roofline candidates (the matrix-core classes: QKV, attention,
-    # O, fc1, fc2 = Q2A_PROF_* 4, 5, 7, 8, 9) on the engine's stream; the per-kernel breakdown of every class comes from
-    # a separate fully-profiled pass after it
     lib.q2a_profile_enable_mask.argtypes = [C.c_void_p, C.c_uint]
-    lib.q2a_profile_enable_mask(C.c_void_p(eng.h), sum(1 << i for i in ROOF_CLASSES))
     prof_ms = (C.c_double * 11)()
     prof_n = (C.c_int64 * 11)()
+    # the dominant matrix-core class (QKV, attention, O, fc1, fc2 = Q2A_PROF_* 4, 5, 7, 8, 9) from one profiled step
+    # before the timed region; inside the timed region HIP events bracket only that class's launches (on the stream
+    # the kernels run on: an event pair costs ~7 us of GPU time per launch, 0.2 ms per step at one clip for one class);
+    # the per-kernel breakdown of every class comes from a separate fully-profiled pass after it
+    lib.q2a_profile_enable_mask(C.c_void_p(eng.h), sum(1 << i for i in ROOF_CLASSES))
+    lib.q2a_profile_read(C.c_void_p(eng.h), prof_ms, prof_n, 11, 1)
+    step()
+    torch.cuda.synchronize()
+    lib.q2a_profile_read(C.c_void_p(eng.h), prof_ms, prof_n, 11, 1)
+    dominant = max(ROOF_CLASSES, key=lambda i: prof_ms[i])
+    lib.q2a_profile_enable_mask(C.c_void_p(eng.h), 1 << dominant)
     lib.q2a_profile_read(C.c_void_p(eng.h), prof_ms, prof_n, 11, 1)
 
     if dist is not None:
@@ -541,14 +548,19 @@ def main():
                 per_kernel[PROF_NAMES[i]].update({"issued_tflops": round(3 * tf, 1),
                                                   "issued_mfma_frac": round(3 * tf / PEAK_FP16_MFMA_TFLOPS, 4)})
 
-    # the roofline objects: the DOMINANT kernel class (largest time per step in the breakdown pass among the matrix-core
-    # classes, each one launch per layer) and the fc1 GEMM (north_star's "Q4_K encoder matmuls"), each from its own
-    # events over the timed region
-    dominant = max(ROOF_CLASSES, key=lambda i: prof_ms[i])
+    # the roofline objects: the DOMINANT kernel class (largest time per step among the matrix-core classes, each one
+    # launch per layer; its events over the timed region) and the fc1 GEMM (north_star's "Q4_K encoder matmuls"; its
+    # events of the breakdown pass unless it is the dominant class)
     roofline = roofline_of(dominant, timed_ms, timed_n, args.config, wt, bf16, clips_per_gpu)
     roofline["dominant"] = True
+    roofline["avg_launch_source"] = "HIP events on the launch stream over the timed region"
     roofline["share_of_step"] = round(prof_ms[dominant] / brk_steps / (elapsed / args.steps * 1e3), 4)
-    roofline_fc1 = roofline_of(8, timed_ms, timed_n, args.config, wt, bf16, clips_per_gpu)
+    if dominant == 8:
+        roofline_fc1 = dict(roofline)
+    else:
+        roofline_fc1 = roofline_of(8, list(prof_ms), list(prof_n), args.config, wt, bf16, clips_per_gpu)
+        roofline_fc1["avg_launch_source"] = "HIP events of the breakdown pass"
+    roofline_fc1.pop("dominant", None)
     roofline_fc1["all_weight_gemms_tflops"] = round(gemm_tf, 1)
 
     cpu = None

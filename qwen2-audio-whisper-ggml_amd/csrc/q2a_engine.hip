@@ -544,20 +544,6 @@ __global__ void k_split_hilo(const float * x, q2a_half * hi, q2a_half * lo, int6
     lo[i] = (_Float16) (v - (float) h);
 }
 
-// V [clips*T][D] f32 -> V^T [clip][head][d][TP] fp16, and its lo image fp16(v - fp16(v)) when vtl is set
-__global__ void k_to_vt(const float * v, q2a_half * vt, q2a_half * vtl, int clips, int T, int H, int TP) {
-    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
-    const int64_t D = (int64_t) H * 64;
-    if (i >= (int64_t) clips * T * D) return;
-    const int64_t m = i / D;
-    const int c = (int) (i % D);
-    const int clip = (int) (m / T), t = (int) (m % T);
-    const int64_t o = (((int64_t) clip * H + c / 64) * 64 + (c % 64)) * TP + t;
-    const _Float16 h = (_Float16) v[i];
-    vt[o] = h;
-    if (vtl) vtl[o] = (_Float16) (v[i] - (float) h);
-}
-
 __global__ void k_to_half(const float * x, q2a_half * y, int64_t n) {
     const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) y[i] = (_Float16) x[i];
@@ -797,31 +783,12 @@ struct q2a_engine {
 
 namespace {
 
-// A NULL `stream` argument of the device-pointer entry points (q2a_encode_device*, q2a_test_*, q2a_projector_apply):
-// the work runs on the handle's own non-blocking stream, ordered as if it had been issued on the caller's legacy
-// default stream (stream 0, torch's default stream): it starts after everything already queued there, and everything
-// queued there afterwards starts after it. Inputs written and outputs read on stream 0 need no extra synchronisation.
-struct null_stream_order {
-    hipStream_t own;
-    hipEvent_t ev = nullptr;
-    null_stream_order(const void * stream, hipStream_t own_stream) : own(own_stream) {
-        if (stream) return;
-        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
-            (void) hipGetLastError();
-            ev = nullptr;
-            (void) hipDeviceSynchronize();   // (no event: order by draining instead)
-            return;
-        }
-        (void) hipEventRecord(ev, 0);
-        (void) hipStreamWaitEvent(own, ev, 0);
-    }
-    ~null_stream_order() {
-        if (!ev) return;
-        (void) hipEventRecord(ev, own);
-        (void) hipStreamWaitEvent(0, ev, 0);
-        (void) hipEventDestroy(ev);
-    }
-};
+// A NULL `stream` argument of the device-pointer entry points (q2a_encode_device*, q2a_test_*, q2a_projector_apply)
+// means the caller's legacy default stream (stream 0, torch's default stream): the work is issued ON it, so it starts
+// after everything already queued there and everything queued there afterwards starts after it; inputs written and
+// outputs read on stream 0 need no extra synchronisation. (Round 5 ran it on the handle's own stream between two
+// cross-stream events: 0.2 ms per encode at one clip, diag/null_stream_ab.py, profiles/r06e_null_stream.jsonl.)
+inline hipStream_t call_stream(const void * stream) { return (hipStream_t) stream; }
 
 int engine_init(q2a_engine * e, int device) {
     int n = 0;
@@ -905,7 +872,7 @@ int ensure_host_bufs(q2a_engine * e, int clips, int64_t maxn) {
 int reserve(q2a_engine * e, int B) {
     if (B <= e->cap_clips) return Q2A_OK;
     HIP_TRY(hipSetDevice(e->device));
-    HIP_TRY(hipStreamSynchronize(e->stream));
+    HIP_TRY(hipDeviceSynchronize());   // earlier calls may have run on any caller stream (or stream 0)
     if (e->ws) { (void) hipFree(e->ws); e->ws = nullptr; }
     if (e->meta_host) { (void) hipHostFree(e->meta_host); e->meta_host = nullptr; }
     const dims & d = e->d;
@@ -1055,6 +1022,7 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
         q2a_gemm_args a = gemm_base(e, l, 0, e->actD, M);
         a.bias = e->lv<const float *>(l, L_BQKV);
         a.qh = e->qh; a.ql = e->ql; a.kh = e->kh; a.kl = e->kl; a.vt = e->vt; a.vtl = e->vtl;
+        a.v_rows = e->bf16 ? 0 : 1;   // reference contract: V hi / lo row-major like K (bf16 contract: V^T)
         // ggml_scale(Q, 1/sqrt(dh)) (:2054); the reference-contract attention also wants log2(e) folded in (its
         // softmax runs in log2 units): one f32 multiply by fl(log2 e)/8, 2^-3 being exact
         a.qscale = (1.0f / sqrtf((float) (d.D / d.H))) * (e->bf16 ? 1.0f : Q2A_LOG2E);
@@ -1063,6 +1031,7 @@ int run_block(q2a_engine * e, int l, int B, hipStream_t s) {
     {
         q2a_attn_args at{e->qh, e->ql, e->kh, e->kl, e->vt, B, d.T, d.D, d.H, e->TP, nullptr, nullptr, e->bf16 ? 1 : 0};
         at.vtl = e->vtl;
+        at.v_rows = e->bf16 ? 0 : 1;
         if (mode == 0 || mode == 4) at.outH = e->actD; else at.outF = e->attF;
         PLAUNCH(e, s, Q2A_PROF_ATTN, q2a_launch_attention(at, s));
         if (mode == 3) {
@@ -1375,7 +1344,7 @@ int q2a_set_force_encode(q2a_engine * e, int on) {
 void q2a_close(q2a_engine * e) {
     if (!e) return;
     (void) hipSetDevice(e->device);
-    if (e->stream) (void) hipStreamSynchronize(e->stream);
+    (void) hipDeviceSynchronize();   // (calls may have run on caller streams or stream 0, not only e->stream)
     free_host_bufs(e);
     free_ws(e);
     for (auto & r : e->pending) { (void) hipEventDestroy(r.a); (void) hipEventDestroy(r.b); }
@@ -1407,8 +1376,7 @@ int q2a_encode_device(q2a_engine * e, const float * pcm_dev, int64_t pcm_stride,
                       int n_clips, int offset_ms, float * out_dev, int32_t * status, void * stream) {
     if (!e) return Q2A_ERR_ARG;
     HIP_TRY(hipSetDevice(e->device));
-    hipStream_t s = stream ? (hipStream_t) stream : e->stream;
-    null_stream_order nso(stream, s);
+    hipStream_t s = call_stream(stream);
     return encode_impl(e, pcm_dev, pcm_stride, n_samples, n_clips, offset_ms, nullptr, out_dev, status, s);
 }
 
@@ -1416,8 +1384,7 @@ int q2a_encode_device_ex(q2a_engine * e, const float * pcm_dev, int64_t pcm_stri
                          const int32_t * offsets_ms, int n_clips, float * out_dev, int32_t * status, void * stream) {
     if (!e || !offsets_ms) { set_err("invalid arguments"); return Q2A_ERR_ARG; }
     HIP_TRY(hipSetDevice(e->device));
-    hipStream_t s = stream ? (hipStream_t) stream : e->stream;
-    null_stream_order nso(stream, s);
+    hipStream_t s = call_stream(stream);
     return encode_impl(e, pcm_dev, pcm_stride, n_samples, n_clips, 0, offsets_ms, out_dev, status, s);
 }
 
@@ -1591,8 +1558,7 @@ int q2a_profile_read(q2a_engine * e, double * ms, int64_t * counts, int n, int r
 int q2a_test_linear(q2a_engine * e, int layer, int which, const float * x, int M, float * y, void * stream) {
     if (!e || layer < 0 || layer >= e->d.L || which < 0 || which > 3 || M <= 0) return Q2A_ERR_ARG;
     HIP_TRY(hipSetDevice(e->device));
-    hipStream_t s = stream ? (hipStream_t) stream : e->stream;
-    null_stream_order nso(stream, s);
+    hipStream_t s = call_stream(stream);
     const dims & d = e->d;
     int rc = reserve(e, (M + d.T - 1) / d.T);
     if (rc) return rc;
@@ -1622,8 +1588,7 @@ int q2a_test_linear(q2a_engine * e, int layer, int which, const float * x, int M
 int q2a_test_block(q2a_engine * e, int layer, float * x, int n_clips, void * stream) {
     if (!e || layer < 0 || layer >= e->d.L || n_clips <= 0) return Q2A_ERR_ARG;
     HIP_TRY(hipSetDevice(e->device));
-    hipStream_t s = stream ? (hipStream_t) stream : e->stream;
-    null_stream_order nso(stream, s);
+    hipStream_t s = call_stream(stream);
     int rc = reserve(e, n_clips);
     if (rc) return rc;
     const size_t bytes = (size_t) n_clips * e->d.T * e->d.D * 4;
@@ -1646,8 +1611,7 @@ int q2a_test_frontend(q2a_engine * e, const float * pcm_dev, int64_t pcm_stride,
                       float * x_dev, void * stream) {
     if (!e || !pcm_dev || !n_samples || !x_dev || n_clips <= 0) return Q2A_ERR_ARG;
     HIP_TRY(hipSetDevice(e->device));
-    hipStream_t s = stream ? (hipStream_t) stream : e->stream;
-    null_stream_order nso(stream, s);
+    hipStream_t s = call_stream(stream);
     int rc = reserve(e, n_clips);
     if (rc) return rc;
     int max_frames = 0;
@@ -1662,8 +1626,7 @@ int q2a_test_frontend(q2a_engine * e, const float * pcm_dev, int64_t pcm_stride,
 int q2a_test_pool_ln(q2a_engine * e, const float * x_dev, int n_clips, float * out_dev, void * stream) {
     if (!e || !x_dev || !out_dev || n_clips <= 0) return Q2A_ERR_ARG;
     HIP_TRY(hipSetDevice(e->device));
-    hipStream_t s = stream ? (hipStream_t) stream : e->stream;
-    null_stream_order nso(stream, s);
+    hipStream_t s = call_stream(stream);
     int rc = reserve(e, n_clips);
     if (rc) return rc;
     HIP_TRY(hipEventSynchronize(e->meta_evt));
@@ -1687,8 +1650,7 @@ int q2a_test_attention(q2a_engine * e, const float * q, const float * k, const f
                        void * stream) {
     if (!e || n_clips <= 0) return Q2A_ERR_ARG;
     HIP_TRY(hipSetDevice(e->device));
-    hipStream_t s = stream ? (hipStream_t) stream : e->stream;
-    null_stream_order nso(stream, s);
+    hipStream_t s = call_stream(stream);
     int rc = reserve(e, n_clips);
     if (rc) return rc;
     const dims & d = e->d;
@@ -1696,10 +1658,11 @@ int q2a_test_attention(q2a_engine * e, const float * q, const float * k, const f
     const dim3 g((unsigned) ((n + 255) / 256)), b(256);
     hipLaunchKernelGGL(k_split_hilo, g, b, 0, s, q, e->qh, e->ql, n, Q2A_LOG2E);   // the kernel's log2 units
     hipLaunchKernelGGL(k_split_hilo, g, b, 0, s, k, e->kh, e->kl, n, 1.0f);
-    hipLaunchKernelGGL(k_to_vt, g, b, 0, s, v, e->vt, e->vtl, n_clips, d.T, d.H, e->TP);
+    hipLaunchKernelGGL(k_split_hilo, g, b, 0, s, v, e->vt, e->vtl, n, 1.0f);   // V hi / lo row-major (the engine's layout)
     LAUNCH(hipGetLastError());
     q2a_attn_args at{e->qh, e->ql, e->kh, e->kl, e->vt, n_clips, d.T, d.D, d.H, e->TP, nullptr, out};
     at.vtl = e->vtl;
+    at.v_rows = 1;
     LAUNCH(q2a_launch_attention(at, s));
     return Q2A_OK;
 }
@@ -1787,8 +1750,7 @@ int q2a_projector_get_dims(const q2a_projector * p, int * d_in, int * d_out, int
 int q2a_projector_apply(q2a_projector * p, const float * x, int64_t rows, float * y, void * stream) {
     if (!p || !x || !y || rows <= 0 || rows > (1 << 30) / 4) return Q2A_ERR_ARG;
     HIP_TRY(hipSetDevice(p->device));
-    hipStream_t s = stream ? (hipStream_t) stream : p->stream;
-    null_stream_order nso(stream, s);
+    hipStream_t s = call_stream(stream);
     const int M = (int) rows, K = p->d_in, N = p->d_out, blk = p->blk;
     const int64_t MP = (rows + 255) / 256 * 256;
     const size_t a_bytes = ((size_t) M * K * 2 + 255) & ~size_t(255);

@@ -226,7 +226,8 @@ constexpr int ALPHA_OFF = 24 * 1024;        //   + alpha = dy_{b-1}/dy_b per til
 // vmcnt waits are raised by S_EPI, so nothing drains between tiles.
 constexpr int FIN_OFF = SBUF_OFF + 21 * 1024;   // dy_last | dx_last | bias of the finishing tile (persistent form): the
                                                 //   three pad pieces' slots, which every other block fills with dummies
-constexpr int S_EPI = 16;                        // global stores per wave of the persistent epilogue
+// (S_EPI = 16 * PERS global stores per wave of the persistent epilogue: 16 for fc1's fp16 pre-activation, 32 for the
+// Q|K|V hi and lo images)
 struct no_tiles {
     __device__ bool operator()(int &, int &) const { return false; }
 };
@@ -543,6 +544,8 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
         Q2A_KSTEP(1, stage_tail(0, 1), stage_tail(1, 0), stage_tail(1, 2), stage_tail(1, 3), 10, 10, 10, 10);
     } else if constexpr (PERS) {
         static_assert(BLK == 256, "persistent 8-phase loop: Q4_K only");
+        constexpr int S_EPI = 16 * PERS;
+        static_assert(13 + S_EPI < 64, "vmcnt immediate range");
         // every tile's block 0 runs with its first five waits raised by S_EPI (the previous tile's epilogue stores sit
         // between its phase 0 and phase 1); for the first tile nothing is there, so the prologue drains its loads
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -562,8 +565,8 @@ __device__ __forceinline__ void mainloop_8phase(const q2a_gemm_args & p, f4 (&ac
             BS_T1();
             asm volatile("" ::: "memory");
             Q2A_KSTEP(0, stage(1, 1, kt + 1), (stage(0, 0, kt + 2), stage_scales(kt / 4 + 1)), stage(0, 2, kt + 2),
-                      stage(0, 3, kt + 2), 26, 29, 29, 29);
-            Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 29, 13, 10, 10);
+                      stage(0, 3, kt + 2), 10 + S_EPI, 13 + S_EPI, 13 + S_EPI, 13 + S_EPI);
+            Q2A_KSTEP(1, stage(0, 1, kt + 2), stage(1, 0, kt + 3), stage(1, 2, kt + 3), stage(1, 3, kt + 3), 13 + S_EPI, 13, 10, 10);
             Q2A_KSTEP(0, (alpha_compute(), stage(1, 1, kt + 3)), stage(0, 0, kt + 4), stage(0, 2, kt + 4), stage(0, 3, kt + 4),
                       10, 10, 10, 10);
             Q2A_KSTEP(1, stage(0, 1, kt + 4), stage(1, 0, kt + 5), stage(1, 2, kt + 5), stage(1, 3, kt + 5), 10, 10, 10, 10);
@@ -756,7 +759,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
         // persistent 8-phase tiles (launch_pipe8: fc1's pre-activation, M a multiple of 256, K >= 512): virtual
         // workgroup ids v = blockIdx.x + r * gridDim.x mapped exactly like the one-tile-per-workgroup grid (gridDim is
         // a multiple of 8, so v and blockIdx.x share an XCD), the pipeline runs across the tiles (mainloop_8phase PERS)
-        static_assert(EPI == Q2A_EPI_PRE_H && BLK == 256 && BM == 256 && BN == 256 && NW == 8, "persistent form: fc1 Q4_K");
+        static_assert((EPI == Q2A_EPI_PRE_H || EPI == Q2A_EPI_QKV) && BLK == 256 && BM == 256 && BN == 256 && NW == 8,
+                      "persistent form: Q4_K fc1 pre-activation / Q|K|V with row-major V");
+        constexpr bool QKV = EPI == Q2A_EPI_QKV;
         auto tile_at = [&](int v, int & tm0, int & tn0) {
             const int x8 = v & 7;
             const int w = (x8 < rr ? x8 * (qq + 1) : rr * (qq + 1) + (x8 - rr) * qq) + (v >> 3);
@@ -787,8 +792,16 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
             return true;
         };
         const uint32_t fin = (uint32_t) (uintptr_t) (const __attribute__((address_space(3))) char *) lds_raw + FIN_OFF;
-        // the finished tile: acc * (dy_last[m] * dx_last[n]) + bias[n] -> fp16 (the PIPE = 1 epilogue's operations,
-        // bit for bit), 16 B per lane after one lane exchange, straight from registers: S_EPI stores per wave
+        // the finished tile: acc * (dy_last[m] * dx_last[n]) + bias[n] (Q: * qscale) -> fp16 (the PIPE = 1 epilogues'
+        // operations, bit for bit), straight from registers: fc1 one image, Q|K|V the hi and the lo image
+        // (fp16(v - hi)) of the tile's part (256 | D: a tile lies in one of Q, K, V; V row-major, q2a_gemm_args.v_rows).
+        // Whole 128-B output lines per store: a 16-row block's wave columns (64 fp16 = one line per row) leave as two
+        // stores of 8 rows x 8 lanes x 16 B instead of two of 16 rows x 64 B. Register moves only (VALU, no LDS):
+        //   1. v_permlane16_swap pairs lanes q, q^1 (rows of 16 lanes): lane (q, l) then holds 16 B of row l for each
+        //      column-tile pair jp, chunk c = 2 (q & 1) + (q >> 1) (+ 4 jp) of the row's eight 16-B chunks;
+        //   2. DPP row_ror:8 pairs lanes l, l ^ 8: the lower half keeps chunk c of its row and takes chunk c + 4 of
+        //      row l + 8 (store B), the upper half the other way round (store A) — every row's 8 chunks in one store.
+        // Exactly S_EPI = 16 (fc1) / 32 (Q|K|V) stores per wave on every tile (M % 256 == 0: no row is skipped).
         auto epi = [&](f4 (&ac)[8][4], int tm0, int tn0) {
             const int ln = (int) __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));   // lane, rematerialised
             const int q = ln >> 4, l16 = ln & 15;
@@ -808,56 +821,71 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                          "+v"(b4[1]), "+v"(b4[2]), "+v"(b4[3]), "+v"(yc[0]), "+v"(yc[1]), "+v"(yc[2]), "+v"(yc[3]),
                          "+v"(yc[4]), "+v"(yc[5]), "+v"(yc[6]), "+v"(yc[7]));
             typedef _Float16 h4p __attribute__((ext_vector_type(4)));
-            // whole 128-B output lines per store: a 16-row block's wave columns (64 fp16 = one line per row) leave as two
-            // stores of 8 rows x 8 lanes x 16 B instead of two of 16 rows x 64 B. Register moves only (VALU, no LDS):
-            //   1. v_permlane16_swap pairs lanes q, q^1 (rows of 16 lanes): lane (q, l) then holds 16 B of row l for
-            //      each column-tile pair jp, chunk c = 2 (q & 1) + (q >> 1) (+ 4 jp) of the row's eight 16-B chunks;
-            //   2. DPP row_ror:8 pairs lanes l, l ^ 8: the lower half keeps chunk c of its row and takes chunk c + 4 of
-            //      row l + 8 (store B), the upper half the other way round (store A) — every row's 8 chunks in one store
             const int hi8 = l16 >> 3;
-            const int colw = tn0 + wn * 64 + pcol + 32 * hi8;
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                uint32_t hv[2][4];   // (scalars, not uint4: a lane-varying select of a uint4 array element went to scratch)
-#pragma unroll
-                for (int jp = 0; jp < 2; ++jp) {
-                    h4p ha, hb;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) {
-#pragma clang fp contract(off)
-                        const float va = kq_final(ac[i][2 * jp][r], yc[i], dx4[2 * jp][r]) + b4[2 * jp][r];
-                        const float vb = kq_final(ac[i][2 * jp + 1][r], yc[i], dx4[2 * jp + 1][r]) + b4[2 * jp + 1][r];
-                        ha[r] = (_Float16) va;
-                        hb[r] = (_Float16) vb;
-                    }
-                    uint2 ua, ub;
-                    __builtin_memcpy(&ua, &ha, 8);
-                    __builtin_memcpy(&ub, &hb, 8);
-                    // odd rows of ua <-> even rows of ub: (ua, ub) is then this lane's 8 consecutive columns
-                    const auto rx = __builtin_amdgcn_permlane16_swap(ua.x, ub.x, false, false);
-                    const auto ry = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
-                    hv[jp][0] = rx[0]; hv[jp][1] = ry[0]; hv[jp][2] = rx[1]; hv[jp][3] = ry[1];
-                }
-                // lanes l < 8 send their jp = 1 piece to lane l + 8, lanes l >= 8 their jp = 0 piece to lane l - 8
-                uint32_t sa4[4], sb4[4];
+            // destination images and column of this lane's 16-B piece (QKV: within the part's [M][D] rows)
+            const int part = QKV ? tn0 / p.D : 0;
+            q2a_half * dhi = QKV ? (part == 0 ? p.qh : part == 1 ? p.kh : p.vt) : p.outH;
+            q2a_half * dlo = QKV ? (part == 0 ? p.ql : part == 1 ? p.kl : p.vtl) : nullptr;
+            const int64_t ld = QKV ? p.D : p.ldo;
+            const int colw = tn0 - part * p.D + wn * 64 + pcol + 32 * hi8;
+            const float vsc = QKV && part == 0 ? p.qscale : 1.0f;
+            // one image's two 16-B pieces per lane (jp = 0, 1) -> stores A (rows 16i + (l & 7)) and B (+ 8)
+            auto store_lines = [&](uint32_t (&hv)[2][4], q2a_half * dst, int i) {
+                uint32_t sa4[4], sb4[4];   // (scalars, not uint4: a lane-varying select of a uint4 array went to scratch)
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
+                    // lanes l < 8 send their jp = 1 piece to lane l + 8, lanes l >= 8 their jp = 0 piece to lane l - 8
                     const uint32_t snd = hi8 ? hv[0][k] : hv[1][k];
                     const uint32_t rcv = (uint32_t) __builtin_amdgcn_mov_dpp((int) snd, 0x128, 0xF, 0xF, false);   // row_ror:8
                     sa4[k] = hi8 ? rcv : hv[0][k];   // rows 16 i + (l & 7): chunk c (l < 8) / c + 4 (l >= 8)
                     sb4[k] = hi8 ? hv[1][k] : rcv;   // rows 16 i + 8 + (l & 7)
                 }
-                const uint4 sa = make_uint4(sa4[0], sa4[1], sa4[2], sa4[3]);
-                const uint4 sb = make_uint4(sb4[0], sb4[1], sb4[2], sb4[3]);
-                q2a_half * o0 = p.outH + (int64_t) (tm0 + wm * 128 + i * 16 + (l16 & 7)) * p.ldo + colw;
-                if (Q2A_ST) q2a_st(sa, (uint4 *) o0);
-                if (Q2A_ST) q2a_st(sb, (uint4 *) (o0 + 8 * p.ldo));
+                q2a_half * o0 = dst + (int64_t) (tm0 + wm * 128 + i * 16 + (l16 & 7)) * ld + colw;
+                if (Q2A_ST) q2a_st(make_uint4(sa4[0], sa4[1], sa4[2], sa4[3]), (uint4 *) o0);
+                if (Q2A_ST) q2a_st(make_uint4(sb4[0], sb4[1], sb4[2], sb4[3]), (uint4 *) (o0 + 8 * ld));
+            };
+            auto pair_swap = [&](h4p ha, h4p hb, uint32_t (&out)[4]) {
+                uint2 ua, ub;
+                __builtin_memcpy(&ua, &ha, 8);
+                __builtin_memcpy(&ub, &hb, 8);
+                // odd rows of ua <-> even rows of ub: (ua, ub) is then this lane's 8 consecutive columns
+                const auto rx = __builtin_amdgcn_permlane16_swap(ua.x, ub.x, false, false);
+                const auto ry = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
+                out[0] = rx[0]; out[1] = ry[0]; out[2] = rx[1]; out[3] = ry[1];
+            };
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                uint32_t hv[2][4], lv[2][4];
+#pragma unroll
+                for (int jp = 0; jp < 2; ++jp) {
+                    h4p ha, hb, la, lb;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+#pragma clang fp contract(off)
+                        float va = kq_final(ac[i][2 * jp][r], yc[i], dx4[2 * jp][r]) + b4[2 * jp][r];
+                        float vb = kq_final(ac[i][2 * jp + 1][r], yc[i], dx4[2 * jp + 1][r]) + b4[2 * jp + 1][r];
+                        if (QKV) {   // ggml_scale after the bias add (exact 2^-3 times fl(log2 e): one rounding)
+                            va = va * vsc;
+                            vb = vb * vsc;
+                        }
+                        ha[r] = (_Float16) va;
+                        hb[r] = (_Float16) vb;
+                        if (QKV) {
+                            la[r] = (_Float16) (va - (float) ha[r]);
+                            lb[r] = (_Float16) (vb - (float) hb[r]);
+                        }
+                    }
+                    pair_swap(ha, hb, hv[jp]);
+                    if (QKV) pair_swap(la, lb, lv[jp]);
+                }
+                store_lines(hv, dhi, i);
+                if (QKV) store_lines(lv, dlo, i);
             }
             // (no reset: the next tile's block-0 start writes every accumulator, kq_first2)
         };
         Q2A_STAMP(ST, 0);
         Q2A_STAMP_RT(ST, 8);
-        mainloop_8phase<BLK, false, false, ST, 1>(p, acc, lds_raw, m0, n0, lane, wave, wm, wn, next, epi);
+        mainloop_8phase<BLK, false, false, ST, QKV ? 2 : 1>(p, acc, lds_raw, m0, n0, lane, wave, wm, wn, next, epi);
         Q2A_STAMP(ST, 6);
         Q2A_STAMP_RT(ST, 9);
         return;
@@ -1294,19 +1322,35 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     };
     typedef _Float16 h4v __attribute__((ext_vector_type(4)));
     // 8 fp16 = this lane's 16-B piece of columns [32 jp + 16 (q&1) + 8 (q>>1), +8) from chunks (a: tile 2jp, b: 2jp+1)
+    // (v_permlane16_swap: the odd 16-lane rows of a's words trade places with the even rows of b's, VALU only)
     auto pair16 = [&](h4v a, h4v b) -> uint4 {
         uint2 ua, ub;
         __builtin_memcpy(&ua, &a, 8);
         __builtin_memcpy(&ub, &b, 8);
-        const bool odd = q & 1;
-        const uint2 send = odd ? ua : ub;
-        uint2 recv;
-        recv.x = __shfl_xor(send.x, 16, 64);
-        recv.y = __shfl_xor(send.y, 16, 64);
-        return odd ? make_uint4(recv.x, recv.y, ub.x, ub.y) : make_uint4(ua.x, ua.y, recv.x, recv.y);
+        const auto rx = __builtin_amdgcn_permlane16_swap(ua.x, ub.x, false, false);
+        const auto ry = __builtin_amdgcn_permlane16_swap(ua.y, ub.y, false, false);
+        return make_uint4(rx[0], ry[0], rx[1], ry[1]);
+    };
+    // whole 128-B lines per store: x0 / x1 are this lane's 16-B pieces of row 16i + l16 for the two halves of a line;
+    // lanes l, l ^ 8 trade one piece (DPP row_ror:8) so that store A covers rows 16i + (l & 7) and store B rows
+    // 16i + 8 + (l & 7), 8 rows x 128 B each (instead of 16 rows x 64 B), the upper eight lanes writing the line's
+    // second half: column offset + 64 B for l >= 8
+    const int hi8 = l16 >> 3;
+    auto line_pair = [&](const uint4 & x0, const uint4 & x1, uint4 & a, uint4 & b) {
+        const uint32_t p0[4] = {x0.x, x0.y, x0.z, x0.w}, p1[4] = {x1.x, x1.y, x1.z, x1.w};
+        uint32_t ra[4], rb[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {   // (scalar selects: a lane-varying select of a vector array went to scratch)
+            const uint32_t snd = hi8 ? p0[k] : p1[k];
+            const uint32_t rcv = (uint32_t) __builtin_amdgcn_mov_dpp((int) snd, 0x128, 0xF, 0xF, false);   // row_ror:8
+            ra[k] = hi8 ? rcv : p0[k];
+            rb[k] = hi8 ? p1[k] : rcv;
+        }
+        a = make_uint4(ra[0], ra[1], ra[2], ra[3]);
+        b = make_uint4(rb[0], rb[1], rb[2], rb[3]);
     };
     const int pcol = 16 * (q & 1) + 8 * (q >> 1);    // column of this lane's 16-B piece within a 32-column pair
-    if (PIPE == 1 && (EPI == Q2A_EPI_PRE_H || (EPI == Q2A_EPI_QKV && part < 2))) {
+    if (PIPE == 1 && (EPI == Q2A_EPI_PRE_H || (EPI == Q2A_EPI_QKV && (part < 2 || p.v_rows)))) {
       if constexpr (PIPE == 1 && (EPI == Q2A_EPI_PRE_H || EPI == Q2A_EPI_QKV)) {
         // fp16 outputs of the 8-phase tile (fc1's pre-activation; Q / K hi and lo), staged through LDS so every store
         // instruction writes two WHOLE 512-B output rows: all 8 waves write the tile [256 rows][256 cols] into the idle
@@ -1358,7 +1402,8 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                     q2a_st(v, (uint4 *) (p.outH + orow * p.ldo + n0 + g * 8));
                     if (p.o_dup) *(uint4 *) (p.outH + orow * p.ldo + n0 + g * 8 + p.o_dup) = v;
                 } else {
-                    q2a_half * dst = pass == 0 ? (part == 0 ? p.qh : p.kh) : (part == 0 ? p.ql : p.kl);
+                    q2a_half * dst = pass == 0 ? (part == 0 ? p.qh : part == 1 ? p.kh : p.vt)
+                                               : (part == 0 ? p.ql : part == 1 ? p.kl : p.vtl);
                     q2a_st(v, (uint4 *) (dst + (int64_t) m * p.D + n0 - part * p.D + g * 8));
                 }
             }
@@ -1370,7 +1415,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
         Q2A_STAMP(ST, 6);
         Q2A_STAMP_RT(ST, 9);
       }
-    } else if (EPI == Q2A_EPI_QKV && part == 2) {
+    } else if (EPI == Q2A_EPI_QKV && part == 2 && !p.v_rows) {
       if constexpr (EPI == Q2A_EPI_QKV) {
             // V^T [clip][head][d][TP]: the wave's WR rows (t) of its 64 columns (d, one head) staged [d][t] in its own LDS
             // region, then stored two d-rows per instruction, 32 lanes x 8 B (4 t) = 256 contiguous bytes per row. (Per
@@ -1449,7 +1494,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
         const int orr = REMAP ? rbase - oq * p.o_rpg : 0;
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
-            const int ml = i * 16 + l16, m = rbase + ml;
+            uint4 hvj[2], lvj[2];
 #pragma unroll
             for (int jp = 0; jp < NJ / 2; ++jp) {
                 h4v ha, hb, la, lb;
@@ -1488,11 +1533,18 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                         }
                     }
                 }
-                const uint4 hv = pair16(ha, hb);
-                uint4 lv;
-                if (EPI == Q2A_EPI_QKV && !BF) lv = pair16(la, lb);
+                hvj[jp] = pair16(ha, hb);
+                if (EPI == Q2A_EPI_QKV && !BF) lvj[jp] = pair16(la, lb);
+            }
+            uint4 hA, hB, lA, lB;
+            line_pair(hvj[0], hvj[1], hA, hB);
+            if (EPI == Q2A_EPI_QKV && !BF) line_pair(lvj[0], lvj[1], lA, lB);
+            const int col = pcol + 32 * hi8;
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                const int ml = i * 16 + 8 * hf + (l16 & 7), m = rbase + ml;
+                const uint4 hv = hf ? hB : hA;
                 if (m < p.M) {
-                    const int col = 32 * jp + pcol;
                     if (REMAP) {
                         const bool wrap = orr + ml >= p.o_rpg;
                         const int64_t row = (int64_t) (oq + (wrap ? 1 : 0)) * p.o_gstride + (orr + ml - (wrap ? p.o_rpg : 0)) + p.o_off;
@@ -1500,8 +1552,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
                         if (p.o_dup) *(uint4 *) (p.outH + row * p.ldo + cbase + col + p.o_dup) = hv;
                     } else {
                         const int64_t o = (int64_t) m * p.D + cbase - part * p.D + col;
-                        if (Q2A_ST) q2a_st(hv, (uint4 *) ((part == 0 ? p.qh : p.kh) + o));
-                        if (!BF && Q2A_ST) q2a_st(lv, (uint4 *) ((part == 0 ? p.ql : p.kl) + o));
+                        if (Q2A_ST) q2a_st(hv, (uint4 *) ((part == 0 ? p.qh : part == 1 ? p.kh : p.vt) + o));
+                        if (EPI == Q2A_EPI_QKV && !BF && Q2A_ST)
+                            q2a_st(hf ? lB : lA, (uint4 *) ((part == 0 ? p.ql : part == 1 ? p.kl : p.vtl) + o));
                     }
                 }
             }
@@ -1605,17 +1658,17 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
         }
         store_half(64);
     } else {
-        // f32 outputs: residual add (O-proj, fc2), GELU (+ positional rows for conv2), plain store
+        // f32 outputs: residual add (O-proj, fc2), GELU (+ positional rows for conv2), plain store; whole 128-B lines per
+        // store (line_pair on the column tiles 2jp, 2jp + 1: 8 rows x 128 B instead of 16 rows x 64 B). Every lane
+        // computes its row (loads clamped to row M-1) so the lane exchange sees defined values; stores check the row.
         const int pq = EPI == Q2A_EPI_CONV2 ? rbase / p.T : 0;
         const int pt0 = EPI == Q2A_EPI_CONV2 ? rbase - pq * p.T : 0;
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
-            const int ml = i * 16 + l16, m = rbase + ml;
-            if (m >= p.M) continue;
-            float * orow = p.outF + (int64_t) m * p.ldo + cbase + 4 * q;
+            const int ml = i * 16 + l16, m = rbase + ml, mc = min(m, p.M - 1);
             f4 add[NJ];
             if (EPI == Q2A_EPI_RESID) {
-                const float * rrow = p.resid ? p.resid + (int64_t) m * p.ldo + cbase + 4 * q : orow;
+                const float * rrow = (p.resid ? p.resid : p.outF) + (int64_t) mc * p.ldo + cbase + 4 * q;
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) add[j] = *(const f4 *) (rrow + 16 * j);
             } else if (EPI == Q2A_EPI_CONV2) {
@@ -1624,20 +1677,30 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
 #pragma unroll
                 for (int j = 0; j < NJ; ++j) add[j] = *(const f4 *) (perow + 16 * j);
             }
+            f4 v[NJ];
 #pragma unroll
             for (int j = 0; j < NJ; ++j) {
-                f4 v;
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    v[r] = val(i, j, r);
-                    if (EPI == Q2A_EPI_RESID) v[r] = v[r] + add[j][r];        // (acc + bias) + x
-                    else if (EPI == Q2A_EPI_CONV2) v[r] = add[j][r] + v[r];   // pe + gelu(...)
+                    v[j][r] = val(i, j, r);
+                    if (EPI == Q2A_EPI_RESID) v[j][r] = v[j][r] + add[j][r];        // (acc + bias) + x
+                    else if (EPI == Q2A_EPI_CONV2) v[j][r] = add[j][r] + v[j][r];   // pe + gelu(...)
                 }
-                if (Q2A_ST) q2a_st(v, (f4 *) (orow + 16 * j));
-                if (EPI == Q2A_EPI_GELU_F && p.outH) {   // fp16 copy (exact: GELU table values are fp16) for the next GEMM
+                if (EPI == Q2A_EPI_GELU_F && p.outH && m < p.M) {   // fp16 copy (exact: GELU table values are fp16) for the next GEMM
                     typedef _Float16 h4s __attribute__((ext_vector_type(4)));
-                    const h4s hv = {(_Float16) v[0], (_Float16) v[1], (_Float16) v[2], (_Float16) v[3]};
+                    const h4s hv = {(_Float16) v[j][0], (_Float16) v[j][1], (_Float16) v[j][2], (_Float16) v[j][3]};
                     *(h4s *) (p.outH + (int64_t) m * p.ldo + cbase + 4 * q + 16 * j) = hv;
+                }
+            }
+#pragma unroll
+            for (int jp = 0; jp < NJ / 2; ++jp) {
+                uint4 a, b;
+                line_pair(__builtin_bit_cast(uint4, v[2 * jp]), __builtin_bit_cast(uint4, v[2 * jp + 1]), a, b);
+                const int col = cbase + 4 * q + 16 * (2 * jp + hi8);
+#pragma unroll
+                for (int hf = 0; hf < 2; ++hf) {
+                    const int mr = rbase + i * 16 + 8 * hf + (l16 & 7);
+                    if (mr < p.M && Q2A_ST) q2a_st(hf ? b : a, (uint4 *) (p.outF + (int64_t) mr * p.ldo + col));
                 }
             }
         }
@@ -1750,13 +1813,15 @@ int cu_count() {
 // than the second launch and the 128x128 tiles' lower rate.
 template <int EPI, int BLK>
 hipError_t launch_pipe8(const q2a_gemm_args & a, hipStream_t s) {
-    if constexpr (EPI == Q2A_EPI_PRE_H && BLK == 256) {
-        // persistent tiles (k_gemm PIPE = 2): whole 256-row tiles only, at least two Q4_K blocks
+    if constexpr ((EPI == Q2A_EPI_PRE_H || EPI == Q2A_EPI_QKV) && BLK == 256) {
+        // persistent tiles (k_gemm PIPE = 2): whole 256-row tiles only, at least two Q4_K blocks; Q|K|V only with V
+        // row-major (the V^T image needs the LDS-staged transposing epilogue)
         const int cus = cu_count();
         const int ntl = (a.N / 256) * ((a.M - a.m_base) / 256);
         const int grid = std::min(ntl, cus / 8 * 8);
         // (the workgroup's tile list holds 64 entries)
-        if ((a.M - a.m_base) % 256 == 0 && a.K >= 512 && ntl > 0 && cus >= 8 && ntl <= 64 * grid) {
+        if ((a.M - a.m_base) % 256 == 0 && a.K >= 512 && ntl > 0 && cus >= 8 && ntl <= 64 * grid &&
+            (EPI != Q2A_EPI_QKV || (a.v_rows && a.vtl && a.D % 256 == 0))) {
             hipLaunchKernelGGL((k_gemm<256, 256, 2, 4, EPI, BLK, 2>), dim3(grid), dim3(512), 0, s, a);
             return hipGetLastError();
         }

@@ -99,6 +99,8 @@ struct q2a_gemm_args {
     const q2a_half * wext2;
     int split_kq;                     // allow the small-tile split-K for k-quant / Q8_0 / Q4_0 weights (q2a_gemm_kq_ksplit)
     q2a_half * vtl;                   // Q2A_EPI_QKV: V^T lo image fp16(v - fp16(v)), same layout as vt (null = not written)
+    int v_rows;                       // Q2A_EPI_QKV: 1 = V hi / lo row-major [M][D] into vt / vtl (like Q and K; the engine's
+                                      //   reference contract), 0 = V^T [clip][head][64][TP] (bf16 contract, ggml backend)
     int m_base;                       // first output row of the launch (tiles cover rows [m_base, M)); set by the launcher
 };
 
@@ -129,6 +131,8 @@ struct q2a_attn_args {
     float * outF;        // [clips*T][D] f32  (quantized paths)
     int bf16;            // bf16-activation mode: qh/kh/vt and outH hold bf16, ql/kl unused, one MFMA per QK^T step
     const q2a_half * vtl;   // V^T lo image (v - fp16(v)) when q2a_attention_wants_vlo(), else unused
+    int v_rows;             // reference contract: 1 = vt / vtl hold V hi / lo row-major [clips*T][D] (the K layout; the
+                            //   kernel reads its P.V operand by transposing LDS reads), 0 = V^T [clip][head][64][TP]
 };
 // Reference contract (bf16 == 0): qh/ql hold Q * Q2A_LOG2E (after the 1/sqrt(dh) scale), split hi/lo — the kernel
 // works in log2 units (P = exp2(S' - m')); every producer (QKV epilogue qscale, ggml backend prep, test entry) folds it.
