@@ -442,15 +442,18 @@ def main():
     prof_n = (C.c_int64 * 11)()
     # the dominant matrix-core class (QKV, attention, O, fc1, fc2 = Q2A_PROF_* 4, 5, 7, 8, 9) from one profiled step
     # before the timed region; inside the timed region HIP events bracket only that class's launches (on the stream
-    # the kernels run on: an event pair costs ~7 us of GPU time per launch, 0.2 ms per step at one clip for one class);
-    # the per-kernel breakdown of every class comes from a separate fully-profiled pass after it
+    # the kernels run on). An event pair costs ~9 us of GPU time per launch (profiles/r06e_vrows_persistent_qkv_ab.json:
+    # 128 pairs = 1.1 ms per step at one clip), under 0.2 % of a step from 8 clips up; below that the same events run
+    # over an identical pass right after the timed region instead, so `value` carries none. The per-kernel breakdown of
+    # every class comes from a separate fully-profiled pass.
     lib.q2a_profile_enable_mask(C.c_void_p(eng.h), sum(1 << i for i in ROOF_CLASSES))
     lib.q2a_profile_read(C.c_void_p(eng.h), prof_ms, prof_n, 11, 1)
     step()
     torch.cuda.synchronize()
     lib.q2a_profile_read(C.c_void_p(eng.h), prof_ms, prof_n, 11, 1)
     dominant = max(ROOF_CLASSES, key=lambda i: prof_ms[i])
-    lib.q2a_profile_enable_mask(C.c_void_p(eng.h), 1 << dominant)
+    events_in_timed = clips_per_gpu >= 8
+    lib.q2a_profile_enable_mask(C.c_void_p(eng.h), (1 << dominant) if events_in_timed else 0)
     lib.q2a_profile_read(C.c_void_p(eng.h), prof_ms, prof_n, 11, 1)
 
     if dist is not None:
@@ -463,6 +466,11 @@ def main():
     if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - ts
+    if not events_in_timed:   # the dominant class's events over an identical pass (small batches)
+        lib.q2a_profile_enable_mask(C.c_void_p(eng.h), 1 << dominant)
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
     lib.q2a_profile_read(C.c_void_p(eng.h), prof_ms, prof_n, 11, 0)
     timed_ms, timed_n = list(prof_ms), list(prof_n)
     # breakdown pass (not timed): every kernel class bracketed by events
@@ -553,7 +561,9 @@ def main():
     # events of the breakdown pass unless it is the dominant class)
     roofline = roofline_of(dominant, timed_ms, timed_n, args.config, wt, bf16, clips_per_gpu)
     roofline["dominant"] = True
-    roofline["avg_launch_source"] = "HIP events on the launch stream over the timed region"
+    roofline["avg_launch_source"] = ("HIP events on the launch stream over the timed region" if events_in_timed else
+                                     "HIP events on the launch stream over an identical pass after the timed region "
+                                     "(events cost ~9 us per launch, 5 % of a one-clip step)")
     roofline["share_of_step"] = round(prof_ms[dominant] / brk_steps / (elapsed / args.steps * 1e3), 4)
     if dominant == 8:
         roofline_fc1 = dict(roofline)
