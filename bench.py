@@ -218,8 +218,8 @@ def host_cpu_info() -> dict:
 
 
 # The profile set measured on the current tree; its summaries are cited ahead of older rounds' (tags do not sort
-# by date: r04y was taken after r04z, and r05w, not r05x, is the round-5 closing set).
-PROFILE_TAG = "r05w"
+# by date: r04y was taken after r04z, and r05w, not r05x, is the round-5 closing set; r06h is round 6's set).
+PROFILE_TAG = "r06h"
 
 
 def _profile_files(names) -> list:

@@ -106,11 +106,11 @@ int q2a_reserve(q2a_engine * e, int max_clips, int64_t max_samples);
  *   offset_ms  whisper_full_params.offset_ms (window start = offset_ms / 10 mel frames)
  *   out_dev    [n_clips][n_out][n_audio_state] f32 (embd_enc of each clip)
  *   status     host array [n_clips] (Q2A_CLIP_*), may be NULL
- *   stream     hipStream_t to run on, or NULL: the engine's own stream, ordered as if the work had been issued on
- *              the legacy default stream 0 (it starts after everything queued there before the call, and work queued
- *              there afterwards starts after it) — the same rule for every device-pointer entry point below and
- *              q2a_projector_apply. The call is asynchronous w.r.t. the host except for the small per-batch
- *              metadata upload: synchronise (the given stream, or stream 0) before reading out_dev on the host.
+ *   stream     hipStream_t to run on, or NULL: the legacy default stream 0 itself (the work starts after everything
+ *              queued there before the call, and work queued there afterwards starts after it) — the same rule for
+ *              every device-pointer entry point below and q2a_projector_apply. The call is asynchronous w.r.t. the
+ *              host except for the small per-batch metadata upload: synchronise (the given stream, or stream 0)
+ *              before reading out_dev on the host.
  * Audio longer than 30 s is truncated to one 30 s window, as in the reference (qwen2-whisper.cpp:2366-2372). */
 int q2a_encode_device(q2a_engine * e, const float * pcm_dev, int64_t pcm_stride, const int32_t * n_samples,
                       int n_clips, int offset_ms, float * out_dev, int32_t * status, void * stream);

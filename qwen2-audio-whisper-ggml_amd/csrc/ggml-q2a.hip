@@ -1384,6 +1384,7 @@ int run_fused_attention(q2a_backend_ctx * b, ggml_cgraph * g, int i, bool vt_rea
         q2a_attn_args at{(const q2a_half *) ready->qh, (const q2a_half *) ready->ql, (const q2a_half *) ready->kh,
                          (const q2a_half *) ready->kl, (const q2a_half *) ready->vt, 1, (int) T, (int) D, (int) H, TP, nullptr, o};
         at.vtl = ready->vtl;
+        at.v_rows = 1;   // (run_qkv_fused writes V row-major)
         if (out16 && merged) { at.outH = (q2a_half *) out16; at.outF = nullptr; }
         Q2A_HIP(q2a_launch_attention(at, b->stream));
         if (!merged)
@@ -1554,7 +1555,7 @@ void run_qkv_fused(q2a_backend_ctx * b, const qkv_route & r, qkv_ops & ops) {
     ops = {(_Float16 *) ob, (_Float16 *) (ob + hb), (_Float16 *) (ob + 2 * hb), (_Float16 *) (ob + 3 * hb),
            (_Float16 *) (ob + 4 * hb), vlo ? (_Float16 *) (ob + 4 * hb + vb1) : nullptr};
     const act_operand ao = activation_operand(b, x, M, K, blk, 0);
-    // (V^T's pad columns T <= t < TP: written as zeros by the epilogue of a one-clip launch, M == T)
+    // (V hi / lo row-major: no pad columns; the attention clamps its key rows to T - 1)
     q2a_gemm_args a;
     memset(&a, 0, sizeof(a));
     a.A = ao.A; a.lda = K; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
@@ -1562,6 +1563,7 @@ void run_qkv_fused(q2a_backend_ctx * b, const qkv_route & r, qkv_ops & ops) {
     a.bias = bias;
     a.qh = (q2a_half *) ops.qh; a.ql = (q2a_half *) ops.ql; a.kh = (q2a_half *) ops.kh; a.kl = (q2a_half *) ops.kl;
     a.vt = (q2a_half *) ops.vt; a.vtl = (q2a_half *) ops.vtl;
+    a.v_rows = 1;   // V hi / lo row-major [T][D] like K (the attention below reads it with k_attn_t<true>)
     a.T = T; a.D = D; a.H = H; a.TP = TP;
     // (x + b) * s then * log2 e in the unfused path; s = 2^-k makes one multiply by s * log2 e the same rounding
     a.qscale = r.qscale * Q2A_LOG2E;
@@ -1790,9 +1792,9 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                 !is_weight_buffer(m->src[0]) || ((uintptr_t) m->data & 15) != 0)
                 return false;
         const int64_t D = wq->ne[1], T = x->ne[1], H = D / 64;
-        // (T % 4: the epilogue's V^T stores are 4-t groups that only zero the pad columns of a group starting at or
-        // past T, q2a_gemm.hip; any other T keeps the separate projections)
-        if (wq->ne[0] != D || D % 64 != 0 || T % 4 != 0 || x->ne[2] != 1 || x->ne[3] != 1 || T * D >= (1ll << 31)) return false;
+        // (any T: the fused GEMM writes V row-major, q2a_gemm_args.v_rows — the V^T epilogue's 4-t groups, which needed
+        // T % 4 == 0, are not used on this route)
+        if (wq->ne[0] != D || D % 64 != 0 || x->ne[2] != 1 || x->ne[3] != 1 || T * D >= (1ll << 31)) return false;
         if (!row_vec_f32(qa->src[1], D) || !row_vec_f32(va->src[1], D) || !is_weight_buffer(qa->src[1]) ||
             !is_weight_buffer(va->src[1]) || !same_shape_rows(qm, qa) || !same_shape_rows(vm, va))
             return false;
