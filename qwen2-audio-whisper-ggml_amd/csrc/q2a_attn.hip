@@ -11,8 +11,9 @@
 // normalisation is applied once at the end.
 //
 // Kernels (the schedules measured and not adopted live in diag/attn_variants.hip, built only into diag libraries):
-//   k_attn_t       reference contract: one 256-thread workgroup = 4 waves x 32 queries of one (clip, head), K/V tiles
-//                  of 32 keys by LDS-DMA into three LDS stages, software-pipelined, 16x16x32 MFMAs
+//   k_attn_t       reference contract: one 256-thread workgroup = 4 waves x 32 queries of one (clip, head) (x 16 when
+//                  that grid would leave CUs idle), K/V tiles of 32 keys by LDS-DMA into three LDS stages,
+//                  software-pipelined, 16x16x32 MFMAs
 //   k_attn_pp<BF>  bf16-activation contract (BF = true): 8-wave ping-pong, one 512-thread workgroup = 256 queries
 // The S accumulator feeds the P.V MFMA as its B operand with no data movement (K rows permuted so a lane's scores are
 // the keys of its P.V fragment; cdna_hip_programming.md §3 "An accumulator tile as the next MFMA's operand").
@@ -148,8 +149,13 @@ __device__ __forceinline__ float sum_lane32(float x) {
 // them as whole 128-B rows, no transposing epilogue) and the P.V A operand V^T[d][keys] is read out of the [key][d] LDS
 // image by ds_read_b64_tr_b16 (two 4-key reads per 8-key fragment); !VR: the V^T [clip][head][64][TP] image (the ggml
 // backend's operands) read by ds_read_b128.
-template <bool VR>
+// NQB = 16-query blocks per wave: 2 (128 queries per workgroup) or 1 (64, for grids too small to fill the chip — one
+// clip). A block's arithmetic does not depend on its wave-mates (the lazy re-base is decided per block), so both forms
+// give every query the same bits.
+template <bool VR, int NQB>
 __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
+    static_assert(NQB == 1 || NQB == 2, "16 or 32 queries per wave");
+    constexpr int QWG = 64 * NQB;   // queries per workgroup
     constexpr int KROW = 128, VROW = 64;
     constexpr int KIMG = KS * KROW, VIMG = 64 * VROW;
     constexpr int STAGE = 2 * KIMG + 2 * VIMG;                   // Kh | Kl | Vh^T | Vl^T of 32 keys
@@ -158,18 +164,18 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
     __shared__ __attribute__((aligned(16))) char ldsC[STAGE];
     const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int T = p.T, D = p.D;
-    const int nq = (T + 127) / 128, total = (int) gridDim.x;
+    const int nq = (T + QWG - 1) / QWG, total = (int) gridDim.x;
     const int L = (int) blockIdx.x;
     const int w = (total & 7) ? L : (L & 7) * (total >> 3) + (L >> 3);   // XCD-contiguous work order: the q-tiles of one (clip, head) on one XCD
     const int qt = w % nq, h = (w / nq) % p.H, clip = w / (nq * p.H);
-    const int q0 = qt * 128 + wave * 32;
+    const int q0 = qt * QWG + wave * 16 * NQB;
     const int64_t rowbase = (int64_t) clip * T;
     const int c16 = lane & 15, g = lane >> 4;
 
     // Q fragments (B operand): query 16qb + c16, d = 32ds + 8g .. +7
-    half8 qh[2][2], ql[2][2];
+    half8 qh[NQB][2], ql[NQB][2];
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
+    for (int qb = 0; qb < NQB; ++qb) {
         const int q = min(q0 + 16 * qb + c16, T - 1);
         const q2a_half * sh = p.qh + (rowbase + q) * D + h * 64 + 8 * g;
         const q2a_half * sl = p.ql + (rowbase + q) * D + h * 64 + 8 * g;
@@ -208,12 +214,15 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
         __builtin_amdgcn_global_load_lds((const void *) (vlb + vo), (lds_ptr_t) (st + 2 * KIMG + VIMG + wave * 1024), 16, 0, 0);
     };
 
-    f4v_t o[2][4];
+    f4v_t o[NQB][4];
+    float m_run[NQB], l_run[NQB];
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb)
+    for (int qb = 0; qb < NQB; ++qb) {
 #pragma unroll
         for (int db = 0; db < 4; ++db) o[qb][db] = f4v_t{0.f, 0.f, 0.f, 0.f};
-    float m_run[2] = {0.f, 0.f}, l_run[2] = {0.f, 0.f};
+        m_run[qb] = 0.f;
+        l_run[qb] = 0.f;
+    }
     const int ntiles = (T + KS - 1) / KS;
     // LDS byte offsets: K row of (kb, i = c16), chunk 4ds + g (swizzled); V^T row c16 (+16db), granule g (swizzled)
     uint32_t kofs[2][2], vofs;
@@ -244,10 +253,10 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
         const short8_t v8 = {lo4[0], lo4[1], lo4[2], lo4[3], hi4[0], hi4[1], hi4[2], hi4[3]};
         return __builtin_bit_cast(half8, v8);
     };
-    typedef f4v_t sc_t[2][2];   // [qb][kb]
+    typedef f4v_t sc_t[NQB][2];   // [qb][kb]
     auto splat = [&](sc_t & s) {
 #pragma unroll
-        for (int qb = 0; qb < 2; ++qb) {
+        for (int qb = 0; qb < NQB; ++qb) {
             float nm = -m_run[qb];
             asm volatile("" : "+v"(nm));
 #pragma unroll
@@ -255,12 +264,12 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
         }
     };
     // P of the tile: [qb] = B fragment of keys 8g .. 8g+7 (hi and lo halves)
-    half8 ph[2], pl[2];
-    typedef float ex_t[2][8];   // exp2 of one tile's scores, [qb][4kb + r]
+    half8 ph[NQB], pl[NQB];
+    typedef float ex_t[NQB][8];   // exp2 of one tile's scores, [qb][4kb + r]
     // P hi / lo pairs and the lane sums of one tile's exponentials
-    auto split = [&](const ex_t & e, float (&ls)[2]) {
+    auto split = [&](const ex_t & e, float (&ls)[NQB]) {
 #pragma unroll
-        for (int qb = 0; qb < 2; ++qb) {
+        for (int qb = 0; qb < NQB; ++qb) {
             float a = e[qb][0];
 #pragma unroll
             for (int j = 1; j < 8; ++j) a += e[qb][j];
@@ -277,7 +286,7 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
     };
     auto exps = [&](const sc_t & sv, ex_t & e) {
 #pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
+        for (int qb = 0; qb < NQB; ++qb)
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -287,7 +296,7 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
     };
     // region A: S'^T - m' of the tile at stage st into s (initialised by the caller with the splat); with e: the
     // previous tile's P split and sums in the MFMA issue gaps
-    auto qk = [&](const char * st, sc_t & s, const ex_t * e, float (&ls)[2]) {
+    auto qk = [&](const char * st, sc_t & s, const ex_t * e, float (&ls)[NQB]) {
         launder_ofs();
 #pragma unroll
         for (int ds = 0; ds < 2; ++ds) {
@@ -298,7 +307,7 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
                 kl[kb] = *(const half8 *) (st + KIMG + kofs[kb][ds]);
             }
 #pragma unroll
-            for (int qb = 0; qb < 2; ++qb)
+            for (int qb = 0; qb < NQB; ++qb)
 #pragma unroll
                 for (int kb = 0; kb < 2; ++kb) {
                     s[qb][kb] = mma16(kh[kb], qh[qb][ds], s[qb][kb]);
@@ -310,13 +319,13 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
             split(*e, ls);
             __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
-            for (int i = 0; i < 12; ++i) {
+            for (int i = 0; i < 6 * NQB; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
             }
             __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
-            for (int i = 0; i < 12; ++i) {
+            for (int i = 0; i < 6 * NQB; ++i) {
                 __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
                 __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
             }
@@ -325,7 +334,7 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
     auto mask = [&](sc_t & sv, int t) {   // keys >= T (last tile only): key of (kb, r) in lane group g is 8g + 4kb + r
         if (t == ntiles - 1) {
 #pragma unroll
-            for (int qb = 0; qb < 2; ++qb)
+            for (int qb = 0; qb < NQB; ++qb)
 #pragma unroll
                 for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -334,14 +343,15 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
         }
     };
     // re-base query block qb to the tile's max over its 32 keys (4 lane groups): first tile m' := that max
-    auto rebase = [&](sc_t & sv, int qb, bool first) {
+    auto rebase = [&](sc_t & sv, int qb, bool first, bool on = true) {
         float mx = sv[qb][0][0];
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
             for (int r = 0; r < 4; ++r) mx = fmaxf(mx, sv[qb][kb][r]);
         mx = max_lane32(max_lane16(mx));
-        const float sh = first ? mx : fmaxf(mx, 0.f);
+        // (on = false: a shift of exactly 0 — alpha 1, every value unchanged)
+        const float sh = first ? mx : on ? fmaxf(mx, 0.f) : 0.f;
         if (!first) {
             const float alpha = __builtin_amdgcn_exp2f(-sh);
             l_run[qb] *= alpha;
@@ -369,7 +379,7 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
             }
         }
 #pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
+        for (int qb = 0; qb < NQB; ++qb)
 #pragma unroll
             for (int db = 0; db < 4; ++db) {
                 o[qb][db] = mma16(vl[db], ph[qb], o[qb][db]);
@@ -379,22 +389,28 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
         exps(sn, e);
         splat(init);
         // both stay in this region (not sunk past the barrier into the next tile's head)
-        asm volatile("" : "+v"(init[0][0]), "+v"(init[0][1]), "+v"(init[1][0]), "+v"(init[1][1]));
-        asm volatile("" : "+v"(e[0][0]), "+v"(e[0][1]), "+v"(e[0][2]), "+v"(e[0][3]), "+v"(e[0][4]), "+v"(e[0][5]),
-                          "+v"(e[0][6]), "+v"(e[0][7]), "+v"(e[1][0]), "+v"(e[1][1]), "+v"(e[1][2]), "+v"(e[1][3]),
-                          "+v"(e[1][4]), "+v"(e[1][5]), "+v"(e[1][6]), "+v"(e[1][7]));
+        if constexpr (NQB == 2) {
+            asm volatile("" : "+v"(init[0][0]), "+v"(init[0][1]), "+v"(init[1][0]), "+v"(init[1][1]));
+            asm volatile("" : "+v"(e[0][0]), "+v"(e[0][1]), "+v"(e[0][2]), "+v"(e[0][3]), "+v"(e[0][4]), "+v"(e[0][5]),
+                              "+v"(e[0][6]), "+v"(e[0][7]), "+v"(e[1][0]), "+v"(e[1][1]), "+v"(e[1][2]), "+v"(e[1][3]),
+                              "+v"(e[1][4]), "+v"(e[1][5]), "+v"(e[1][6]), "+v"(e[1][7]));
+        } else {
+            asm volatile("" : "+v"(init[0][0]), "+v"(init[0][1]));
+            asm volatile("" : "+v"(e[0][0]), "+v"(e[0][1]), "+v"(e[0][2]), "+v"(e[0][3]), "+v"(e[0][4]), "+v"(e[0][5]),
+                              "+v"(e[0][6]), "+v"(e[0][7]));
+        }
         __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {   // one exponential per MFMA gap (8 of the 16 cycles issue VALU)
+        for (int i = 0; i < 8 * NQB; ++i) {   // one exponential per MFMA gap (8 of the 16 cycles issue VALU)
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);
         }
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < 4 * NQB; ++i) {
             __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
             __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
         }
-        __builtin_amdgcn_sched_group_barrier(0x002, 16, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 8 * NQB, 0);
     };
 
     sc_t sn, init;
@@ -402,31 +418,47 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
     // iteration t: stage sK holds tile t+1, sV tile t (its V for P.V, its K for the rare re-base), tile t+2 -> sD
     auto iter = [&](const char * sK, const char * sV, char * sD, int t) {
         if (t + 2 < ntiles) dma_tile(sD, t + 2);
-        float ls[2];
+        float ls[NQB];
 #pragma unroll
-        for (int qb = 0; qb < 2; ++qb)
+        for (int qb = 0; qb < NQB; ++qb)
 #pragma unroll
             for (int kb = 0; kb < 2; ++kb) sn[qb][kb] = init[qb][kb];
         // region A: QK^T(t+1) beside the P split / sums of tile t. (After the last tile it reads a stage holding an
         // older tile; those scores are never used.)
         qk(sK, sn, &ex, ls);
-        if (t != 0 && __any(ls[0] > PLIM || ls[1] > PLIM)) {   // rare: re-base from tile t's scores (K(t) in place)
+        // rare: re-base from tile t's scores (K(t) in place), decided per 16-query block (a block whose lanes all stay
+        // under PLIM keeps its reference point and its exponentials)
+        bool rb[NQB], any_rb = false;
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb) {
+            rb[qb] = __any(ls[qb] > PLIM);
+            any_rb |= rb[qb];
+        }
+        if (t != 0 && any_rb) {
             sc_t s2;
             splat(s2);
-            float dummy[2];
+            float dummy[NQB];
             qk(sV, s2, nullptr, dummy);
             mask(s2, t);
 #pragma unroll
-            for (int qb = 0; qb < 2; ++qb) {
-                const float sh = rebase(s2, qb, false);
+            for (int qb = 0; qb < NQB; ++qb) {
+                const float sh = rebase(s2, qb, false, rb[qb]);
 #pragma unroll
                 for (int kb = 0; kb < 2; ++kb) sn[qb][kb] -= sh;
             }
-            exps(s2, ex);   // P of tile t again, against the new reference point
+            // P of tile t again, against the new reference point — only for the re-based blocks: the others keep the
+            // exponentials of S(t) - m' as first computed (a recomputation from the current m' can differ in the
+            // last bit when m' moved in the previous iteration)
+            ex_t e2;
+            exps(s2, e2);
+#pragma unroll
+            for (int qb = 0; qb < NQB; ++qb)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) ex[qb][j] = rb[qb] ? e2[qb][j] : ex[qb][j];
             split(ex, ls);
         }
-        l_run[0] += ls[0];
-        l_run[1] += ls[1];
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb) l_run[qb] += ls[qb];
         mask(sn, t + 1);
         // region B: P.V(t) beside the exponentials of tile t+1
         pv(sV, init, sn, ex);
@@ -435,17 +467,17 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
 
     dma_tile(ldsA, 0);
     if (ntiles > 1) dma_tile(ldsB, 1);
-    asm volatile("" :: "v"(qh[0][0]), "v"(qh[0][1]), "v"(qh[1][0]), "v"(qh[1][1]), "v"(ql[0][0]), "v"(ql[0][1]),
-                 "v"(ql[1][0]), "v"(ql[1][1]));
+#pragma unroll
+    for (int qb = 0; qb < NQB; ++qb) asm volatile("" :: "v"(qh[qb][0]), "v"(qh[qb][1]), "v"(ql[qb][0]), "v"(ql[qb][1]));
     __syncthreads();
     {
-        float dummy[2];
+        float dummy[NQB];
         sc_t s0;
         splat(s0);
         qk(ldsA, s0, nullptr, dummy);   // tile 0 against m' = 0, then m' := its max
         mask(s0, 0);
-        rebase(s0, 0, true);
-        rebase(s0, 1, true);
+#pragma unroll
+        for (int qb = 0; qb < NQB; ++qb) rebase(s0, qb, true);
         exps(s0, ex);
         splat(init);
     }
@@ -458,7 +490,7 @@ __global__ __launch_bounds__(256, 3) void k_attn_t(const q2a_attn_args p) {
     }
 
 #pragma unroll
-    for (int qb = 0; qb < 2; ++qb) {
+    for (int qb = 0; qb < NQB; ++qb) {
         const float l_tot = sum_lane32(sum_lane16(l_run[qb]));
         const float inv = 1.0f / l_tot;
         const int q = q0 + 16 * qb + c16;
@@ -733,9 +765,18 @@ hipError_t Q2A_ATTN_LAUNCH(const q2a_attn_args & a, hipStream_t s) {
         hipLaunchKernelGGL(k_attn_pp<true>, dim3(((a.T + 255) / 256) * a.H * a.n_clips), dim3(512), 0, s, a);
     } else {
         if (!a.vtl) return hipErrorInvalidValue;
-        const dim3 grid(((a.T + 127) / 128) * a.H * a.n_clips);
-        if (a.v_rows) hipLaunchKernelGGL(k_attn_t<true>, grid, dim3(256), 0, s, a);
-        else hipLaunchKernelGGL(k_attn_t<false>, grid, dim3(256), 0, s, a);
+        // 32 queries per wave, or 16 when that grid would leave CUs idle (one clip: 240 workgroups of 128 queries on
+        // 256 CUs, one wave per SIMD); the two forms give the same bits
+        const int n2 = ((a.T + 127) / 128) * a.H * a.n_clips;
+        const bool narrow = n2 < q2a_cu_count();
+        const dim3 grid(narrow ? ((a.T + 63) / 64) * a.H * a.n_clips : n2);
+        if (a.v_rows) {
+            if (narrow) hipLaunchKernelGGL((k_attn_t<true, 1>), grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_attn_t<true, 2>), grid, dim3(256), 0, s, a);
+        } else {
+            if (narrow) hipLaunchKernelGGL((k_attn_t<false, 1>), grid, dim3(256), 0, s, a);
+            else hipLaunchKernelGGL((k_attn_t<false, 2>), grid, dim3(256), 0, s, a);
+        }
     }
     return hipGetLastError();
 }

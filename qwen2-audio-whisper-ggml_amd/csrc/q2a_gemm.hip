@@ -1948,6 +1948,7 @@ hipError_t q2a_launch_gemm(const q2a_gemm_args & a_in, int epi, int blk, hipStre
 }
 
 bool q2a_gemm_wide_tiles(int M, int N, int blk) { (void) blk; return wide_tiles(M, N); }
+int q2a_cu_count() { return cu_count(); }
 
 bool q2a_gemm_pipe8(const q2a_gemm_args & a, int blk) { return pipe8_ok(a, blk) && (blk != 256 || a.beta); }
 

@@ -120,6 +120,8 @@ constexpr int Q2A_BLK_EXACT = 2;
 hipError_t q2a_launch_gemm(const q2a_gemm_args & a, int epi, int blk, hipStream_t s);
 // true when the launcher will use the 256-column tile configuration for this shape (Q2A_EPI_GELU_Q8K needs it)
 bool q2a_gemm_wide_tiles(int M, int N, int blk);
+// compute units of the current device (cached per device ordinal; 0 when it cannot be queried)
+int q2a_cu_count();
 // true when the launcher will use the 8-phase 256x256 kernel for these arguments (its Q4_K flavour fuses
 // Q2A_EPI_GELU_Q8K efficiently)
 bool q2a_gemm_pipe8(const q2a_gemm_args & a, int blk);

@@ -101,6 +101,29 @@ def test_attention_matches_fp32_reference(engines, cfg, D, H, B):
     assert mx < 2e-5 and l2 < 5e-6, (mx, l2)
 
 
+@pytest.mark.parametrize("cfg,D,H,B", [("tiny", 256, 4, 6), ("full", 1280, 20, 2)])
+def test_attention_narrow_grid_gives_the_same_bits(engines, cfg, D, H, B):
+    """One clip launches 16 queries per wave (its 128-query grid would leave CUs idle), a batch 32 (q2a_attn.hip
+    launcher): every clip of the batch must equal that clip run alone, bit for bit (the lazy re-base is decided per
+    16-query block, so a block's arithmetic does not depend on its wave-mates)."""
+    e = engines(cfg, "f16")
+    T = 1500
+    g = torch.Generator(device="cpu").manual_seed(7)
+    q = (torch.randn(B * T, D, generator=g) * 2.0).cuda()   # large scores: the re-base path runs
+    k = (torch.randn(B * T, D, generator=g) * 2.0).cuda()
+    v = torch.randn(B * T, D, generator=g).cuda()
+    out = torch.empty_like(q)
+    e.test_attention(q.data_ptr(), k.data_ptr(), v.data_ptr(), B, out.data_ptr())
+    torch.cuda.synchronize()
+    for b in (0, B - 1):
+        sl = slice(b * T, (b + 1) * T)
+        qs, ks, vs = q[sl].contiguous(), k[sl].contiguous(), v[sl].contiguous()
+        o1 = torch.empty_like(qs)
+        e.test_attention(qs.data_ptr(), ks.data_ptr(), vs.data_ptr(), 1, o1.data_ptr())
+        torch.cuda.synchronize()
+        assert torch.equal(o1, out[sl]), f"clip {b}: batched attention differs from the one-clip launch"
+
+
 def test_attention_propagates_nan(engines):
     """q2a_attn.o is built with -fno-honor-nans (Makefile: the max reductions need no sNaN canonicalisation). A
     non-finite upstream value must still surface: a NaN in one query row makes that row's output NaN (its scores, hence
