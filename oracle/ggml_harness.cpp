@@ -210,6 +210,85 @@ int cmd_graphs(int argc, char ** argv) {
     return eq ? 0 : 6;
 }
 
+// The conv MUL_MAT(F32 x, F16 w) of the backend (run_mm_conv_hilo) at conv2's shape: x all fp16 values (the GELU
+// table's outputs) runs the one-part GEMM, x with one value that is not an fp16 value (a GELU passthrough x >= 10) the
+// three-part one. The rows that hold only fp16 values must come out with the same bits either way; every output is
+// checked against a double-precision dot product of the same operands.
+int cmd_convgate(int argc, char ** argv) {
+    const int device = argc > 2 ? atoi(argv[2]) : 0;
+    ggml_backend_t be = ggml_backend_q2a_init(device);
+    if (!be) { fprintf(stderr, "no Q2A backend\n"); return 3; }
+    const int K = 3840, M = 1500, N = 1280, m_odd = 777, k_odd = 1234;
+    ggml_init_params ip = { 8 * ggml_tensor_overhead(), nullptr, true };
+    ggml_context * cw = ggml_init(ip);
+    ggml_tensor * w = ggml_new_tensor_2d(cw, GGML_TYPE_F16, K, N);
+    ggml_backend_buffer_t bw = ggml_backend_alloc_ctx_tensors(cw, be);
+    ggml_backend_buffer_set_usage(bw, GGML_BACKEND_BUFFER_USAGE_WEIGHTS);
+    uint32_t st = 4242;
+    auto rnd = [&]() { st = st * 1664525u + 1013904223u; return (float) ((st >> 8) & 0xFFFF) / 65536.0f - 0.5f; };
+    std::vector<ggml_fp16_t> wh((size_t) K * N);
+    for (auto & v : wh) v = ggml_fp32_to_fp16(0.05f * rnd());
+    ggml_backend_tensor_set(w, wh.data(), 0, wh.size() * 2);
+    ggml_init_params gp = { 16 * ggml_tensor_overhead() + ggml_graph_overhead(), nullptr, true };
+    ggml_context * c = ggml_init(gp);
+    ggml_tensor * x = ggml_new_tensor_2d(c, GGML_TYPE_F32, K, M);
+    ggml_tensor * y = ggml_mul_mat(c, x, w);   // [M][N] as the conv graph's node: src0 = im2col (F32), src1 = kernel
+    ggml_cgraph * g = ggml_new_graph(c);
+    ggml_build_forward_expand(g, y);
+    ggml_backend_buffer_t bx = ggml_backend_alloc_ctx_tensors(c, be);
+    std::vector<float> xh((size_t) K * M);
+    for (auto & v : xh) v = ggml_fp16_to_fp32(ggml_fp32_to_fp16(4.0f * rnd()));   // fp16 values
+    auto run = [&](std::vector<float> & out) {
+        ggml_backend_tensor_set(x, xh.data(), 0, xh.size() * 4);
+        if (ggml_backend_graph_compute(be, g) != GGML_STATUS_SUCCESS) { fprintf(stderr, "compute failed\n"); exit(5); }
+        out.resize((size_t) M * N);
+        ggml_backend_tensor_get(y, out.data(), 0, out.size() * 4);
+    };
+    // error against the f64 dot product, relative to sum |x w| (the scale of the summation's own rounding)
+    auto rel = [&](const std::vector<float> & out, int m, int n) {
+        double d = 0, a = 0;
+        for (int k = 0; k < K; ++k) {
+            const double p = (double) xh[(size_t) m * K + k] * (double) ggml_fp16_to_fp32(wh[(size_t) n * K + k]);
+            d += p;
+            a += fabs(p);
+        }
+        return fabs((double) out[(size_t) n * M + m] - d) / a;
+    };
+    auto err = [&](const std::vector<float> & out) {
+        double worst = 0;
+        for (int n = 0; n < N; n += 7)
+            for (int m = 0; m < M; m += 3) worst = std::max(worst, rel(out, m, n));
+        return worst;
+    };
+    std::vector<float> y1, y3;
+    run(y1);
+    const double e1 = err(y1);
+    ggml_backend_q2a_stats s1;
+    memset(&s1, 0, sizeof(s1));
+    ggml_backend_q2a_get_stats(be, &s1);
+    xh[(size_t) m_odd * K + k_odd] = 12.345678f;   // not an fp16 value: the three-part GEMM
+    run(y3);
+    const double e3 = err(y3);
+    int64_t diff_other = 0, diff_odd = 0;
+    for (int n = 0; n < N; ++n)
+        for (int m = 0; m < M; ++m) {
+            const bool same = memcmp(&y1[(size_t) n * M + m], &y3[(size_t) n * M + m], 4) == 0;
+            if (m == m_odd) diff_odd += !same;
+            else diff_other += !same;
+        }
+    double e_odd = 0;
+    for (int n = 0; n < N; ++n) e_odd = std::max(e_odd, rel(y3, m_odd, n));
+    printf("{\"mm_conv\": %d, \"max_rel_fp16_inputs\": %.3e, \"max_rel_with_odd_value\": %.3e, \"odd_row_rel\": %.3e, "
+           "\"other_rows_differing\": %lld, \"odd_row_outputs_changed\": %lld}\n", s1.n_mul_mat_conv, e1, e3, e_odd,
+           (long long) diff_other, (long long) diff_odd);
+    ggml_backend_buffer_free(bx);
+    ggml_free(c);
+    ggml_backend_buffer_free(bw);
+    ggml_free(cw);
+    ggml_backend_free(be);
+    return 0;
+}
+
 // The pinned host buffer type and host-memory registration (ggml-q2a.h; the reference's ggml-cuda.h:34, 40-41):
 // a host-buffer tensor is ordinary CPU memory to ggml (is_host, written in place), copies between it and a device
 // tensor carry the bytes unchanged, the device and the registry expose it the way ggml's generic code looks it up, and
@@ -297,6 +376,7 @@ int main(int argc, char ** argv) {
     if (std::string(argv[1]) == "encode") return cmd_encode(argc, argv);
     if (std::string(argv[1]) == "graphs") return cmd_graphs(argc, argv);
     if (std::string(argv[1]) == "hostbuf") return cmd_hostbuf(argc, argv);
+    if (std::string(argv[1]) == "convgate") return cmd_convgate(argc, argv);
     fprintf(stderr, "unknown command %s\n", argv[1]);
     return 1;
 }

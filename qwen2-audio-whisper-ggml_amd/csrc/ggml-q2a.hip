@@ -513,19 +513,26 @@ __global__ void k_attn_out(const float * o, tview d, int T, int H, int64_t n) {
 // [M][K] -> [M][PK] against [N][PK]. P = 3 (conv_parts): hi = fp16(x), mid = fp16(x - hi), lo = fp16(x - hi - mid)
 // hold x exactly (24 bits in three 11-bit pieces), so every product is the f32 product exactly. Both conv nodes use
 // it: conv2's input is mostly the GELU table's fp16 values (mid = lo = 0), but ggml_vec_gelu_f32 passes x >= 10
-// through as f32 (ggml.c:2562), which two parts (22 bits) would round
-__global__ void k_hilo_rows(const float * x, _Float16 * a, int K, int P, int n) {
+// through as f32 (ggml.c:2562), which two parts (22 bits) would round. *inexact is raised when any x is not an fp16
+// value (r != 0, NaN and infinities included): while it stays 0 the mid and lo parts are all zero, and the GEMM over
+// the hi part alone (same K-steps, the zero parts' partials are exact zeros) gives the same bits as the three-part one
+__global__ __launch_bounds__(256) void k_hilo_rows(const float * x, _Float16 * a, int K, int P, int n, int * inexact) {
     const int i = (int) blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const int m = i / K, k = i - m * K;
-    const float v = x[i];
-    const _Float16 h = (_Float16) v;
-    const float r = v - (float) h;   // exact
-    const _Float16 md = (_Float16) r;
-    _Float16 * row = a + (int64_t) m * P * K;
-    row[k] = h;
-    row[K + k] = md;
-    if (P == 3) row[2 * K + k] = (_Float16) (r - (float) md);
+    bool nz = false;
+    if (i < n) {
+        const int m = i / K, k = i - m * K;
+        const float v = x[i];
+        const _Float16 h = (_Float16) v;
+        const float r = v - (float) h;   // exact
+        const _Float16 md = (_Float16) r;
+        _Float16 * row = a + (int64_t) m * P * K;
+        row[k] = h;
+        row[K + k] = md;
+        if (P == 3) row[2 * K + k] = (_Float16) (r - (float) md);
+        nz = !(r == 0.0f);
+    }
+    // one atomic per wave that holds such a value (inexact is null for conv1, whose mel rows hold them everywhere)
+    if (inexact && __any(nz) && (threadIdx.x & 63) == 0) atomicOr(inexact, 1);
 }
 __global__ void k_dup_rows(const _Float16 * w, _Float16 * o, int K, int P, int n) {
     const int i = (int) blockIdx.x * blockDim.x + threadIdx.x;
@@ -1179,7 +1186,8 @@ void run_mm_conv_hilo(q2a_backend_ctx * b, ggml_tensor * op) {
     const size_t t_bytes = ((size_t) M * N * 4 + 255) & ~size_t(255);
     const size_t p_bytes = S > 1 ? ((size_t) S * M * N * 4 + 255) & ~size_t(255) : 0;
     const size_t d_bytes = cached ? 0 : (size_t) N * P * K * 2;
-    char * s = (char *) scratch(b, a_bytes + t_bytes + p_bytes + d_bytes);
+    char * s = (char *) scratch(b, a_bytes + t_bytes + p_bytes + d_bytes + 256);
+    int * inexact = (int *) (s + a_bytes + t_bytes + p_bytes + d_bytes);
     b->quant_src = nullptr;
     const _Float16 * wdup = (const _Float16 *) wd.dev;
     if (!cached) {   // not a model weight: duplicate this call's bytes into the scratch
@@ -1190,7 +1198,12 @@ void run_mm_conv_hilo(q2a_backend_ctx * b, ggml_tensor * op) {
     _Float16 * A = (_Float16 *) s;
     float * tmp = (float *) (s + a_bytes);
     const int n = M * K;
-    hipLaunchKernelGGL(k_hilo_rows, grid1(n), dim3(256), 0, b->stream, (const float *) x->data, A, K, P, n);
+    // the one-part alternative only for deep K (conv2, K = 3 x 1280: its input is the GELU table's fp16 values);
+    // conv1's normalised log-mel is never fp16-valued
+    const bool gated = S <= 1 && K >= 1024;
+    if (gated) Q2A_HIP(hipMemsetAsync(inexact, 0, sizeof(int), b->stream));
+    hipLaunchKernelGGL(k_hilo_rows, grid1(n), dim3(256), 0, b->stream, (const float *) x->data, A, K, P, n,
+                       gated ? inexact : nullptr);
     q2a_gemm_args a;
     memset(&a, 0, sizeof(a));
     a.A = (const q2a_half *) A; a.lda = P * K; a.a_rpg = M; a.a_gstride = 0; a.a_step = 1;
@@ -1203,7 +1216,17 @@ void run_mm_conv_hilo(q2a_backend_ctx * b, ggml_tensor * op) {
         a.split_stride = (int64_t) M * N;
         a.split_store = 1;
     }
+    // two launches, one of which computes: over the hi part alone when every x is an fp16 value (conv2's GELU-table
+    // input, unless a value >= 10 passed through), over all P parts otherwise — the same bits either way
+    a.gate = gated ? inexact : nullptr;
+    a.gate_on = 1;
     Q2A_HIP(q2a_launch_gemm(a, Q2A_EPI_STORE_F, Q2A_BLK_EXACT, b->stream));
+    if (a.gate) {
+        q2a_gemm_args a1 = a;
+        a1.K = K;
+        a1.gate_on = 0;
+        Q2A_HIP(q2a_launch_gemm(a1, Q2A_EPI_STORE_F, Q2A_BLK_EXACT, b->stream));
+    }
     hipLaunchKernelGGL(k_transpose_f32, dim3((unsigned) ((N + 63) / 64), (unsigned) ((M + 63) / 64)), dim3(256), 0, b->stream,
                        (const float *) tmp, (float *) op->data, M, N);
 }

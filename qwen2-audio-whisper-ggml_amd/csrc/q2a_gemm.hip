@@ -674,6 +674,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm(const q2a_gemm_args p_
     constexpr bool EX = BLK_ == Q2A_BLK_EXACT;             // fp16 operands, f64 sum of per-K-step partials
     constexpr int BLK = (BF || EX) ? 0 : BLK_;
     static_assert(!EX || PIPE == 0, "exact accumulation: small-tile kernels only");
+    if constexpr (EX) {
+        if (p.gate && ((*p.gate != 0) != (p.gate_on != 0))) return;   // the other launch of this node computes it
+    }
     constexpr int NW = WM * WN;
     constexpr int MI = BM / WM / 16, NJ = BN / WN / 16;   // 16x16 tiles per wave
     constexpr int LA = BM / 8 / NW, LB = BN / 8 / NW;     // glds instructions per wave per stage

@@ -98,6 +98,10 @@ struct q2a_gemm_args {
     const float * gamma2;
     const q2a_half * wext2;
     int split_kq;                     // allow the small-tile split-K for k-quant / Q8_0 / Q4_0 weights (q2a_gemm_kq_ksplit)
+    // Q2A_BLK_EXACT kernels: when gate is set, the launch computes only if (*gate != 0) == (gate_on != 0) — a
+    // device-side choice between two launches of one node (every workgroup reads the flag and leaves otherwise)
+    const int * gate;
+    int gate_on;
     q2a_half * vtl;                   // Q2A_EPI_QKV: V^T lo image fp16(v - fp16(v)), same layout as vt (null = not written)
     int v_rows;                       // Q2A_EPI_QKV: 1 = V hi / lo row-major [M][D] into vt / vtl (like Q and K; the engine's
                                       //   reference contract), 0 = V^T [clip][head][64][TP] (bf16 contract, ggml backend)

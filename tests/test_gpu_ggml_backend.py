@@ -158,6 +158,20 @@ def test_graph_capture_dropped_when_scratch_grows(harness):
     assert info["equal"] is True
 
 
+def test_conv_one_part_gemm_gives_the_three_part_bits(harness):
+    """The conv MUL_MAT at conv2's shape (oracle/ggml_harness.cpp cmd_convgate): with every activation an fp16 value
+    the backend computes over the hi part alone; one value that is not (a GELU passthrough x >= 10) sends the node to
+    the three-part GEMM. Rows that hold only fp16 values carry the same bits under both, the one row with the odd value
+    changes, and both runs sit within f32 rounding of a double-precision dot product (error / sum |x w|)."""
+    r = subprocess.run([harness, "convgate"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:] + r.stdout[-2000:]
+    info = json.loads(r.stdout.strip().splitlines()[-1])
+    assert info["mm_conv"] == 1, info
+    assert info["other_rows_differing"] == 0, info
+    assert info["odd_row_outputs_changed"] > 1000, info
+    assert info["max_rel_fp16_inputs"] < 1e-6 and info["max_rel_with_odd_value"] < 1e-6 and info["odd_row_rel"] < 1e-6, info
+
+
 @pytest.mark.parametrize("cfg", ["tiny", "full"])
 def test_conv_hilo_path_runs_and_matches_exact_f32(harness, make_model, make_clip, golden, xbuild_bar, cfg, tmp_path):
     """the conv MUL_MAT(F32 im2col, F16 kernel) runs on the fp16 MFMA GEMM with hi/lo-split activations
