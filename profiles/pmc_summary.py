@@ -46,6 +46,33 @@ def load(path, counter):
     return per
 
 
+def resid_split(path, counter):
+    """O and fc2 share the residual-epilogue kernels: per layer the O launch comes first, then fc2's (its main rounds,
+    plus at 64 clips the 128x128 partial-round tail right after them). Dispatch order splits them: a RESID dispatch
+    that is not a 128x128 tail alternates O / fc2; a tail belongs to the fc2 launch before it. Returns the per-layer
+    KiB of each (fc2 = main + tail)."""
+    rows = []
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            m = re.search(r"k_gemm<(\d+), (\d+), (\d+), (\d+), (\d+), (\d+), (\d+)>", row.get("Kernel_Name", ""))
+            if row.get("Counter_Name") == counter and m and int(m.group(5)) == 1 and int(m.group(6)) != 2:
+                tail = int(m.group(1)) == 128 and int(m.group(2)) == 128
+                rows.append((int(row["Dispatch_Id"]), tail, float(row["Counter_Value"])))
+    rows.sort()
+    o, fc2 = [], []
+    nxt_o = True
+    for _, tail, v in rows:
+        if tail and fc2:
+            fc2[-1] += v
+        elif nxt_o:
+            o.append(v)
+            nxt_o = False
+        else:
+            fc2.append(v)
+            nxt_o = True
+    return o, fc2
+
+
 def main():
     fetch_csv, write_csv, out, source = sys.argv[1:5]
     fetch, write = load(fetch_csv, "FETCH_SIZE"), load(write_csv, "WRITE_SIZE")
@@ -67,6 +94,15 @@ def main():
         while key in res:
             key += "'"
         res[key] = e
+    of, ff = resid_split(fetch_csv, "FETCH_SIZE")
+    ow, fw = resid_split(write_csv, "WRITE_SIZE")
+    for cls, f, w in (("gemm_o", of, ow), ("gemm_fc2", ff, fw)):
+        if f and w:
+            e = {"class": cls, "kernel": "residual-epilogue kernels split by dispatch order (profiles/pmc_summary.py "
+                 "resid_split)", "dispatches": min(len(f), len(w)), "FETCH_SIZE_KiB_avg": sum(f) / len(f),
+                 "WRITE_SIZE_KiB_avg": sum(w) / len(w)}
+            e["hbm_bytes_per_launch_corrected"] = (2 * e["FETCH_SIZE_KiB_avg"] + e["WRITE_SIZE_KiB_avg"]) * 1024
+            res[cls] = e
     with open(out, "w") as fo:
         json.dump({"source": source,
                    "units": "FETCH_SIZE/WRITE_SIZE in KiB per dispatch; gfx950 correction: FETCH_SIZE x2 (16-B/lane "
