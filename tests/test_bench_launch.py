@@ -120,3 +120,30 @@ def test_roofline_objects_name_the_dominant_kernel():
     f = bench.roofline_of(8, ms, n, "q4k64", "q4_k", False, 64)
     assert f["flop_per_launch"] == 2.0 * 96000 * 5120 * 1280 and "PRE_H,256,2" in f["kernel"]
     assert bench.roofline_of(5, ms, n, "q4k64", "q4_k", False, 2)["traffic"] is None   # other batch: no counters
+
+
+def test_pmc_summary_splits_o_and_fc2_by_dispatch_order(tmp_path):
+    """CPU-only: profiles/pmc_summary.py gives O and fc2 their own traffic although they share the residual-epilogue
+    kernels — per layer O first, then fc2's main rounds and (64 clips) its 128x128 partial-round tail."""
+    sys.path.insert(0, os.path.join(ROOT, "profiles"))
+    import pmc_summary
+    main = "void (anonymous namespace)::k_gemm<256, 256, 2, 4, 1, 256, 1>(q2a_gemm_args)"
+    tail = "void (anonymous namespace)::k_gemm<128, 128, 2, 2, 1, 256, 0>(q2a_gemm_args)"
+    other = "void (anonymous namespace)::k_gemm<256, 256, 2, 4, 7, 256, 2>(q2a_gemm_args)"
+    seq = [(other, 5.0), (main, 10.0), (main, 40.0), (tail, 4.0), (other, 5.0), (main, 12.0), (main, 44.0), (tail, 6.0)]
+    paths = {}
+    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+        p = tmp_path / f"{counter}.csv"
+        with open(p, "w") as f:
+            f.write('"Dispatch_Id","Kernel_Name","Counter_Name","Counter_Value"\n')
+            for i, (k, v) in enumerate(seq):
+                f.write(f'{i + 1},"{k}","{counter}",{v}\n')
+        paths[counter] = str(p)
+    o, fc2 = pmc_summary.resid_split(paths["FETCH_SIZE"], "FETCH_SIZE")
+    assert o == [10.0, 12.0] and fc2 == [44.0, 50.0]
+    out = tmp_path / "s.json"
+    sys.argv = ["pmc_summary.py", paths["FETCH_SIZE"], paths["WRITE_SIZE"], str(out), "test"]
+    pmc_summary.main()
+    k = json.load(open(out))["kernels"]
+    assert k["gemm_o"]["hbm_bytes_per_launch_corrected"] == (2 * 11.0 + 11.0) * 1024
+    assert k["gemm_fc2"]["hbm_bytes_per_launch_corrected"] == (2 * 47.0 + 47.0) * 1024
