@@ -282,6 +282,42 @@ def committed_counter(config: str, cls: int, suffix: str, field: str):
     return None, None
 
 
+def mfma_util_of(config: str, clips: int):
+    """The metric's "MFMA util %" over a whole step, from the committed PROFILE_TAG profile set of this workload: every
+    kernel's SQ MFMA-busy fraction (SQ_VALU_MFMA_BUSY_CYCLES over its active cycles,
+    profiles/sq_summary.py) weighted by its rocprofv3 time per step, over the step time measured under rocprofv3 by the
+    same collection. Kernels without MFMA work count as 0. None when the set lacks any of the three summaries."""
+    if clips != CONFIGS[config][1]:
+        return None
+    pdir = os.path.join(ROOT, "profiles")
+    if not os.path.isdir(pdir):
+        return None
+    for tag in (PROFILE_TAG,):   # (an older set's kernel names need not match the current tree's)
+        sq_f, st_f, b_f = (f"{tag}_{config}_sq_mfma.json", f"{tag}_{config}_rocprof_kernel_stats.csv",
+                           f"{tag}_{config}_bench_under_rocprof.json")
+        if not all(os.path.exists(os.path.join(pdir, f)) for f in (sq_f, st_f, b_f)):
+            continue
+        import csv
+        with open(os.path.join(pdir, sq_f)) as f:
+            # keys "class | kernel name" (profiles/sq_summary.py)
+            busy = {k.split(" | ", 1)[-1]: e["mfma_busy_frac"] for k, e in json.load(f)["kernels"].items()
+                    if "mfma_busy_frac" in e}
+        with open(os.path.join(pdir, b_f)) as f:
+            b = json.loads(f.read().strip().splitlines()[-1])
+        with open(os.path.join(pdir, st_f)) as f:
+            rows = list(csv.DictReader(f))
+        # steps in the traced run (warm-up, timed, breakdown and dominant-class passes): one attention launch per layer
+        steps = sum(int(r["Calls"]) for r in rows if "k_attn" in r["Name"]) / 32
+        if steps <= 0:
+            continue
+        weighted = sum(busy.get(r["Name"], 0.0) * float(r["TotalDurationNs"]) for r in rows) / steps / 1e6
+        return {"value": round(weighted / b["ms_per_step"], 4), "mfma_busy_ms_per_step": round(weighted, 2),
+                "step_ms_under_rocprof": b["ms_per_step"],
+                "sources": [f"profiles/{sq_f}", f"profiles/{st_f}", f"profiles/{b_f}"],
+                "definition": "sum over kernels of SQ MFMA-busy fraction x rocprofv3 time per step, over the step time"}
+    return None
+
+
 def roofline_of(cls: int, timed_ms, timed_n, config: str, wt: str, bf16: bool, clips: int) -> dict:
     """roofline object of one class: achieved = algorithmic flops per launch / its average launch time (HIP events on
     the engine's stream over the timed region), against the dense fp16 / bf16 MFMA peak (the MFMA dtype issued, also
@@ -603,6 +639,7 @@ def main():
         "tflops_total": round(FLOP_PER_CLIP * total_clips / elapsed / 1e12, 1),
         "roofline": roofline,
         "roofline_gemm_fc1": roofline_fc1,
+        "mfma_util": mfma_util_of(args.config, clips_per_gpu),
         "cpu_baseline": cpu,
         "c_group": c_group,
         "pcie_inclusive_frames_per_s": round(pcie_rate, 1) if pcie_rate else None,

@@ -147,3 +147,17 @@ def test_pmc_summary_splits_o_and_fc2_by_dispatch_order(tmp_path):
     k = json.load(open(out))["kernels"]
     assert k["gemm_o"]["hbm_bytes_per_launch_corrected"] == (2 * 11.0 + 11.0) * 1024
     assert k["gemm_fc2"]["hbm_bytes_per_launch_corrected"] == (2 * 47.0 + 47.0) * 1024
+
+
+def test_step_mfma_util_from_the_committed_profile_set():
+    """CPU-only: the bench line's `mfma_util` (the metric's "MFMA util %" over a whole step) comes from the committed
+    PROFILE_TAG set of the workload — SQ busy per kernel x rocprofv3 time per step / step time — for the BASELINE
+    configs and the 64-clip F16 / one-clip Q4_K lines (the exact-Q8_0 q80x64 extra has no set: its line carries null)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    for config in ("q4k64", "f16x1", "q80bf16x64", "f16x64", "q4kx1"):
+        u = bench.mfma_util_of(config, bench.CONFIGS[config][1])
+        assert u is not None, config
+        assert 0.1 < u["value"] < 0.9, (config, u)
+        assert all(src.startswith(f"profiles/{bench.PROFILE_TAG}_{config}_") for src in u["sources"]), u
+    assert bench.mfma_util_of("q4k64", 3) is None   # another batch than the profiled one: no figure
