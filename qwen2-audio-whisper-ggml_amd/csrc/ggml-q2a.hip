@@ -541,7 +541,10 @@ __global__ void k_dup_rows(const _Float16 * w, _Float16 * o, int K, int P, int n
     for (int q = 0; q < P; ++q) o[(int64_t) r * P * K + q * K + k] = w[i];
 }
 // t [R][C] -> o [C][R] (f32), 64x64 tiles through LDS
-__global__ __launch_bounds__(256) void k_transpose_f32(const float * t, float * o, int R, int C) {
+// with bias (the conv's ADD of its [1][C] bias row, then GELU): o[c][r] = gelu(t[r][c] + bias[c]), the f32 ADD and
+// the table GELU of the two graph nodes (k_rows<0>, k_rows<3>) on the same values
+__global__ __launch_bounds__(256) void k_transpose_f32(const float * t, float * o, int R, int C, const float * bias,
+                                                       const uint16_t * gelu_tab) {
     __shared__ float tile[64][65];
     const int r0 = (int) blockIdx.y * 64, c0 = (int) blockIdx.x * 64;
     for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
@@ -551,7 +554,11 @@ __global__ __launch_bounds__(256) void k_transpose_f32(const float * t, float * 
     __syncthreads();
     for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
         const int cc = idx >> 6, rr = idx & 63;
-        if (r0 + rr < R && c0 + cc < C) o[(int64_t) (c0 + cc) * R + r0 + rr] = tile[rr][cc];
+        if (r0 + rr < R && c0 + cc < C) {
+            float v = tile[rr][cc];
+            if (bias) v = gelu_tab_f(v + bias[c0 + cc], gelu_tab);
+            o[(int64_t) (c0 + cc) * R + r0 + rr] = v;
+        }
     }
 }
 
@@ -1173,8 +1180,9 @@ bool conv_hilo_ok(const ggml_tensor * op) {
 int conv_parts(int K) { (void) K; return 3; }
 
 // out[n][m] = sum_k x[m][k] * w[n][k] (ggml MUL_MAT with src0 = x F32, src1 = w F16): GEMM [M][N] into the scratch,
-// then one transpose into the node's [N][M] layout
-void run_mm_conv_hilo(q2a_backend_ctx * b, ggml_tensor * op) {
+// then one transpose into the node's [N][M] layout — or, with gelu_out, into that node's: gelu(out + bias[n]) (the
+// conv's ADD(bias) and GELU nodes folded into the transpose)
+void run_mm_conv_hilo(q2a_backend_ctx * b, ggml_tensor * op, ggml_tensor * gelu_out = nullptr, const float * bias = nullptr) {
     const ggml_tensor * x = op->src[0];
     const ggml_tensor * w = op->src[1];
     const int K = (int) x->ne[0], M = (int) x->ne[1], N = (int) w->ne[1];
@@ -1228,7 +1236,8 @@ void run_mm_conv_hilo(q2a_backend_ctx * b, ggml_tensor * op) {
         Q2A_HIP(q2a_launch_gemm(a1, Q2A_EPI_STORE_F, Q2A_BLK_EXACT, b->stream));
     }
     hipLaunchKernelGGL(k_transpose_f32, dim3((unsigned) ((N + 63) / 64), (unsigned) ((M + 63) / 64)), dim3(256), 0, b->stream,
-                       (const float *) tmp, (float *) op->data, M, N);
+                       (const float *) tmp, (float *) (gelu_out ? gelu_out->data : op->data), M, N, gelu_out ? bias : nullptr,
+                       gelu_table(b->device));
 }
 
 // diagnostic (GGML_Q2A_CONV_F64=1): the conv MUL_MAT(F32 x, F16 w) summed in double, one thread per output, rounded
@@ -1953,9 +1962,37 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                 }
                 if (!mm_fast_ok(op) && conv_f64_diag(op)) { run_mm_conv_f64(b, op); b->stats.n_mul_mat_conv++; break; }
                 if (!mm_fast_ok(op) && conv_hilo_ok(op)) {
-                    run_mm_conv_hilo(b, op);
+                    // the conv graph's MUL_MAT -> RESHAPE -> ADD(bias [1][C]) -> GELU (ggml_conv_1d_ph, then
+                    // qwen2-whisper.cpp's bias add and GELU), every link its producer's sole consumer: one transpose
+                    // writes the GELU node
+                    int last = i;
+                    ggml_tensor * gout = nullptr;
+                    const float * cbias = nullptr;
+                    if (!no_fuse) {
+                        int j = i + 1;
+                        ggml_tensor * prod = op;
+                        while (node(j) && (node(j)->op == GGML_OP_RESHAPE || node(j)->op == GGML_OP_VIEW) &&
+                               node(j)->src[0] == prod && sole(prod, node(j)) && ggml_is_contiguous(node(j)) &&
+                               node(j)->data == op->data && ggml_nelements(node(j)) == n)
+                            prod = node(j++);
+                        ggml_tensor * ad = node(j), * ge = node(j + 1);
+                        const ggml_tensor * bs = ad ? ad->src[1] : nullptr;
+                        if (ad && ge && ad->op == GGML_OP_ADD && ad->src[0] == prod && sole(prod, ad) && bs &&
+                            bs->type == GGML_TYPE_F32 && ggml_is_contiguous(bs) && bs->ne[0] == 1 && bs->ne[1] == op->ne[1] &&
+                            bs->ne[2] == 1 && bs->ne[3] == 1 && ad->type == GGML_TYPE_F32 && ggml_is_contiguous(ad) &&
+                            ggml_nelements(ad) == n && ad->ne[0] == op->ne[0] && ad->ne[1] == op->ne[1] &&
+                            ge->op == GGML_OP_UNARY && ggml_get_unary_op(ge) == GGML_UNARY_OP_GELU && ge->src[0] == ad &&
+                            sole(ad, ge) && ge->type == GGML_TYPE_F32 && ggml_is_contiguous(ge) && ggml_are_same_shape(ad, ge)) {
+                            gout = ge;
+                            cbias = (const float *) bs->data;
+                            last = j + 1;
+                        }
+                    }
+                    run_mm_conv_hilo(b, op, gout, cbias);
                     b->stats.n_mul_mat_conv++;
                     b->n_mul_mat_conv_total++;
+                    if (gout) b->stats.n_fused += 2;
+                    i = last;
                     break;
                 }
                 if (!mm_fast_ok(op)) { run_mm_f32(b, op); b->stats.n_mul_mat_f32++; break; }
