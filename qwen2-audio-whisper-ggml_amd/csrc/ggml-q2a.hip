@@ -542,9 +542,10 @@ __global__ void k_dup_rows(const _Float16 * w, _Float16 * o, int K, int P, int n
 }
 // t [R][C] -> o [C][R] (f32), 64x64 tiles through LDS
 // with bias (the conv's ADD of its [1][C] bias row, then GELU): o[c][r] = gelu(t[r][c] + bias[c]), the f32 ADD and
-// the table GELU of the two graph nodes (k_rows<0>, k_rows<3>) on the same values
+// the table GELU of the two graph nodes (k_rows<0>, k_rows<3>) on the same values; with addend (an [C][R] f32 array,
+// the encoder's positional rows): o[c][r] = addend[c][r] + t[r][c], the ADD node's one f32 addition
 __global__ __launch_bounds__(256) void k_transpose_f32(const float * t, float * o, int R, int C, const float * bias,
-                                                       const uint16_t * gelu_tab) {
+                                                       const uint16_t * gelu_tab, const float * addend = nullptr) {
     __shared__ float tile[64][65];
     const int r0 = (int) blockIdx.y * 64, c0 = (int) blockIdx.x * 64;
     for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
@@ -557,6 +558,7 @@ __global__ __launch_bounds__(256) void k_transpose_f32(const float * t, float * 
         if (r0 + rr < R && c0 + cc < C) {
             float v = tile[rr][cc];
             if (bias) v = gelu_tab_f(v + bias[c0 + cc], gelu_tab);
+            if (addend) v = addend[(int64_t) (c0 + cc) * R + r0 + rr] + v;
             o[(int64_t) (c0 + cc) * R + r0 + rr] = v;
         }
     }
@@ -2141,6 +2143,40 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                 break;
             }
             case GGML_OP_CONT: case GGML_OP_DUP: case GGML_OP_CPY: {
+                // the encoder's head (qwen2-whisper.cpp:2004): CONT(TRANSPOSE(embd_conv)) read only by ADD(positional
+                // rows, ·) -> one tiled transpose writing the ADD. (The tail's PERMUTE -> CONT -> POOL_1D -> PERMUTE ->
+                // CONT is not folded: the allocator hands the pooled rows' block to the last CONT, so one pass would
+                // read rows another thread has overwritten.)
+                if (op->op == GGML_OP_CONT && !no_fuse && !vprep.count(op) && op->type == GGML_TYPE_F32 && s0 &&
+                    s0->type == GGML_TYPE_F32 && ggml_is_contiguous(op)) {
+                    const ggml_tensor * x = s0->src[0];
+                    const bool swap01 = s0->op == GGML_OP_TRANSPOSE && x && x->type == GGML_TYPE_F32 && ggml_is_contiguous(x) &&
+                                        x->ne[2] == 1 && x->ne[3] == 1 && s0->data == x->data && s0->ne[0] == x->ne[1] &&
+                                        s0->ne[1] == x->ne[0];
+                    int j = i + 1;
+                    while (node(j) && is_view_op(node(j)) && node(j)->src[0] != op) ++j;
+                    ggml_tensor * nx = node(j);
+                    if (swap01 && nx && nx->op == GGML_OP_ADD && sole(op, nx) && nx->type == GGML_TYPE_F32 &&
+                        ggml_is_contiguous(nx) && ggml_are_same_shape(nx, op)) {
+                        const ggml_tensor * pe = nx->src[0] == op ? nx->src[1] : nx->src[0];
+                        auto disjoint = [](const ggml_tensor * u, const ggml_tensor * v) {
+                            return (const char *) u->data + ggml_nbytes(u) <= (const char *) v->data ||
+                                   (const char *) v->data + ggml_nbytes(v) <= (const char *) u->data;
+                        };
+                        if (pe != op && pe->type == GGML_TYPE_F32 && ggml_are_same_shape(pe, op) && pe->nb[0] == 4 &&
+                            pe->nb[1] == (size_t) pe->ne[0] * 4 && nx->src[1] == op && disjoint(nx, x) && disjoint(nx, pe)) {
+                            // x [C rows][T] -> nx [T rows][C]: R = C, C' = T
+                            const int R = (int) x->ne[1], Cc = (int) x->ne[0];
+                            hipLaunchKernelGGL(k_transpose_f32, dim3((unsigned) ((Cc + 63) / 64), (unsigned) ((R + 63) / 64)), dim3(256), 0,
+                                               st, (const float *) x->data, (float *) nx->data, R, Cc, nullptr, nullptr,
+                                               (const float *) pe->data);
+                            b->stats.n_other++;
+                            b->stats.n_fused += 1;
+                            i = j;
+                            break;
+                        }
+                    }
+                }
                 if (vprep.count(op) && !vt_ready_for) {   // V of a fused attention: its V^T operand instead of the f32 copy
                     // (one pending at a time: a second V before the first attention is copied normally)
                     const int T = (int) op->ne[0], H = (int) op->ne[2], TP = (T + 63) / 64 * 64;
