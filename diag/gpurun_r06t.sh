@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 6: the ggml backend's encoder head (transpose + positional rows) in one kernel after the conv bias + GELU fold:
+# round 6: the ggml backend's encoder head (transpose + positional rows) and tail (pool between permutes) folded:
 # the backend suite (fused vs per-node
 # bit-identity included), then whisper_full encode times and a kernel trace
 cd /root/repo

@@ -361,6 +361,19 @@ __global__ void k_pool1d_avg(tview s, tview d, int k, int64_t n) {
     *(float *) (d.base + voff(d, i0, i1, i2, i3)) = acc;
 }
 
+// POOL_1D(AVG, k) over time of [T][C] rows, read and written in that layout: o[t][c] = (sum_k x[k t + ki][c]) / k —
+// the reference's PERMUTE -> CONT -> POOL_1D -> PERMUTE -> CONT (qwen2-whisper.cpp:2160-2172) in one pass, the same
+// f32 operations as k_pool1d_avg (acc from 0, then the division); o must not overlap x
+__global__ void k_pool_rows_avg(const float * x, float * o, int C, int k, int64_t n) {
+    const int64_t i = (int64_t) blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int64_t t = i / C, c = i - t * C;
+    float acc = 0.0f;
+    for (int ki = 0; ki < k; ++ki) acc += x[(t * k + ki) * C + c];
+    acc /= (float) k;
+    o[i] = acc;
+}
+
 // fp32 -> fp16 (RNE) of a contiguous F32 activation block (ggml_fp32_to_fp16_row, the F16 vec_dot_type); 8 per
 // thread (two 16-B loads, one 16-B store) when n % 8 == 0 and both ends are 16-B aligned
 __global__ void k_f32_to_f16(const float * x, _Float16 * y, int64_t n) {
@@ -2143,26 +2156,30 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                 break;
             }
             case GGML_OP_CONT: case GGML_OP_DUP: case GGML_OP_CPY: {
-                // the encoder's head (qwen2-whisper.cpp:2004): CONT(TRANSPOSE(embd_conv)) read only by ADD(positional
-                // rows, ·) -> one tiled transpose writing the ADD. (The tail's PERMUTE -> CONT -> POOL_1D -> PERMUTE ->
-                // CONT is not folded: the allocator hands the pooled rows' block to the last CONT, so one pass would
-                // read rows another thread has overwritten.)
+                // the encoder's head and tail (qwen2-whisper.cpp:2004, 2160-2172): CONT(TRANSPOSE(embd_conv)) read only
+                // by ADD(positional rows, ·) -> one tiled transpose writing the ADD; CONT(PERMUTE(x)) read only by
+                // POOL_1D AVG whose PERMUTE -> CONT restores x's layout -> one pass over x's rows, written into that
+                // CONT, or — when the allocator gave the CONT x's block (rows read and written by different threads
+                // must not overlap) — into the first CONT's own block and copied over
                 if (op->op == GGML_OP_CONT && !no_fuse && !vprep.count(op) && op->type == GGML_TYPE_F32 && s0 &&
                     s0->type == GGML_TYPE_F32 && ggml_is_contiguous(op)) {
                     const ggml_tensor * x = s0->src[0];
-                    const bool swap01 = s0->op == GGML_OP_TRANSPOSE && x && x->type == GGML_TYPE_F32 && ggml_is_contiguous(x) &&
-                                        x->ne[2] == 1 && x->ne[3] == 1 && s0->data == x->data && s0->ne[0] == x->ne[1] &&
-                                        s0->ne[1] == x->ne[0];
+                    const bool swap01 = (s0->op == GGML_OP_TRANSPOSE ||
+                                         (s0->op == GGML_OP_PERMUTE && ((const int32_t *) s0->op_params)[0] == 1 &&
+                                          ((const int32_t *) s0->op_params)[1] == 0 && ((const int32_t *) s0->op_params)[2] == 2 &&
+                                          ((const int32_t *) s0->op_params)[3] == 3)) &&
+                                        x && x->type == GGML_TYPE_F32 && ggml_is_contiguous(x) && x->ne[2] == 1 && x->ne[3] == 1 &&
+                                        s0->data == x->data && s0->ne[0] == x->ne[1] && s0->ne[1] == x->ne[0];
+                    auto disjoint = [](const ggml_tensor * u, const ggml_tensor * v) {
+                        return (const char *) u->data + ggml_nbytes(u) <= (const char *) v->data ||
+                               (const char *) v->data + ggml_nbytes(v) <= (const char *) u->data;
+                    };
                     int j = i + 1;
                     while (node(j) && is_view_op(node(j)) && node(j)->src[0] != op) ++j;
                     ggml_tensor * nx = node(j);
                     if (swap01 && nx && nx->op == GGML_OP_ADD && sole(op, nx) && nx->type == GGML_TYPE_F32 &&
                         ggml_is_contiguous(nx) && ggml_are_same_shape(nx, op)) {
                         const ggml_tensor * pe = nx->src[0] == op ? nx->src[1] : nx->src[0];
-                        auto disjoint = [](const ggml_tensor * u, const ggml_tensor * v) {
-                            return (const char *) u->data + ggml_nbytes(u) <= (const char *) v->data ||
-                                   (const char *) v->data + ggml_nbytes(v) <= (const char *) u->data;
-                        };
                         if (pe != op && pe->type == GGML_TYPE_F32 && ggml_are_same_shape(pe, op) && pe->nb[0] == 4 &&
                             pe->nb[1] == (size_t) pe->ne[0] * 4 && nx->src[1] == op && disjoint(nx, x) && disjoint(nx, pe)) {
                             // x [C rows][T] -> nx [T rows][C]: R = C, C' = T
@@ -2174,6 +2191,29 @@ ggml_status run_nodes(q2a_backend_ctx * b, ggml_cgraph * g) {
                             b->stats.n_fused += 1;
                             i = j;
                             break;
+                        }
+                    }
+                    if (swap01 && nx && nx->op == GGML_OP_POOL_1D && nx->src[0] == op && sole(op, nx)) {
+                        const int32_t * pp = (const int32_t *) nx->op_params;
+                        ggml_tensor * p2 = node(j + 1), * c2 = node(j + 2);
+                        if (pp[0] == GGML_OP_POOL_AVG && pp[1] == pp[2] && pp[3] == 0 && pp[1] >= 1 && nx->type == GGML_TYPE_F32 &&
+                            p2 && c2 && p2->op == GGML_OP_PERMUTE && p2->src[0] == nx && sole(nx, p2) &&
+                            ((const int32_t *) p2->op_params)[0] == 1 && ((const int32_t *) p2->op_params)[1] == 0 &&
+                            c2->op == GGML_OP_CONT && c2->src[0] == p2 && sole(p2, c2) && c2->type == GGML_TYPE_F32 &&
+                            ggml_is_contiguous(c2) && c2->ne[0] == x->ne[0] && c2->ne[1] == x->ne[1] / pp[1] &&
+                            c2->ne[2] == 1 && c2->ne[3] == 1) {
+                            const bool direct = disjoint(c2, x);
+                            if (direct || (disjoint(op, x) && disjoint(op, c2))) {
+                                const int64_t nn2 = ggml_nelements(c2);
+                                float * dst = (float *) (direct ? c2->data : op->data);
+                                hipLaunchKernelGGL(k_pool_rows_avg, grid1(nn2), dim3(256), 0, st, (const float *) x->data, dst,
+                                                   (int) x->ne[0], (int) pp[1], nn2);
+                                if (!direct) Q2A_HIP(hipMemcpyAsync(c2->data, dst, (size_t) nn2 * 4, hipMemcpyDeviceToDevice, st));
+                                b->stats.n_other++;
+                                b->stats.n_fused += 2;
+                                i = j + 2;
+                                break;
+                            }
                         }
                     }
                 }

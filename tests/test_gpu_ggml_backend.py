@@ -137,8 +137,9 @@ def test_backend_fusions_match_per_node(harness, make_model, make_clip, tmp_path
     L = 2
     # per layer: Q bias + scale, V bias, V's CONT (the Q|K|V GEMM writes V^T), O bias + residual, fc1 bias + GELU,
     # fc2 bias + residual, two LayerNorm affines, the attention output CONT;
-    # plus the final LayerNorm affine and the encoder head's positional ADD (one transpose writes it)
-    assert info_f["fused"] == 15 * L + 3, info_f
+    # plus the final LayerNorm affine, the encoder head's positional ADD (one transpose writes it) and the tail's POOL
+    # and second CONT (one pass over the rows)
+    assert info_f["fused"] == 15 * L + 5, info_f
     # the Q, K and V projections of each layer run as one GEMM writing the attention's operands (every weight type)
     assert info_f["mm_grouped"] == L, info_f
     assert info_f["other"] < info_p["other"], (info_f, info_p)
