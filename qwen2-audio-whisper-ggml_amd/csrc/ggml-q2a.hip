@@ -249,7 +249,8 @@ __global__ __launch_bounds__(256) void k_norm_row(tview a, tview d, float eps, c
     constexpr int C = V4 ? 8 : 32;           // per-lane chunks: float4s (V4) or floats
     constexpr int W = V4 ? 4 : 1;
     float v[C][W];
-    double s = 0.0;
+    // every load of the row first, then the sums (a load and its sum in one loop body compiled to a load + vmcnt(0)
+    // per chunk: serial HBM round trips)
 #pragma unroll
     for (int k = 0; k < C; ++k) {
         const int j = lane + 64 * k;
@@ -261,6 +262,11 @@ __global__ __launch_bounds__(256) void k_norm_row(tview a, tview d, float eps, c
         } else {
             v[k][0] = ok ? x[j] : 0.0f;
         }
+    }
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < C; ++k) {
+        const bool ok = (lane + 64 * k) * W < n;
         // (a float4's four terms summed first, then into the running sum: the grouping of the engine's LayerNorm,
         // q2a_exact.hip k_rownorm, so both give the same row bit for bit and the fused LN route below can use it)
         if (ok) {

@@ -190,18 +190,21 @@ __global__ __launch_bounds__(256) void k_mel_norm(const q2a_mel_args p) {
 //   mode 2 Q8_0 (x86 quantize_row_q8_0 ggml-quants.c:943-1000: d = amax/127, id = 127/amax, round-half-even).
 // One wave per row; lane l owns float4 chunks l, l+64, ... so a 256-block is one float4 per lane.
 // ------------------------------------------------------------------------------------------------
+// (the f64 steps stay on the LDS pipe: the same butterfly on DPP / permlane swaps, bit-identical, measured slower —
+// 9.9 against 9.3 ms per step for the Q4_K LayerNorms, diag/gpurun_r06y.sh — it adds VALU to a VALU-heavy kernel)
 __device__ __forceinline__ double wave_sum_d(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
     return v;
 }
 
-// NBQ > 0 (whole-row Q8_K, D = 256 NBQ): 8 rows per workgroup (512 threads); the rows' d and bsum operands are staged
-// in LDS and stored by the workgroup as whole sectors (32 B of d, 256 B of bsums per block column) — one row's 4-B d
-// and 32-B bsum pieces stored by its own wave reach HBM as partial writes (diag/bwbench.hip)
-template <int MODE, bool LN, bool HIN = false, int NBQ = 0>
-__global__ __launch_bounds__(NBQ ? 512 : 256) void k_rownorm(const float * __restrict__ X, int M, int D, const float * __restrict__ g,
-                                                 const float * __restrict__ b, q2a_half * outH, float * dy, q2a_half * aext,
-                                                 int nseg, int ld) {
+// NBQ > 0 (D = 256 NBQ, compile-time): 8 rows per workgroup (512 threads), the LayerNorm weight and bias staged in LDS
+// once per workgroup. Q8_K (MODE 1): the NBQ blocks of a row quantized together; the rows' d and bsum operands are
+// staged in LDS and stored by the workgroup as whole sectors (32 B of d, 256 B of bsums per block column) — one row's
+// 4-B d and 32-B bsum pieces stored by its own wave reach HBM as partial writes (diag/bwbench.hip)
+template <int MODE, bool LN, bool HIN, int NBQ>
+__device__ __forceinline__ void rownorm_rows(const float * __restrict__ X, int M, int D, const float * __restrict__ g,
+                                             const float * __restrict__ b, q2a_half * outH, float * dy, q2a_half * aext,
+                                             int nseg, int ld) {
     const int lane = threadIdx.x & 63;
     constexpr int RPB = NBQ ? 8 : 4;   // rows per workgroup
     const int row0 = blockIdx.x * RPB;
@@ -212,18 +215,27 @@ __global__ __launch_bounds__(NBQ ? 512 : 256) void k_rownorm(const float * __res
     const int row = min(row_raw, M - 1);   // NBQ: every wave stays for the workgroup's barrier
     const float4 * x4 = (const float4 *) (X + (int64_t) row * D);
     const int nch = D / 4;
-    constexpr int MAXC = 8;   // D <= 2048
+    constexpr int MAXC = NBQ ? NBQ : 8;   // float4 chunks per lane (D <= 2048)
     float4 v[MAXC];
+    __shared__ float4 sgb[NBQ ? 2 * 64 * NBQ : 1];   // NBQ: LayerNorm weight | bias
     float mean = 0.f, scale = 1.f;
     if (LN) {
+        // all of the row's loads first, then the sums: a load and its sum under one `c < nch` branch compiled to a
+        // load + vmcnt(0) per chunk, i.e. five serial HBM round trips per row (the summation order is unchanged)
+#pragma unroll
+        for (int u = 0; u < MAXC; ++u) {
+            const int c = lane + 64 * u;
+            if (NBQ || c < nch) v[u] = x4[c];
+        }
+        if constexpr (NBQ > 0) {   // the affine operands into LDS once per workgroup, under the rows' loads
+            for (int i = threadIdx.x; i < 2 * 64 * NBQ; i += 512)
+                sgb[i] = i < 64 * NBQ ? ((const float4 *) g)[i] : ((const float4 *) b)[i - 64 * NBQ];
+        }
         double s = 0.0;
 #pragma unroll
         for (int u = 0; u < MAXC; ++u) {
             const int c = lane + 64 * u;
-            if (c < nch) {
-                v[u] = x4[c];
-                s += (double) v[u].x + (double) v[u].y + (double) v[u].z + (double) v[u].w;
-            }
+            if (NBQ || c < nch) s += (double) v[u].x + (double) v[u].y + (double) v[u].z + (double) v[u].w;
         }
         s = wave_sum_d(s);
         mean = (float) (s / D);
@@ -231,7 +243,7 @@ __global__ __launch_bounds__(NBQ ? 512 : 256) void k_rownorm(const float * __res
 #pragma unroll
         for (int u = 0; u < MAXC; ++u) {
             const int c = lane + 64 * u;
-            if (c < nch) {
+            if (NBQ || c < nch) {
                 v[u].x = v[u].x - mean; v[u].y = v[u].y - mean; v[u].z = v[u].z - mean; v[u].w = v[u].w - mean;
                 s2 += (double) (v[u].x * v[u].x) + (double) (v[u].y * v[u].y) + (double) (v[u].z * v[u].z) +
                       (double) (v[u].w * v[u].w);
@@ -243,29 +255,32 @@ __global__ __launch_bounds__(NBQ ? 512 : 256) void k_rownorm(const float * __res
     } else if (HIN) {   // fp16 rows (e.g. the GELU output, exactly fp16-valued by the LUT)
         typedef _Float16 h4_t __attribute__((ext_vector_type(4)));
         const h4_t * xh = (const h4_t *) ((const q2a_half *) X + (int64_t) row * D);
+        h4_t h[MAXC];   // loads first (see the LN branch), then the conversions
 #pragma unroll
         for (int u = 0; u < MAXC; ++u) {
             const int c = lane + 64 * u;
-            if (c < nch) {
-                const h4_t h = xh[c];
-                v[u] = make_float4((float) h[0], (float) h[1], (float) h[2], (float) h[3]);
-            }
+            if (NBQ || c < nch) h[u] = xh[c];
+        }
+#pragma unroll
+        for (int u = 0; u < MAXC; ++u) {
+            const int c = lane + 64 * u;
+            if (NBQ || c < nch) v[u] = make_float4((float) h[u][0], (float) h[u][1], (float) h[u][2], (float) h[u][3]);
         }
     } else {
 #pragma unroll
         for (int u = 0; u < MAXC; ++u) {
             const int c = lane + 64 * u;
-            if (c < nch) v[u] = x4[c];
+            if (NBQ || c < nch) v[u] = x4[c];
         }
     }
+    if constexpr (NBQ > 0 && LN) __syncthreads();   // sgb filled
     if constexpr (MODE == 1 && NBQ > 0) {
         // whole row resident: the NBQ Q8_K blocks of the row quantized with interleaved reductions
         float4 y[NBQ];
 #pragma unroll
         for (int u = 0; u < NBQ; ++u) {
             if (LN) {
-                const int c = lane + 64 * u;
-                const float4 gg = ((const float4 *) g)[c], bb = ((const float4 *) b)[c];
+                const float4 gg = sgb[lane + 64 * u], bb = sgb[64 * NBQ + lane + 64 * u];
                 y[u].x = (v[u].x * scale) * gg.x + bb.x;
                 y[u].y = (v[u].y * scale) * gg.y + bb.y;
                 y[u].z = (v[u].z * scale) * gg.z + bb.z;
@@ -291,13 +306,14 @@ __global__ __launch_bounds__(NBQ ? 512 : 256) void k_rownorm(const float * __res
         }
         return;
     }
+    if (NBQ && row_raw >= M) return;   // (after the workgroup's barrier)
 #pragma unroll
     for (int u = 0; u < MAXC; ++u) {
         const int c = lane + 64 * u;
-        if (c >= nch) continue;
+        if (!NBQ && c >= nch) continue;
         float4 y = v[u];
         if (LN) {
-            const float4 gg = ((const float4 *) g)[c], bb = ((const float4 *) b)[c];
+            const float4 gg = NBQ ? sgb[c] : ((const float4 *) g)[c], bb = NBQ ? sgb[64 * NBQ + c] : ((const float4 *) b)[c];
             y.x = (y.x * scale) * gg.x + bb.x;
             y.y = (y.y * scale) * gg.y + bb.y;
             y.z = (y.z * scale) * gg.z + bb.z;
@@ -327,6 +343,21 @@ __global__ __launch_bounds__(NBQ ? 512 : 256) void k_rownorm(const float * __res
             quant_q80_block(y, lane, o, dy + (int64_t) bf * ld + m);
         }
     }
+}
+
+template <int MODE, bool LN, bool HIN = false>
+__global__ __launch_bounds__(256) void k_rownorm(const float * __restrict__ X, int M, int D, const float * __restrict__ g,
+                                                 const float * __restrict__ b, q2a_half * outH, float * dy, q2a_half * aext,
+                                                 int nseg, int ld) {
+    rownorm_rows<MODE, LN, HIN, 0>(X, M, D, g, b, outH, dy, aext, nseg, ld);
+}
+
+// rows of D = 1280 (the model width): compile-time row length, 8 rows per 512-thread workgroup
+template <int MODE, bool LN>
+__global__ __launch_bounds__(512) void k_rownorm5(
+    const float * __restrict__ X, int M, int D, const float * __restrict__ g, const float * __restrict__ b, q2a_half * outH,
+    float * dy, q2a_half * aext, int nseg, int ld) {
+    rownorm_rows<MODE, LN, false, 5>(X, M, D, g, b, outH, dy, aext, nseg, ld);
 }
 
 // Q8_K quantizer for fp16 rows (the fc1 GELU output), 16 lanes per 256-block: a wave quantizes four blocks at
@@ -575,13 +606,19 @@ hipError_t q2a_launch_layernorm(const q2a_ln_args & a, hipStream_t s) {
     if (a.D % 4 != 0 || a.D > 2048) return hipErrorInvalidValue;
     if (a.mode == 1 && a.D % 256) return hipErrorInvalidValue;
     if (a.mode == 2 && a.D % 32) return hipErrorInvalidValue;
-    const dim3 grid((a.M + 3) / 4), blk(256);
-    if (a.mode == 0) hipLaunchKernelGGL((k_rownorm<0, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
+    const dim3 grid((a.M + 3) / 4), blk(256), grid8((a.M + 7) / 8), blk8(512);
+    const bool d1280 = a.D == 1280;   // the model width: compile-time row length (k_rownorm NBQ = 5)
+    if (a.mode == 0 && d1280)
+        hipLaunchKernelGGL((k_rownorm5<0, true>), grid8, blk8, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
+    else if (a.mode == 4 && d1280)
+        hipLaunchKernelGGL((k_rownorm5<4, true>), grid8, blk8, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
+    else if (a.mode == 2 && d1280)
+        hipLaunchKernelGGL((k_rownorm5<2, true>), grid8, blk8, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
+    else if (a.mode == 0) hipLaunchKernelGGL((k_rownorm<0, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else if (a.mode == 3) hipLaunchKernelGGL((k_rownorm<3, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else if (a.mode == 4) hipLaunchKernelGGL((k_rownorm<4, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
-    else if (a.mode == 1 && a.D == 1280)
-        hipLaunchKernelGGL((k_rownorm<1, true, false, 5>), dim3((a.M + 7) / 8), dim3(512), 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy,
-                           a.aext, 1, a.dy_ld);
+    else if (a.mode == 1 && d1280)
+        hipLaunchKernelGGL((k_rownorm5<1, true>), grid8, blk8, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else if (a.mode == 1) hipLaunchKernelGGL((k_rownorm<1, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     else hipLaunchKernelGGL((k_rownorm<2, true>), grid, blk, 0, s, a.X, a.M, a.D, a.g, a.b, a.outH, a.dy, a.aext, 1, a.dy_ld);
     return hipGetLastError();
@@ -616,7 +653,7 @@ hipError_t q2a_launch_quant_act(const q2a_quant_args & a, hipStream_t s) {
     } else if (a.mode == 2 && a.XH) {
         hipLaunchKernelGGL((k_rownorm<2, false, true>), grid, blk, 0, s, X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext, nseg, a.dy_ld);
     } else if (a.mode == 1 && seg == 1280 && nseg == 1) {   // f32 rows of D = 1280 (attention output): 5 blocks interleaved
-        hipLaunchKernelGGL((k_rownorm<1, false, false, 5>), dim3((a.M + 7) / 8), dim3(512), 0, s, X, a.M, seg, nullptr, nullptr,
+        hipLaunchKernelGGL((k_rownorm5<1, false>), dim3((a.M + 7) / 8), dim3(512), 0, s, X, a.M, seg, nullptr, nullptr,
                            a.outH, a.dy, a.aext, 1, a.dy_ld);
     } else if (a.mode == 1) {
         hipLaunchKernelGGL((k_rownorm<1, false>), grid, blk, 0, s, X, a.M * nseg, seg, nullptr, nullptr, a.outH, a.dy, a.aext, nseg, a.dy_ld);

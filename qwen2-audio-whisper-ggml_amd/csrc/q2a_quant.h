@@ -8,6 +8,29 @@
 
 namespace {
 
+// Cross-lane steps of the Q8_K quantizers on the VALU (v_permlane32_swap / v_permlane16_swap, DPP row_ror / quad_perm)
+// instead of the LDS pipe (ds_bpermute / ds_swizzle): max and integer sums, exact in any order. A swap of x with
+// itself leaves {x, partner} or {partner, x} in the two results, so their max is lane ^ 32 (^ 16) combined with the
+// lane. LayerNorm + Q8_K 9.7 -> 9.3 ms per step at 64 clips, bit-identical (diag/gpurun_r06y.sh).
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u(uint32_t v) {
+    return (uint32_t) __builtin_amdgcn_mov_dpp((int) v, CTRL, 0xF, 0xF, false);
+}
+// row_ror:n — lane i receives lane (i - n) mod 16 of its 16-lane row; quad_perm xor 2 / xor 1
+constexpr int DPP_ROR8 = 0x128, DPP_ROR4 = 0x124, DPP_ROR12 = 0x12C, DPP_XOR2 = 0x4E, DPP_XOR1 = 0xB1;
+
+// max over the 64 lanes (exact in any order)
+__device__ __forceinline__ float wave_max_f(float x) {
+    x = fmaxf(x, __uint_as_float(dpp_u<DPP_ROR8>(__float_as_uint(x))));
+    x = fmaxf(x, __uint_as_float(dpp_u<DPP_ROR4>(__float_as_uint(x))));
+    x = fmaxf(x, __uint_as_float(dpp_u<DPP_XOR2>(__float_as_uint(x))));
+    x = fmaxf(x, __uint_as_float(dpp_u<DPP_XOR1>(__float_as_uint(x))));
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    x = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+    const auto t = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+    return fmaxf(__uint_as_float(t[0]), __uint_as_float(t[1]));
+}
+
 // The Q8_K scale comes from the signed value of the FIRST element (in row order) whose |x| is the block maximum
 // (quantize_row_q8_K_ref's strict '>' scan, :3793-3798). Found in two cheap steps instead of carrying
 // (|x|, x, index) through every reduction step: (1) a plain max of |x| over the block's lanes, (2) a ballot of
@@ -19,7 +42,8 @@ __device__ __forceinline__ float first_max_value(float amax, float local_first, 
     const int g0 = lane & ~(group_lanes - 1);
     const unsigned long long gm = group_lanes == 64 ? m : (m >> g0) & ((1ull << group_lanes) - 1);
     const int src = g0 + (gm ? __builtin_ctzll(gm) : 0);
-    const float v = __shfl(local_first, src);
+    const float v = group_lanes == 64 ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(local_first), src))
+                                      : __shfl(local_first, src);
     return gm ? v : amax;
 }
 
@@ -27,8 +51,7 @@ __device__ __forceinline__ float first_max_value(float amax, float local_first, 
 __device__ __forceinline__ void quant_q8k_block(float4 y, int lane, q2a_half * codes, float * dy_out, q2a_half * aext) {
     // max |x| and the signed value of its FIRST occurrence (strict '>' scan, :3793-3798)
     float vv[4] = {y.x, y.y, y.z, y.w};
-    float amax = fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w)));
-    for (int o = 32; o > 0; o >>= 1) amax = fmaxf(amax, __shfl_xor(amax, o));
+    const float amax = wave_max_f(fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w))));
     float lf = 0.f;
     bool has = false;
     for (int e = 3; e >= 0; --e)
@@ -47,9 +70,9 @@ __device__ __forceinline__ void quant_q8k_block(float4 y, int lane, q2a_half * c
     if (lane == 0) *dy_out = d;
     // bsums over 16 = 4 lanes, then bsum32_j = lanes 8j..8j+7
     int s = q[0] + q[1] + q[2] + q[3];
-    s += __shfl_xor(s, 1);
-    s += __shfl_xor(s, 2);
-    s += __shfl_xor(s, 4);
+    s += (int) dpp_u<DPP_XOR1>((uint32_t) s);
+    s += (int) dpp_u<DPP_XOR2>((uint32_t) s);
+    s += (int) dpp_u<DPP_ROR12>((uint32_t) s);   // + lane + 4: lanes 8j now hold lanes 8j .. 8j + 7 (others unused)
     if ((lane & 7) == 0) {
         const int j = lane >> 3;
         const int hi = (s >= 0) ? (s >> 6) : -((-s + 63) >> 6);   // floor(s / 64)
@@ -61,16 +84,7 @@ __device__ __forceinline__ void quant_q8k_block(float4 y, int lane, q2a_half * c
 
 // quantize one 256-block held by 16 lanes (16 consecutive values per lane; lane group = lane >> 4 = one row):
 // same arithmetic as quant_q8k_block, four rows per wave at once. Cross-lane steps stay inside the 16-lane group
-// (ds_swizzle xor patterns). codes: this lane's 16 codes; aext: the row's 16-half bsum operand.
-__device__ __forceinline__ int swz_xor_i(int v, int o) {
-    switch (o) {
-        case 1: return __builtin_amdgcn_ds_swizzle(v, 0x041F);
-        case 2: return __builtin_amdgcn_ds_swizzle(v, 0x081F);
-        case 4: return __builtin_amdgcn_ds_swizzle(v, 0x101F);
-        default: return __builtin_amdgcn_ds_swizzle(v, 0x201F);
-    }
-}
-__device__ __forceinline__ float swz_xor_f(float v, int o) { return __int_as_float(swz_xor_i(__float_as_int(v), o)); }
+// (DPP within the row). codes: this lane's 16 codes; aext: the row's 16-half bsum operand.
 
 // the arithmetic of quant_q8k_row16 with this lane's 16 codes stored (when st) and the block's d and this lane
 // PAIR's bsum32 (sub-block sub / 2) returned instead of stored
@@ -81,8 +95,10 @@ __device__ __forceinline__ void quant_q8k_row16c(const float (&v)[16], int sub, 
 #pragma unroll
     for (int e = 14; e >= 0; --e) lm = fabsf(v[e]) >= fabsf(lm) ? v[e] : lm;
     float amax = fabsf(lm);
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) amax = fmaxf(amax, swz_xor_f(amax, o));
+    amax = fmaxf(amax, __uint_as_float(dpp_u<DPP_ROR8>(__float_as_uint(amax))));   // max over the 16-lane row (DPP)
+    amax = fmaxf(amax, __uint_as_float(dpp_u<DPP_ROR4>(__float_as_uint(amax))));
+    amax = fmaxf(amax, __uint_as_float(dpp_u<DPP_XOR2>(__float_as_uint(amax))));
+    amax = fmaxf(amax, __uint_as_float(dpp_u<DPP_XOR1>(__float_as_uint(amax))));
     const int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
     const float mx = first_max_value(amax, lm, fabsf(lm) == amax, lane, 16);
     // codes as floats: rint(iscale x) is the reference's MIN(127, nearest_int(.)) value — the MIN never binds:
@@ -117,7 +133,7 @@ __device__ __forceinline__ void quant_q8k_row16c(const float (&v)[16], int sub, 
 #pragma unroll
     for (int e = 0; e < 16; e += 2) s2 = s2 + f2_t{q[e], q[e + 1]};
     int s = (int) (s2[0] + s2[1]);
-    s += swz_xor_i(s, 1);                                     // bsum32 of sub-block j = sub / 2
+    s += (int) dpp_u<DPP_XOR1>((uint32_t) s);                  // bsum32 of sub-block j = sub / 2
     d_out = d;
     s_out = s;
 }
@@ -145,9 +161,7 @@ __device__ __forceinline__ void quant_q8k_blocks(const float4 (&y)[NB], int lane
 #pragma unroll
     for (int u = 0; u < NB; ++u) amax[u] = fmaxf(fmaxf(fabsf(y[u].x), fabsf(y[u].y)), fmaxf(fabsf(y[u].z), fabsf(y[u].w)));
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-        for (int u = 0; u < NB; ++u) amax[u] = fmaxf(amax[u], __shfl_xor(amax[u], o));
+    for (int u = 0; u < NB; ++u) amax[u] = wave_max_f(amax[u]);
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
         const float vv[4] = {y[u].x, y[u].y, y[u].z, y[u].w};
@@ -176,9 +190,11 @@ __device__ __forceinline__ void quant_q8k_blocks(const float4 (&y)[NB], int lane
         s[u] = q[0] + q[1] + q[2] + q[3];
     }
 #pragma unroll
-    for (int o = 1; o < 8; o <<= 1)
+    for (int u = 0; u < NB; ++u) s[u] += (int) dpp_u<DPP_XOR1>((uint32_t) s[u]);
 #pragma unroll
-        for (int u = 0; u < NB; ++u) s[u] += __shfl_xor(s[u], o);
+    for (int u = 0; u < NB; ++u) s[u] += (int) dpp_u<DPP_XOR2>((uint32_t) s[u]);
+#pragma unroll
+    for (int u = 0; u < NB; ++u) s[u] += (int) dpp_u<DPP_ROR12>((uint32_t) s[u]);   // + lane + 4: lanes 8j: their 8 lanes
     if ((lane & 7) == 0) {
         const int j = lane >> 3;
 #pragma unroll
