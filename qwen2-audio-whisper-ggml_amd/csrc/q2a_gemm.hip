@@ -80,16 +80,16 @@ constexpr int ROWB = BK * 2;   // bytes per LDS row (64 halves)
 constexpr int GROUP_M = 4;   // swept 2..32 at the batched shapes (round 1): 4 best by ~1 %
 
 __device__ __forceinline__ float gelu_lut(float x, const uint16_t * tab) {
-    // ggml_vec_gelu_f32 with GGML_GELU_FP16 (ggml.c:2556-2570)
-    if (x <= -10.0f) return 0.0f;
-    if (x >= 10.0f) return x;
+    // ggml_vec_gelu_f32 with GGML_GELU_FP16 (ggml.c:2556-2570). The table read is unconditional (every fp16 bit
+    // pattern indexes the 64 Ki-entry table) and the two range branches are selects: a lookup inside the branches
+    // compiled to a load + vmcnt(0) per element, the epilogue's lookups one serial round trip each
     const _Float16 h = (_Float16) x;
     uint16_t u;
     __builtin_memcpy(&u, &h, 2);
     const uint16_t g = __ldg(tab + u);
     _Float16 gh;
     __builtin_memcpy(&gh, &g, 2);
-    return (float) gh;
+    return x <= -10.0f ? 0.0f : x >= 10.0f ? x : (float) gh;
 }
 
 // same lookup against the compact |x| <= 10 table staged in LDS, result as fp16 (it is fp16 by construction)
@@ -129,16 +129,15 @@ __device__ __forceinline__ void gelu_c16_x8(const float (&x)[8], _Float16 (&y)[8
     }
 }
 
+// (unconditional read at a clamped index + selects, like gelu_lut: inside the range branches each read waited alone)
 __device__ __forceinline__ float gelu_lut_c(float x, const uint16_t * lut) {
-    if (x <= -10.0f) return 0.0f;
-    if (x >= 10.0f) return x;
     const _Float16 h = (_Float16) x;
     uint16_t u;
     __builtin_memcpy(&u, &h, 2);
-    const uint16_t g = lut[(u & 0x7FFF) + ((u & 0x8000) ? Q2A_GELU_C_HALF : 0)];
+    const uint16_t g = lut[min((uint32_t) (u & 0x7FFF), (uint32_t) (Q2A_GELU_C_HALF - 1)) + ((u & 0x8000) ? Q2A_GELU_C_HALF : 0)];
     _Float16 gh;
     __builtin_memcpy(&gh, &g, 2);
-    return (float) gh;
+    return x <= -10.0f ? 0.0f : x >= 10.0f ? x : (float) gh;
 }
 
 // Q4_K block-ratio accumulation (every Q4_K kernel, 8-phase and small-tile, runs exactly these float operations in
