@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -134,16 +135,15 @@ __global__ void k_unary(tview a, tview d, int64_t n, float scale, const uint16_t
 // every operand's rows are f32-contiguous: one wave per row, the row index decomposed once per wave in 32 bits (the
 // generic kernels above pay six 64-bit divisions per element), float4 accesses when rows are 16-B aligned.
 // OP: 0 add, 1 mul, 2 scale, 3 GELU. Same float operations as the generic kernels.
+// (the table read unconditional, the range branches as selects: inside the branches each read waited alone)
 __device__ __forceinline__ float gelu_tab_f(float x, const uint16_t * gelu_tab) {
-    if (x <= -10.0f) return 0.0f;
-    if (x >= 10.0f) return x;
     const _Float16 h = (_Float16) x;
     uint16_t u;
     __builtin_memcpy(&u, &h, 2);
     const uint16_t g = gelu_tab[u];
     _Float16 gh;
     __builtin_memcpy(&gh, &g, 2);
-    return (float) gh;
+    return x <= -10.0f ? 0.0f : x >= 10.0f ? x : (float) gh;
 }
 
 template <int OP, bool V4>
@@ -563,24 +563,70 @@ __global__ void k_dup_rows(const _Float16 * w, _Float16 * o, int K, int P, int n
 // with bias (the conv's ADD of its [1][C] bias row, then GELU): o[c][r] = gelu(t[r][c] + bias[c]), the f32 ADD and
 // the table GELU of the two graph nodes (k_rows<0>, k_rows<3>) on the same values; with addend (an [C][R] f32 array,
 // the encoder's positional rows): o[c][r] = addend[c][r] + t[r][c], the ADD node's one f32 addition
-__global__ __launch_bounds__(256) void k_transpose_f32(const float * t, float * o, int R, int C, const float * bias,
-                                                       const uint16_t * gelu_tab, const float * addend = nullptr) {
+// (every caller's t, o, bias, table and addend are distinct buffers: the conv scratch, the node's output checked
+// disjoint from the others, weights)
+__global__ __launch_bounds__(256) void k_transpose_f32(const float * __restrict__ t, float * __restrict__ o, int R, int C,
+                                                       const float * __restrict__ bias, const uint16_t * __restrict__ gelu_tab,
+                                                       const float * __restrict__ addend = nullptr) {
     __shared__ float tile[64][65];
     const int r0 = (int) blockIdx.y * 64, c0 = (int) blockIdx.x * 64;
-    for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
-        const int rr = idx >> 6, cc = idx & 63;
-        if (r0 + rr < R && c0 + cc < C) tile[rr][cc] = t[(int64_t) (r0 + rr) * C + c0 + cc];
+    // unrolled with clamped (always valid) addresses, so each thread's 16 loads are in flight together; a load under
+    // the bounds branch waited alone
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+        const int idx = (int) threadIdx.x + 256 * it, rr = idx >> 6, cc = idx & 63;
+        tile[rr][cc] = t[(int64_t) min(r0 + rr, R - 1) * C + min(c0 + cc, C - 1)];
     }
     __syncthreads();
-    for (int idx = threadIdx.x; idx < 64 * 64; idx += 256) {
-        const int cc = idx >> 6, rr = idx & 63;
-        if (r0 + rr < R && c0 + cc < C) {
-            float v = tile[rr][cc];
-            if (bias) v = gelu_tab_f(v + bias[c0 + cc], gelu_tab);
-            if (addend) v = addend[(int64_t) (c0 + cc) * R + r0 + rr] + v;
-            o[(int64_t) (c0 + cc) * R + r0 + rr] = v;
+    // the operand mode is uniform: one unrolled loop per mode, so the loads of different elements are not split by
+    // per-element branches
+    // per-element branches (the conditional stores included: values first, then the stores). The GELU table reads are
+    // asm loads behind one wait: as plain loads the compiler moved each into the x > -10 branch with its own wait
+    auto out = [&](auto has_bias, auto has_addend) {
+        float v[16];
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int idx = (int) threadIdx.x + 256 * it, cc = idx >> 6, rr = idx & 63;
+            v[it] = tile[rr][cc];
+            if constexpr (decltype(has_bias)::value) v[it] = v[it] + bias[min(c0 + cc, C - 1)];
         }
-    }
+        if constexpr (decltype(has_bias)::value) {
+            uint32_t g[16];
+#pragma unroll
+            for (int it = 0; it < 16; ++it) {
+                const _Float16 h = (_Float16) v[it];
+                uint16_t u;
+                __builtin_memcpy(&u, &h, 2);
+                asm volatile("global_load_ushort %0, %1, off" : "=v"(g[it]) : "v"(gelu_tab + u) : "memory");
+            }
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(g[0]), "+v"(g[1]), "+v"(g[2]), "+v"(g[3]), "+v"(g[4]), "+v"(g[5]), "+v"(g[6]),
+                         "+v"(g[7]), "+v"(g[8]), "+v"(g[9]), "+v"(g[10]), "+v"(g[11]), "+v"(g[12]), "+v"(g[13]), "+v"(g[14]),
+                         "+v"(g[15]) :: "memory");
+#pragma unroll
+            for (int it = 0; it < 16; ++it) {   // gelu_tab_f's ranges (ggml_vec_gelu_f32, GGML_GELU_FP16)
+                const uint16_t gg = (uint16_t) g[it];
+                _Float16 gh;
+                __builtin_memcpy(&gh, &gg, 2);
+                v[it] = v[it] <= -10.0f ? 0.0f : v[it] >= 10.0f ? v[it] : (float) gh;
+            }
+        }
+        if constexpr (decltype(has_addend)::value) {
+#pragma unroll
+            for (int it = 0; it < 16; ++it) {
+                const int idx = (int) threadIdx.x + 256 * it, cc = idx >> 6, rr = idx & 63;
+                v[it] = addend[(int64_t) min(c0 + cc, C - 1) * R + min(r0 + rr, R - 1)] + v[it];
+            }
+        }
+#pragma unroll
+        for (int it = 0; it < 16; ++it) {
+            const int idx = (int) threadIdx.x + 256 * it, cc = idx >> 6, rr = idx & 63;
+            if (r0 + rr < R && c0 + cc < C) o[(int64_t) (c0 + cc) * R + r0 + rr] = v[it];
+        }
+    };
+    if (bias && addend) out(std::true_type{}, std::true_type{});
+    else if (bias) out(std::true_type{}, std::false_type{});
+    else if (addend) out(std::false_type{}, std::true_type{});
+    else out(std::false_type{}, std::false_type{});
 }
 
 // ------------------------------------------------------------------------------------------------
