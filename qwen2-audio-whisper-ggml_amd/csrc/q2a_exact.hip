@@ -63,11 +63,24 @@ __global__ __launch_bounds__(256) void k_mel_frames(const q2a_mel_args p) {
     const float * pcm = p.pcm + (int64_t) c * p.pcm_stride;
     const int off = i * 160;
     if (do_fft) {
-        for (int j = lane; j < NFFT; j += 64) {
-            const int x = off + j;
-            float v = 0.f;
-            if (x < n_s) v = x < 200 ? (200 - x < n ? pcm[200 - x] : 0.f) : pcm[x - 200];
-            s_in[w][j] = x < n_s ? hann[j] * v : 0.f;
+        // the frame's loads issued together at clamped (always readable) addresses, then selected: a load under the
+        // reflect / range branches waited alone, seven serial round trips per frame
+        constexpr int NT = (NFFT + 63) / 64;
+        const float * srcp = n > 0 ? pcm : hann;
+        const int imax = max(n - 1, 0);
+        float raw[NT], hw[NT];
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int j = lane + 64 * t, x = off + j;
+            const int src = x < 200 ? 200 - x : x - 200;
+            raw[t] = srcp[min(max(src, 0), imax)];
+            hw[t] = hann[min(j, NFFT - 1)];
+        }
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int j = lane + 64 * t, x = off + j;
+            const float v = (x < n_s && (x >= 200 || 200 - x < n)) ? raw[t] : 0.f;
+            if (j < NFFT) s_in[w][j] = x < n_s ? hw[t] * v : 0.f;
         }
     }
     __syncthreads();
