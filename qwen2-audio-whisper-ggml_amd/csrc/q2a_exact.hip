@@ -546,13 +546,21 @@ __global__ __launch_bounds__(256) void k_pool_ln(const q2a_pool_args p) {
     const float4 * b4 = (const float4 *) (p.X + ((int64_t) c * p.T + 2 * t + 1) * p.D);
     const int nch = p.D / 4;
     constexpr int MAXC = 8;
-    float4 v[MAXC];
+    float4 v[MAXC], bv[MAXC];
+    // the rows' loads at clamped chunk indices (always readable) before any arithmetic: under the `ch < nch` branches
+    // each chunk's loads waited alone
+#pragma unroll
+    for (int u = 0; u < MAXC; ++u) {
+        const int ch = min(lane + 64 * u, nch - 1);
+        v[u] = a4[ch];
+        bv[u] = b4[ch];
+    }
     double s = 0.0;
 #pragma unroll
     for (int u = 0; u < MAXC; ++u) {
         const int ch = lane + 64 * u;
         if (ch < nch) {
-            const float4 a = a4[ch], b = b4[ch];
+            const float4 a = v[u], b = bv[u];
             v[u].x = ((0.f + a.x) + b.x) / 2; v[u].y = ((0.f + a.y) + b.y) / 2;
             v[u].z = ((0.f + a.z) + b.z) / 2; v[u].w = ((0.f + a.w) + b.w) / 2;
             s += (double) v[u].x + (double) v[u].y + (double) v[u].z + (double) v[u].w;
@@ -573,18 +581,22 @@ __global__ __launch_bounds__(256) void k_pool_ln(const q2a_pool_args p) {
     s2 = wave_sum_d(s2);
     const float scale = 1.0f / sqrtf((float) (s2 / p.D) + 1e-5f);
     float4 * o4 = (float4 *) (p.out + ((int64_t) c * TO + t) * p.D);
+    // affine operands likewise (clamped, all in flight), then the stores
+#pragma unroll
+    for (int u = 0; u < MAXC; ++u) {
+        const int ch = min(lane + 64 * u, nch - 1);
+        const float4 gg = ((const float4 *) p.g)[ch], bb = ((const float4 *) p.b)[ch];
+        float4 y;
+        y.x = (v[u].x * scale) * gg.x + bb.x;
+        y.y = (v[u].y * scale) * gg.y + bb.y;
+        y.z = (v[u].z * scale) * gg.z + bb.z;
+        y.w = (v[u].w * scale) * gg.w + bb.w;
+        v[u] = y;
+    }
 #pragma unroll
     for (int u = 0; u < MAXC; ++u) {
         const int ch = lane + 64 * u;
-        if (ch < nch) {
-            const float4 gg = ((const float4 *) p.g)[ch], bb = ((const float4 *) p.b)[ch];
-            float4 y;
-            y.x = (v[u].x * scale) * gg.x + bb.x;
-            y.y = (v[u].y * scale) * gg.y + bb.y;
-            y.z = (v[u].z * scale) * gg.z + bb.z;
-            y.w = (v[u].w * scale) * gg.w + bb.w;
-            o4[ch] = y;
-        }
+        if (ch < nch) o4[ch] = v[u];
     }
 }
 
