@@ -218,9 +218,9 @@ def host_cpu_info() -> dict:
 
 
 # The profile set measured on the current tree; its summaries are cited ahead of older rounds' (tags do not sort
-# by date: r04y was taken after r04z, and r05w, not r05x, is the round-5 closing set). Round 6: r06o for the one-clip
-# configs; the 64-clip configs' newest summaries (r06h) sort last among theirs.
-PROFILE_TAG = "r06o"
+# by date: r04y was taken after r04z, and r05w, not r05x, is the round-5 closing set). Round 6: r06ad, the closing set
+# after the late-round load fixes (r06o before them).
+PROFILE_TAG = "r06ad"
 
 
 def _profile_files(names) -> list:
